@@ -1,0 +1,232 @@
+/*
+ * imls_gpu.h — C ABI of the MI355X-native IMLS-ICP registration path.
+ *
+ * This is the drop-in boundary for the reference's per-scan Matching → Solving loop
+ * (spirit-man/Planetary-LiDAR-Odometry, laser_odometry.cpp:478-660).  Every entry point
+ * replaces one reference interface; the citation is on each declaration.  The library
+ * (libimls_gpu.so) is hand-written HIP for gfx950; there is NO CPU fallback: every compute
+ * entry point returns IMLS_ERR_DEVICE when no MI355X is present.
+ *
+ * Conventions
+ *   - Plain C types only; no C++ exceptions cross the ABI.  Status: 0 = OK, < 0 = error class
+ *     (imls_status).  imls_last_error(ctx) returns a human-readable message.
+ *   - Point inputs are float32 with an arbitrary stride in floats, so both the reference's
+ *     48-byte pcl::PointXYZINormal AoS (xyz at float 0, normal at float 4, stride 12) and
+ *     packed SoA/AoS layouts are accepted without a host copy by the caller.
+ *   - The caller keeps ownership of every host buffer; the library copies in.
+ *   - One context per host thread: a context is NOT thread-safe (the reference matcher is
+ *     single-threaded too, laser_odometry.cpp:708).  A context owns its device buffers, its
+ *     HIP stream and its spatial index.
+ *   - 4x4 poses are row-major doubles: T[r*4 + c].
+ */
+#ifndef IMLS_GPU_H
+#define IMLS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IMLS_GPU_ABI_VERSION 1
+
+typedef enum imls_status {
+    IMLS_OK = 0,
+    IMLS_ERR_ARG = -1,          /* bad argument (null pointer, size, stride) */
+    IMLS_ERR_DEVICE = -2,       /* no MI355X / HIP runtime error */
+    IMLS_ERR_STATE = -3,        /* call order (e.g. project before set_target) */
+    IMLS_ERR_UNSUPPORTED = -4,  /* method or option not built on the GPU path */
+    IMLS_ERR_CAPACITY = -5      /* exceeds a compiled-in capacity */
+} imls_status;
+
+/* laser_odometry.matching_method.method (config.json; laser_odometry.cpp:487, 557-568) */
+typedef enum imls_match_method {
+    IMLS_MATCH_IMLS = 0,        /* "IMLS"      → IMLSICPMatcher::ProjSourcePtToSurface */
+    IMLS_MATCH_PLANE_ICP = 1    /* "plane_ICP" → plane_ICP_proj (laser_odometry.cpp:277-413) */
+} imls_match_method;
+
+/* laser_odometry.solve_method.method (config.json; laser_odometry.cpp:173-275) */
+typedef enum imls_solve_method {
+    IMLS_SOLVE_LS = 0,          /* "LS"     → SolveMotionEstimationProblemLS (solver.cpp:74-166) */
+    IMLS_SOLVE_RANSAC = 1,      /* "RANSAC" → SolveMotionEstimationProblemRANSAC (solver.cpp:222-385) */
+    IMLS_SOLVE_WEIGHTED_LS = 2  /* "Weighted LS" (solver.cpp:168-220); unit weights when used directly */
+} imls_solve_method;
+
+/* solve_method.RANSAC.final_solve_method (config.json; solver.cpp:368-384) */
+typedef enum imls_final_method {
+    IMLS_FINAL_LS = 0,
+    IMLS_FINAL_WEIGHTED_LS = 1,
+    IMLS_FINAL_DRPM = 2
+} imls_final_method;
+
+/* Per-frame outcome of imls_register_frame (laser_odometry.cpp:570-646). */
+typedef enum imls_frame_status {
+    IMLS_FRAME_MAX_ITERS = 0,   /* ran all `iterations` without meeting the convergence test */
+    IMLS_FRAME_CONVERGED = 1,   /* ‖Δt‖ < delta_dist_threshold && angle(Δ) < delta_angle_threshold */
+    IMLS_FRAME_TOO_FEW = 2,     /* correspondences < correspond_number → break, pose kept */
+    IMLS_FRAME_SOLVE_FAILED = 3 /* solver returned false → break, pose kept */
+} imls_frame_status;
+
+/* Reject counters, same categories and order as ProjSourcePtToSurface
+ * (imls_icp.cpp:506-511, printed at 736-744). */
+enum {
+    IMLS_REJ_NO_NORMAL = 0,
+    IMLS_REJ_TOO_FAR = 1,
+    IMLS_REJ_INVALID_NORMAL = 2,
+    IMLS_REJ_NORMAL_CONSTRAINT = 3,
+    IMLS_REJ_MLS_FAIL = 4,
+    IMLS_REJ_NAN_INF_HEIGHT = 5,
+    IMLS_NUM_REJ = 6
+};
+
+/*
+ * All parameters of the path.  Field names follow the config.json key paths of the
+ * reference (laser_odometry.*), read at laser_odometry.cpp:487-518, 570, 606, 640-641 and
+ * 183-243.  imls_default_params() fills the values of the reference's shipped config.json.
+ */
+typedef struct imls_params {
+    /* laser_odometry.matching_method */
+    int32_t matching_method;          /* imls_match_method */
+    int32_t correspond_number;        /* matching_method.correspond_number (6) */
+
+    /* laser_odometry.matching_method.IMLS  (IMLSICPMatcher members, imls_icp.h:114-146) */
+    double h;                         /* IMLS.h: NN-1 rejection radius (imls_icp.cpp:620) */
+    double r;                         /* IMLS.r: kNN search radius (imls_icp.cpp:607, 375) */
+    int32_t get_normals;              /* IMLS.get_normals.enabled */
+    int32_t search_number_normal;     /* IMLS.get_normals.search_number_normal */
+    double r_normal;                  /* IMLS.get_normals.r_normal */
+    int32_t use_projected_distance;   /* IMLS.use_projected_distance.enabled */
+    int32_t normal_angle_constraint;  /* IMLS.normal_angle_constraint.enabled */
+    double r_proj;                    /* IMLS.use_projected_distance.r_proj */
+    double angle_diff_threshold;      /* IMLS.normal_angle_constraint.angle_diff_threshold (deg) */
+    int32_t search_number;            /* IMLS."IMLS function".search_number (K, ≤ 32) */
+    int32_t use_tensor_voting;        /* IMLS.use_tensor_voting.enabled (not on the GPU path) */
+    int32_t tensor_k;
+    int32_t recompute_normal_count_mode; /* SURVEY Q1 switch: 0 = reference (libnabo knn() return
+                                            value is a statistic → recompute path rejects), 1 = count */
+    double tensor_sigma;
+    double tensor_distance_threshold;
+
+    /* laser_odometry.matching_method.plane_ICP (laser_odometry.cpp:295-299) */
+    double picp_r;
+    double picp_r_proj;
+    double picp_angle_diff_threshold;
+    int32_t picp_use_projected_distance;
+    int32_t picp_normal_angle_constraint;
+
+    /* laser_odometry.solve_method */
+    int32_t solve_method;             /* imls_solve_method */
+    int32_t iterations;               /* solve_method.iterations (30) */
+    double delta_dist_threshold;      /* solve_method.delta_dist_threshold (1e-3 m) */
+    double delta_angle_threshold;     /* solve_method.delta_angle_threshold (rad) */
+    double ls_threshold;              /* solve_method.LS.threshold (0.02) */
+
+    /* laser_odometry.solve_method.RANSAC (solver.cpp:222-385) */
+    int32_t ransac_max_iterations;
+    int32_t ransac_final_method;      /* imls_final_method */
+    double ransac_distance_threshold;
+    double ransac_min_inliers_percentage;
+    double ransac_huber_threshold;
+    double ransac_ls_threshold;
+    double drpm_threshold;
+    double drpm_stdev_points;
+    double drpm_stdev_normals;
+    uint32_t ransac_seed;             /* glibc rand() seed; 1 = the reference's unseeded process */
+
+    /* laser_odometry */
+    int32_t transform_normal;         /* laser_odometry.transform_normal (laser_odometry.cpp:541-548) */
+    int32_t max_queue_size;           /* laser_odometry.max_queue_size (map FIFO length) */
+    int32_t _reserved[4];
+} imls_params;
+
+/* Per-iteration record of imls_register_frame (the reference writes the same quantities to
+ * imls_iter_results.txt and stdout: laser_odometry.cpp:579, 625; imls_icp.cpp:736-744). */
+typedef struct imls_iter_trace {
+    double delta[16];                 /* Δ of this iteration */
+    double pose[16];                  /* rPose after `rPose = Δ·rPose` (laser_odometry.cpp:619) */
+    uint64_t reject[IMLS_NUM_REJ];
+    uint64_t n_valid;                 /* correspondences ("USED POINTS FINAL") */
+    uint64_t n_kept;                  /* rows kept by the trimmed LS (LS path only) */
+} imls_iter_trace;
+
+typedef struct imls_ctx imls_ctx;
+
+/* ---- lifecycle ------------------------------------------------------------------------- */
+int imls_abi_version(void);
+void imls_default_params(imls_params* p);
+/* Replaces `IMLSICPMatcher matcher;` + setParameters (laser_odometry.cpp:489, 514-518;
+ * imls_icp.cpp:9-30, 146-168).  Returns NULL on failure (no device). */
+imls_ctx* imls_create(int device, const imls_params* p);
+void imls_destroy(imls_ctx* ctx);
+/* Replaces IMLSICPMatcher::setParameters (imls_icp.h:62-66). */
+int imls_set_params(imls_ctx* ctx, const imls_params* p);
+const char* imls_last_error(const imls_ctx* ctx);
+/* Run every launch of the context on `stream` (a hipStream_t); NULL restores the context's own. */
+int imls_set_stream(imls_ctx* ctx, void* hip_stream);
+int imls_synchronize(imls_ctx* ctx);
+
+/* ---- clouds ---------------------------------------------------------------------------- */
+/* Replaces IMLSICPMatcher::setTargetPointCloud (imls_icp.cpp:80-103): drops points with
+ * non-finite xyz (RemoveNANandINFData, imls_icp.cpp:58-72), keeps order, builds the index.
+ * xyz/nrm: host float pointers, element i at xyz + i*stride_floats (nrm likewise).
+ * n_kept (nullable) receives the number of points after the NaN filter. */
+int imls_set_target(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n,
+                    size_t stride_floats, size_t* n_kept);
+/* Replaces IMLSICPMatcher::setSourcePointCloud (imls_icp.cpp:74-78). kept_index (nullable,
+ * capacity n) receives the input index of every kept point, in order. */
+int imls_set_source(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n,
+                    size_t stride_floats, size_t* n_kept, uint32_t* kept_index);
+/* Same, for clouds already resident in device memory as SoA float32[6][n]
+ * (x[], y[], z[], nx[], ny[], nz[]) — inputs stay in HBM, no PCIe in the hot loop. */
+int imls_set_target_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
+int imls_set_source_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
+
+/* ---- matching -------------------------------------------------------------------------- */
+/* Replaces IMLSICPMatcher::ProjSourcePtToSurface (imls_icp.cpp:496-745) applied to the source
+ * transformed by `pose` (laser_odometry.cpp:527-549).  Outputs (each nullable, capacity =
+ * n_kept source points, float32 xyz triples) are compacted in SOURCE ORDER like the
+ * reference's erase-based loop: x_out = transformed source point (in_cloud after the call),
+ * y_out = its projection on the implicit surface, n_out = the NN-1 map normal (out_cloud);
+ * src_index_out = index into the kept source cloud.  reject[6] in imls_icp.cpp:506-511 order. */
+int imls_project(imls_ctx* ctx, const double pose[16], float* x_out, float* y_out, float* n_out,
+                 uint32_t* src_index_out, size_t* n_valid, uint64_t reject[IMLS_NUM_REJ]);
+
+/* ---- solving --------------------------------------------------------------------------- */
+/* Replaces solveMotionEstimationProblem(solve_method, ...) (laser_odometry.cpp:173-275) on the
+ * device-resident correspondences of the last imls_project.  *ok mirrors the bool return. */
+int imls_solve(imls_ctx* ctx, double delta_out[16], int* ok);
+/* Replaces SolveMotionEstimationProblemLS / WeightedLS (solver.cpp:74-220) on host arrays of
+ * N double triples (s = source, d = target, n = target normal; weights nullable = unit). */
+int imls_solve_correspondences(imls_ctx* ctx, int32_t method, const double* s, const double* d,
+                               const double* n, const double* weights, size_t N,
+                               double delta_out[16], int* ok);
+
+/* ---- fused registration ---------------------------------------------------------------- */
+/* The device-resident equivalent of laser_odometry.cpp:478-660 for one frame: rPose = I, then
+ * up to `iterations` × {transform, match, gate, solve, rPose = Δ·rPose, convergence test}, one
+ * host synchronisation at the end.  trace (nullable) receives `iterations` records; only the
+ * first *iters_run are meaningful. */
+int imls_register_frame(imls_ctx* ctx, double pose_out[16], int* iters_run, int* status,
+                        imls_iter_trace* trace);
+/* Asynchronous form: enqueue on the context stream and return; collect with
+ * imls_register_frame_result (which synchronises the stream). */
+int imls_register_frame_async(imls_ctx* ctx);
+int imls_register_frame_result(imls_ctx* ctx, double pose_out[16], int* iters_run, int* status,
+                               imls_iter_trace* trace);
+
+/* ---- instrumentation ------------------------------------------------------------------- */
+/* When enabled, HIP events bracket every launch of the projection kernel (on the stream it is
+ * launched on); imls_kernel_timing returns the accumulated milliseconds and launch count since
+ * the last reset.  kernel: 0 = projection, 1 = index build (all its kernels), 2 = solve chain. */
+int imls_enable_timing(imls_ctx* ctx, int enable);
+int imls_kernel_timing(imls_ctx* ctx, int kernel, double* total_ms, uint64_t* launches);
+int imls_reset_timing(imls_ctx* ctx);
+/* Sizes of the last built index (for roofline accounting): points, leaves, tree levels,
+ * total neighbours visited in the last projection (Σ k_q), queries passing the NN/angle gates. */
+int imls_index_stats(imls_ctx* ctx, uint64_t out[8]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IMLS_GPU_H */

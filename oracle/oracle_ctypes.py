@@ -1,0 +1,132 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle_imls.so).  TEST INFRASTRUCTURE ONLY.
+
+Importable only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+Parity status: unpinned (see imls_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import pathlib
+import sys
+
+import numpy as np
+
+ORACLE_DIR = pathlib.Path(__file__).resolve().parent
+LIB = ORACLE_DIR / "liboracle_imls.so"
+
+
+def _abi():
+    # the params struct lives in the product package's ABI mirror (shared header layout)
+    root = ORACLE_DIR.parent
+    if str(root) not in sys.path:
+        sys.path.insert(0, str(root))
+    import plo_amd  # noqa: E402
+    return plo_amd.load()._abi
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            raise RuntimeError(f"oracle not built: {LIB} (make -C oracle)")
+        L = C.CDLL(str(LIB))
+        abi = _abi()
+        P, VP, SZ = C.POINTER, C.c_void_p, C.c_size_t
+        L.oracle_knn.argtypes = [VP, SZ, VP, SZ, C.c_int, C.c_double, C.c_int, VP, VP]
+        L.oracle_project.argtypes = [VP, SZ, VP, SZ, VP, P(abi.ImlsParams), VP, VP, VP, VP, P(SZ), VP]
+        L.oracle_solve.argtypes = [C.c_int32, VP, VP, VP, VP, SZ, P(abi.ImlsParams), VP, VP, P(C.c_int)]
+        L.oracle_register_frame.argtypes = [VP, SZ, VP, SZ, P(abi.ImlsParams), VP, P(C.c_int), P(C.c_int), VP,
+                                            C.c_int, VP, P(SZ), P(C.c_double), P(C.c_double)]
+        L.oracle_rand_seed.argtypes = [VP, C.c_uint32]
+        L.oracle_rand_next.argtypes = [VP]
+        L.oracle_rand_next.restype = C.c_int32
+        L.oracle_colpiv_qr_solve.argtypes = [VP, C.c_int, C.c_int, VP, VP]
+        L.oracle_delta_from_x.argtypes = [VP, VP]
+        L.oracle_sym_eig6.argtypes = [VP, VP, VP]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _soa6(a) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    assert a.ndim == 2 and a.shape[0] == 6
+    return a
+
+
+def knn(tgt6, q3, K, r, allow_self):
+    tgt6 = _soa6(tgt6)
+    q3 = np.ascontiguousarray(q3, dtype=np.float32)
+    Q = q3.shape[1]
+    d2 = np.zeros((Q, K)); idx = np.zeros((Q, K), dtype=np.int32)
+    rc = lib().oracle_knn(_ptr(tgt6), tgt6.shape[1], _ptr(q3), Q, K, r, int(allow_self), _ptr(d2), _ptr(idx))
+    assert rc == 0
+    return d2, idx
+
+
+def project(src6, tgt6, pose, params):
+    src6, tgt6 = _soa6(src6), _soa6(tgt6)
+    N = src6.shape[1]
+    pose = np.ascontiguousarray(pose, dtype=np.float64).reshape(16)
+    x = np.zeros((N, 3), np.float32); y = np.zeros((N, 3), np.float32); n = np.zeros((N, 3), np.float32)
+    idx = np.zeros(N, np.uint32); rej = np.zeros(6, np.uint64); nv = C.c_size_t()
+    rc = lib().oracle_project(_ptr(src6), N, _ptr(tgt6), tgt6.shape[1], _ptr(pose), C.byref(params),
+                              _ptr(x), _ptr(y), _ptr(n), _ptr(idx), C.byref(nv), _ptr(rej))
+    assert rc == 0
+    k = nv.value
+    return x[:k], y[:k], n[:k], idx[:k], rej
+
+
+def solve(method, s, d, n, params, weights=None, rand_state=None):
+    s, d, n = (np.ascontiguousarray(a, dtype=np.float64).reshape(-1, 3) for a in (s, d, n))
+    w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)
+    D = np.zeros(16); ok = C.c_int()
+    rc = lib().oracle_solve(method, _ptr(s), _ptr(d), _ptr(n), None if w is None else _ptr(w), len(s),
+                            C.byref(params), None if rand_state is None else _ptr(rand_state), _ptr(D), C.byref(ok))
+    assert rc == 0
+    return bool(ok.value), D.reshape(4, 4)
+
+
+def register_frame(src6, tgt6, params, corr_iter=-1):
+    src6, tgt6 = _soa6(src6), _soa6(tgt6)
+    abi = _abi()
+    it = params.iterations
+    trace = (abi.ImlsIterTrace * max(it, 1))()
+    pose = np.zeros(16); iters = C.c_int(); status = C.c_int()
+    N = src6.shape[1]
+    corr = np.zeros((N, 9), np.float32) if corr_iter >= 0 else None
+    cn = C.c_size_t(); ti = C.c_double(); tt = C.c_double()
+    rc = lib().oracle_register_frame(_ptr(src6), N, _ptr(tgt6), tgt6.shape[1], C.byref(params), _ptr(pose),
+                                     C.byref(iters), C.byref(status), trace, corr_iter,
+                                     None if corr is None else _ptr(corr), C.byref(cn), C.byref(ti), C.byref(tt))
+    assert rc == 0
+    out = dict(pose=pose.reshape(4, 4), iters=iters.value, status=status.value,
+               trace=[trace[k] for k in range(iters.value)], seconds_index=ti.value, seconds_total=tt.value)
+    if corr is not None:
+        out["corr"] = corr[:cn.value]
+    return out
+
+
+def rand_sequence(seed, n):
+    st = np.zeros(34, np.int32)
+    lib().oracle_rand_seed(_ptr(st), seed)
+    return np.array([lib().oracle_rand_next(_ptr(st)) for _ in range(n)], dtype=np.int64)
+
+
+def colpiv_qr_solve(A, b):
+    A = np.ascontiguousarray(A, dtype=np.float64); b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(A.shape[1])
+    lib().oracle_colpiv_qr_solve(_ptr(A), A.shape[0], A.shape[1], _ptr(b), _ptr(x))
+    return x
+
+
+def delta_from_x(x):
+    x = np.ascontiguousarray(x, dtype=np.float64); D = np.zeros(16)
+    lib().oracle_delta_from_x(_ptr(x), _ptr(D))
+    return D.reshape(4, 4)

@@ -1,0 +1,154 @@
+"""ctypes mirror of include/imls_gpu.h (the C ABI) — structures, enums and library loading.
+
+The product library is ``csrc/libimls_gpu.so`` (hand-written HIP for gfx950).  There is no CPU
+fallback: `load_library()` raises if the library is missing, and every compute entry point of
+the library returns IMLS_ERR_DEVICE when no MI355X is visible.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "csrc" / "libimls_gpu.so"
+
+IMLS_OK, IMLS_ERR_ARG, IMLS_ERR_DEVICE, IMLS_ERR_STATE, IMLS_ERR_UNSUPPORTED, IMLS_ERR_CAPACITY = 0, -1, -2, -3, -4, -5
+IMLS_MATCH_IMLS, IMLS_MATCH_PLANE_ICP = 0, 1
+IMLS_SOLVE_LS, IMLS_SOLVE_RANSAC, IMLS_SOLVE_WEIGHTED_LS = 0, 1, 2
+IMLS_FINAL_LS, IMLS_FINAL_WEIGHTED_LS, IMLS_FINAL_DRPM = 0, 1, 2
+IMLS_FRAME_MAX_ITERS, IMLS_FRAME_CONVERGED, IMLS_FRAME_TOO_FEW, IMLS_FRAME_SOLVE_FAILED = 0, 1, 2, 3
+REJECT_NAMES = ("no_normal", "too_far", "invalid_normal", "normal_constraint", "mls_fail", "nan_inf_height")
+IMLS_NUM_REJ = 6
+
+STATUS_NAMES = {0: "IMLS_OK", -1: "IMLS_ERR_ARG", -2: "IMLS_ERR_DEVICE", -3: "IMLS_ERR_STATE",
+                -4: "IMLS_ERR_UNSUPPORTED", -5: "IMLS_ERR_CAPACITY"}
+
+_i32, _u32, _f64 = C.c_int32, C.c_uint32, C.c_double
+
+
+class ImlsParams(C.Structure):
+    """Field-for-field mirror of `imls_params` (include/imls_gpu.h)."""
+    _fields_ = [
+        ("matching_method", _i32), ("correspond_number", _i32),
+        ("h", _f64), ("r", _f64),
+        ("get_normals", _i32), ("search_number_normal", _i32),
+        ("r_normal", _f64),
+        ("use_projected_distance", _i32), ("normal_angle_constraint", _i32),
+        ("r_proj", _f64), ("angle_diff_threshold", _f64),
+        ("search_number", _i32), ("use_tensor_voting", _i32), ("tensor_k", _i32),
+        ("recompute_normal_count_mode", _i32),
+        ("tensor_sigma", _f64), ("tensor_distance_threshold", _f64),
+        ("picp_r", _f64), ("picp_r_proj", _f64), ("picp_angle_diff_threshold", _f64),
+        ("picp_use_projected_distance", _i32), ("picp_normal_angle_constraint", _i32),
+        ("solve_method", _i32), ("iterations", _i32),
+        ("delta_dist_threshold", _f64), ("delta_angle_threshold", _f64), ("ls_threshold", _f64),
+        ("ransac_max_iterations", _i32), ("ransac_final_method", _i32),
+        ("ransac_distance_threshold", _f64), ("ransac_min_inliers_percentage", _f64),
+        ("ransac_huber_threshold", _f64), ("ransac_ls_threshold", _f64),
+        ("drpm_threshold", _f64), ("drpm_stdev_points", _f64), ("drpm_stdev_normals", _f64),
+        ("ransac_seed", _u32),
+        ("transform_normal", _i32), ("max_queue_size", _i32),
+        ("_reserved", _i32 * 4),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
+
+
+class ImlsIterTrace(C.Structure):
+    _fields_ = [("delta", _f64 * 16), ("pose", _f64 * 16), ("reject", C.c_uint64 * IMLS_NUM_REJ),
+                ("n_valid", C.c_uint64), ("n_kept", C.c_uint64)]
+
+
+def default_params() -> ImlsParams:
+    """The reference's shipped config.json values (laser_odometry section), matching
+    imls_default_params() in the library; computed here too so CPU-only code needs no GPU."""
+    p = ImlsParams()
+    p.matching_method = IMLS_MATCH_IMLS
+    p.correspond_number = 6
+    p.h, p.r = 1.0, 3.0
+    p.get_normals, p.search_number_normal, p.r_normal = 1, 10, 1.0
+    p.use_projected_distance, p.r_proj = 0, 0.8
+    p.normal_angle_constraint, p.angle_diff_threshold = 1, 30.0
+    p.search_number = 20
+    p.use_tensor_voting, p.tensor_k, p.tensor_sigma, p.tensor_distance_threshold = 0, 50, 0.2, 0.6
+    p.recompute_normal_count_mode = 0
+    p.picp_r, p.picp_r_proj, p.picp_angle_diff_threshold = 1.5, 0.8, 30.0
+    p.picp_use_projected_distance, p.picp_normal_angle_constraint = 0, 1
+    p.solve_method = IMLS_SOLVE_RANSAC
+    p.iterations = 30
+    p.delta_dist_threshold, p.delta_angle_threshold = 0.001, 0.0001745353
+    p.ls_threshold = 0.02
+    p.ransac_max_iterations, p.ransac_final_method = 5000, IMLS_FINAL_DRPM
+    p.ransac_distance_threshold, p.ransac_min_inliers_percentage = 0.8, 0.95
+    p.ransac_huber_threshold, p.ransac_ls_threshold = 0.648, 0.02
+    p.drpm_threshold, p.drpm_stdev_points, p.drpm_stdev_normals = 0.05, 0.02, 0.05
+    p.ransac_seed = 1
+    p.transform_normal, p.max_queue_size = 0, 1
+    return p
+
+
+def _bind(lib: C.CDLL) -> C.CDLL:
+    P, VP, SZ = C.POINTER, C.c_void_p, C.c_size_t
+    sig = {
+        "imls_abi_version": (C.c_int, []),
+        "imls_default_params": (None, [P(ImlsParams)]),
+        "imls_create": (VP, [C.c_int, P(ImlsParams)]),
+        "imls_destroy": (None, [VP]),
+        "imls_set_params": (C.c_int, [VP, P(ImlsParams)]),
+        "imls_last_error": (C.c_char_p, [VP]),
+        "imls_set_stream": (C.c_int, [VP, VP]),
+        "imls_synchronize": (C.c_int, [VP]),
+        "imls_set_target": (C.c_int, [VP, VP, VP, SZ, SZ, P(SZ)]),
+        "imls_set_source": (C.c_int, [VP, VP, VP, SZ, SZ, P(SZ), VP]),
+        "imls_set_target_device": (C.c_int, [VP, VP, SZ, P(SZ)]),
+        "imls_set_source_device": (C.c_int, [VP, VP, SZ, P(SZ)]),
+        "imls_project": (C.c_int, [VP, VP, VP, VP, VP, VP, P(SZ), VP]),
+        "imls_solve": (C.c_int, [VP, VP, P(C.c_int)]),
+        "imls_solve_correspondences": (C.c_int, [VP, C.c_int32, VP, VP, VP, VP, SZ, VP, P(C.c_int)]),
+        "imls_register_frame": (C.c_int, [VP, VP, P(C.c_int), P(C.c_int), VP]),
+        "imls_register_frame_async": (C.c_int, [VP]),
+        "imls_register_frame_result": (C.c_int, [VP, VP, P(C.c_int), P(C.c_int), VP]),
+        "imls_enable_timing": (C.c_int, [VP, C.c_int]),
+        "imls_kernel_timing": (C.c_int, [VP, C.c_int, P(C.c_double), P(C.c_uint64)]),
+        "imls_reset_timing": (C.c_int, [VP]),
+        "imls_index_stats": (C.c_int, [VP, VP]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+ABI_SYMBOLS = (
+    "imls_abi_version", "imls_default_params", "imls_create", "imls_destroy", "imls_set_params",
+    "imls_last_error", "imls_set_stream", "imls_synchronize", "imls_set_target", "imls_set_source",
+    "imls_set_target_device", "imls_set_source_device", "imls_project", "imls_solve",
+    "imls_solve_correspondences", "imls_register_frame", "imls_register_frame_async",
+    "imls_register_frame_result", "imls_enable_timing", "imls_kernel_timing", "imls_reset_timing",
+    "imls_index_stats",
+)
+
+_LIB = None
+
+
+def load_library(path: os.PathLike | None = None) -> C.CDLL:
+    """Load libimls_gpu.so.  Raises (never falls back) when it is missing."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = pathlib.Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(f"HIP extension missing: {p} (run __graft_entry__.build())")
+    lib = _bind(C.CDLL(str(p)))
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+class ImlsError(RuntimeError):
+    def __init__(self, status: int, msg: str = ""):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
