@@ -1,0 +1,219 @@
+"""Benchmark: IMLS-ICP scan-pairs/s on BASELINE config B.
+
+Workload (one "step" = one scan-pair registration, inputs already resident in HBM):
+  synthetic HDL-64 scan (~126k points, all used as queries) vs a 10-scan local map (~1.26M
+  points); index build (NaN filter, Morton sort, tree) + 20 ICP iterations (fixed: delta
+  thresholds −1), each = fused transform/kNN/IMLS projection + trimmed-LS solve + pose update,
+  all on device, one host sync per pair.  LS, t = 0.02; shipped IMLS parameters (h=1, r=3, K=20,
+  30° normal gate).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
+GPU, each registers its own independent pairs (weak scaling); the only exchange is
+one RCCL all-gather of the relative poses for trajectory chaining; max-over-ranks timing.
+
+Prints ONE JSON line (rank 0).  Progress goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+import plo_amd  # noqa: E402
+
+plo_amd.load()
+from planetary_lidar_odometry_amd import config, imls_icp, sequences, synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E nominal (MI355X_MICROARCH.md chip table)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def soa_tensor(cloud, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(synth.soa(cloud))).to(dev).contiguous()
+
+
+def algorithmic_bytes_per_launch(stats: dict, trace, iters: int) -> float:
+    """B_q = 24 (query xyz+n) + 24·[NN found] + 24·k_q + 40·[valid], summed over
+    the queries of one projection launch (k_q from the kernel's own counts)."""
+    n_valid = float(np.mean([t.n_valid for t in trace])) if trace else 0.0
+    return 24.0 * stats["queries"] + 24.0 * stats["nn_found"] / iters + 24.0 * stats["sum_kq"] / iters + 40.0 * n_valid
+
+
+def cpu_baseline(pair, iters_full: int, sample_iters: int = 2):
+    """The oracle (C++ restatement, -O3, 1 thread) on the same pair: index build + `sample_iters`
+    ICP iterations, extrapolated to `iters_full` iterations."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_ctypes as oc
+    p = config.bench_params(sample_iters)
+    r = oc.register_frame(synth.soa(pair.source), synth.soa(pair.target), p)
+    t_idx = r["seconds_index"]
+    t_iter = (r["seconds_total"] - t_idx) / max(r["iters"], 1)
+    t_pair = t_idx + iters_full * t_iter
+    return dict(value=1.0 / t_pair, unit="scan-pairs/s", cores=1, kind="port",
+                sample=f"full pair ({pair.source.size} queries vs {pair.target.size}-pt map): index build "
+                       f"{t_idx:.2f} s + {r['iters']} of {iters_full} ICP iterations at {t_iter:.2f} s each, "
+                       f"extrapolated to {iters_full}; oracle/imls_oracle.cpp -O3, 1 thread",
+                seconds_per_pair=t_pair)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--queries", type=int, default=0, help="0 = all source points; else FPS subsample")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    t0 = time.time()
+    pair = synth.make_pair("hdl64", map_scans=10, scene_seed=rank, traj_seed=2000 + rank, noise_seed=1000 + 97 * rank)
+    src = pair.source if args.queries <= 0 else synth.fps_subsample(pair.source, args.queries, seed=rank)
+    log(f"[rank {rank}] pair generated in {time.time() - t0:.1f}s: {src.size} queries, map {pair.target.size}")
+    s_dev = soa_tensor(src, dev)
+    t_dev = soa_tensor(pair.target, dev)
+    torch.cuda.synchronize()
+
+    p = config.bench_params(args.iters)
+    ctx = imls_icp.ImlsContext(p, device=local)
+
+    def step():
+        ctx.set_target_device(t_dev.data_ptr(), pair.target.size)
+        ctx.set_source_device(s_dev.data_ptr(), src.size)
+        return ctx.register_frame()
+
+    for _ in range(args.warmup):
+        res = step()
+    err = np.linalg.norm(res["pose"][:3, 3] - pair.true_pose[:3, 3])
+    log(f"[rank {rank}] warmup done; pose error vs truth {err * 100:.2f} cm")
+
+    ctx.enable_timing(True)
+    ctx.reset_timing()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    poses = []
+    for _ in range(args.steps):
+        res = step()
+        poses.append(res["pose"])
+    if world > 1:
+        n_units = world * args.steps
+        allp = sequences.gather_relative_poses(np.array(poses), n_units)   # the one RCCL exchange
+        traj = sequences.chain_trajectory(allp)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        elapsed = float(tt.item())
+    ctx.enable_timing(False)
+
+    proj_ms, proj_n = ctx.kernel_timing(0)
+    idx_ms, idx_n = ctx.kernel_timing(1)
+    sol_ms, sol_n = ctx.kernel_timing(2)
+    stats = ctx.index_stats()
+    bytes_launch = algorithmic_bytes_per_launch(stats, res["trace"], args.iters)
+    avg_proj_s = proj_ms / max(proj_n, 1) / 1e3
+    achieved = bytes_launch / avg_proj_s / 1e9 if avg_proj_s > 0 else 0.0
+
+    if rank != 0:
+        ctx.close()
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    traffic = None
+    tj = pathlib.Path(args.traffic_json)
+    if tj.exists():
+        try:
+            tdat = json.loads(tj.read_text())
+            if tdat.get("queries") == stats["queries"] and tdat.get("iters") == args.iters:
+                traffic = tdat.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        log("[rank 0] CPU baseline (oracle, 1 thread) ...")
+        cpu = cpu_baseline(synth.Pair(src, pair.target, pair.true_pose, pair.meta), args.iters)
+        log(f"[rank 0] CPU baseline {cpu['value']:.4f} pairs/s")
+
+    value = world * args.steps / elapsed
+    ms_step = elapsed / args.steps * 1e3
+    out = {
+        "metric": "IMLS-ICP scan-pairs/s (HDL-64 ~120k-pt scan vs 10-scan map, 20 ICP iterations)",
+        "value": value,
+        "unit": "scan-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "ms_per_iteration": (ms_step - idx_ms / max(idx_n, 1)) / args.iters,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded HDL-64 ray-cast urban scene, planetary-lidar-odometry_amd/synth.py)",
+        "config": {
+            "workload": "config B: HDL-64 scan vs 10-scan local map, 1 scan pair per step",
+            "queries": int(stats["queries"]),
+            "map_points": int(stats["points"]),
+            "icp_iterations": args.iters,
+            "solver": "LS (trimmed, t=0.02)",
+            "search_number": p.search_number,
+            "parallelism": f"pairs sharded over {world} GPU(s), RCCL pose all-gather" if world > 1 else "1 GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_project (fused transform + exact radius kNN + IMLS projection + pass-1 normal equations)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_launch,
+            "avg_launch_ms": avg_proj_s * 1e3,
+            "launches": int(proj_n),
+        },
+        "breakdown_ms_per_pair": {
+            "index_build": idx_ms / max(args.steps, 1),
+            "projection": proj_ms / max(args.steps, 1),
+            "solve_chain": sol_ms / max(args.steps, 1),
+        },
+        "cpu_baseline": cpu,
+        "final_pose_error_cm": float(err * 100),
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

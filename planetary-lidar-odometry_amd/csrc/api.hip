@@ -1,0 +1,575 @@
+// api.hip — the C ABI of include/imls_gpu.h: context, uploads, and the fused per-frame loop.
+//
+// imls_register_frame is the device-resident form of laser_odometry.cpp:478-660: all
+// `iterations` × {k_project, solve chain} launches are enqueued back to back on the context
+// stream; convergence / too-few-correspondence exits are taken on the device (a `done` flag
+// every later launch checks first), so the host synchronises once per frame.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+using namespace imlsgpu;
+
+struct imls_ctx {
+    int device = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    imls_params P{};
+    KParams kp{};
+    std::string err;
+    int B = 32;
+    // target
+    DevBuf tpt, tnr, mpt, nodes, tscratch, upload_t;
+    int M = 0, Pl = 0, levels = 0;
+    bool has_target = false;
+    // source
+    DevBuf spt, snr, sscratch, upload_s;
+    int N = 0;
+    bool has_source = false;
+    // correspondences + solver state
+    DevBuf cs, cd, cn, solve_mem, trace_mem, stats, rows_d, pose_tmp;
+    SolveState st{};
+    int st_N = -1, trace_cap = 0;
+    bool has_corr = false;
+    // async frame results
+    imls_iter_trace* h_trace = nullptr;   // pinned
+    double* h_misc = nullptr;             // pinned: pose[16], iters, status
+    int pending_iters = 0;
+    bool pending = false;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;
+    int ev_used = 0;
+    std::vector<std::pair<int, int>> ev_pairs[3];
+    double t_ms[3] = {0, 0, 0};
+    uint64_t t_n[3] = {0, 0, 0};
+};
+
+namespace {
+
+int fail(imls_ctx* c, int code, const std::string& m) {
+    if (c) c->err = m;
+    return code;
+}
+
+bool grow(DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes) return true;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    if (hipMalloc(&b.p, bytes) != hipSuccess) return false;
+    b.bytes = bytes;
+    return true;
+}
+
+KParams make_kparams(const imls_params& p) {
+    KParams k{};
+    k.h2 = p.h * p.h;
+    k.r2 = p.r * p.r;
+    k.angle_thr_deg = p.angle_diff_threshold;
+    k.K = p.search_number;
+    k.angle_on = p.normal_angle_constraint ? 1 : 0;
+    k.get_normals = p.get_normals ? 1 : 0;
+    k.transform_normal = p.transform_normal ? 1 : 0;
+    k.correspond_number = p.correspond_number;
+    k.solve_method = p.solve_method;
+    k.ls_threshold = p.ls_threshold;
+    k.delta_dist = p.delta_dist_threshold;
+    k.delta_angle = p.delta_angle_threshold;
+    return k;
+}
+
+int check_params(imls_ctx* c, const imls_params* p) {
+    if (!p) return fail(c, IMLS_ERR_ARG, "null params");
+    if (p->search_number < 1 || p->search_number > 32) return fail(c, IMLS_ERR_UNSUPPORTED, "search_number must be in [1, 32]");
+    if (p->matching_method != IMLS_MATCH_IMLS) return fail(c, IMLS_ERR_UNSUPPORTED, "matching_method plane_ICP is not built on the GPU path yet");
+    if (p->use_tensor_voting && !p->get_normals) return fail(c, IMLS_ERR_UNSUPPORTED, "tensor voting normals are not on the GPU path");
+    if (p->use_projected_distance) return fail(c, IMLS_ERR_UNSUPPORTED, "use_projected_distance is not built on the GPU path yet");
+    if (!p->get_normals && p->recompute_normal_count_mode) return fail(c, IMLS_ERR_UNSUPPORTED, "recompute-normal count mode is not on the GPU path");
+    if (p->solve_method != IMLS_SOLVE_LS && p->solve_method != IMLS_SOLVE_WEIGHTED_LS)
+        return fail(c, IMLS_ERR_UNSUPPORTED, "solve_method RANSAC is not built on the GPU path yet");
+    if (p->iterations < 0) return fail(c, IMLS_ERR_ARG, "iterations < 0");
+    if (!(p->ls_threshold >= 0 && p->ls_threshold < 0.5)) return fail(c, IMLS_ERR_ARG, "LS threshold must be in [0, 0.5)");
+    return IMLS_OK;
+}
+
+// Per-N solver / correspondence buffers.
+int ensure_solve(imls_ctx* c, int N) {
+    if (c->st_N >= N && c->st.trace) return IMLS_OK;
+    size_t n = (size_t)std::max(N, 1);
+    if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
+    const int pb = std::max(project_blocks((int)n), solve_blocks((int)n)) + 1;
+    size_t bytes = 0;
+    auto add = [&](size_t b) { size_t o = bytes; bytes += (b + 255) / 256 * 256; return o; };
+    size_t o_pose = add(16 * 8), o_delta = add(16 * 8), o_x0 = add(8 * 8), o_done = add(16), o_status = add(16),
+           o_iters = add(16), o_hist = add(kHistBins * 4), o_cc = add(16), o_cl = add((size_t)kCandCap * 8),
+           o_clr = add((size_t)kCandCap * 4), o_ch = add((size_t)kCandCap * 8), o_chr = add((size_t)kCandCap * 4),
+           o_sel = add(16 * 4), o_p1 = add((size_t)pb * kNormEq * 8), o_p2 = add((size_t)pb * kNormEq * 8),
+           o_keys = add(n * 8), o_trace1 = add(sizeof(imls_iter_trace));
+    if (!grow(c->solve_mem, bytes)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (solver)");
+    char* b = (char*)c->solve_mem.p;
+    SolveState& s = c->st;
+    s.pose = (double*)(b + o_pose);
+    s.delta = (double*)(b + o_delta);
+    s.x0 = (double*)(b + o_x0);
+    s.done = (int*)(b + o_done);
+    s.status = (int*)(b + o_status);
+    s.iters = (int*)(b + o_iters);
+    s.hist = (unsigned*)(b + o_hist);
+    s.cand_count = (unsigned*)(b + o_cc);
+    s.cand_lo = (unsigned long long*)(b + o_cl);
+    s.cand_lo_row = (unsigned*)(b + o_clr);
+    s.cand_hi = (unsigned long long*)(b + o_ch);
+    s.cand_hi_row = (unsigned*)(b + o_chr);
+    s.sel = (int*)(b + o_sel);
+    s.partial1 = (double*)(b + o_p1);
+    s.partial2 = (double*)(b + o_p2);
+    s.keys = (double*)(b + o_keys);
+    s.trace = (imls_iter_trace*)(b + o_trace1);
+    s.partial_cap = pb;
+    c->st_N = (int)n;
+    return IMLS_OK;
+}
+
+int ensure_trace(imls_ctx* c, int iters) {
+    if (c->trace_cap >= iters && c->h_trace) return IMLS_OK;
+    if (!grow(c->trace_mem, (size_t)std::max(iters, 1) * sizeof(imls_iter_trace))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (trace)");
+    if (c->h_trace) (void)hipHostFree(c->h_trace);
+    if (hipHostMalloc((void**)&c->h_trace, (size_t)std::max(iters, 1) * sizeof(imls_iter_trace)) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "hipHostMalloc (trace)");
+    c->trace_cap = std::max(iters, 1);
+    return IMLS_OK;
+}
+
+TreeView tree_view(imls_ctx* c) {
+    TreeView t;
+    t.mpt = (const float4*)c->mpt.p;
+    t.nodes = (const float4*)c->nodes.p;
+    t.tpt = (const float4*)c->tpt.p;
+    t.tnr = (const float4*)c->tnr.p;
+    t.M = c->M;
+    t.B = c->B;
+    t.P = c->Pl;
+    t.levels = c->levels;
+    return t;
+}
+
+int ev_pair(imls_ctx* c) {
+    if (c->ev_used + 2 > (int)c->ev.size()) {
+        for (int k = 0; k < 64; ++k) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return -1;
+            c->ev.push_back(e);
+        }
+    }
+    int i = c->ev_used;
+    c->ev_used += 2;
+    return i;
+}
+
+void timed_begin(imls_ctx* c, int kind, int& slot) {
+    slot = -1;
+    if (!c->timing) return;
+    slot = ev_pair(c);
+    if (slot >= 0) hipEventRecord(c->ev[slot], c->stream);
+}
+void timed_end(imls_ctx* c, int kind, int slot) {
+    if (slot < 0) return;
+    hipEventRecord(c->ev[slot + 1], c->stream);
+    c->ev_pairs[kind].push_back({slot, slot + 1});
+}
+void harvest_timing(imls_ctx* c) {
+    for (int k = 0; k < 3; ++k) {
+        for (auto& pr : c->ev_pairs[k]) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, c->ev[pr.first], c->ev[pr.second]) == hipSuccess) {
+                c->t_ms[k] += ms;
+                c->t_n[k] += 1;
+            }
+        }
+        c->ev_pairs[k].clear();
+    }
+    c->ev_used = 0;
+}
+
+// Pack a strided host cloud into SoA6 floats and upload.
+int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, size_t n, size_t stride) {
+    if (!xyz || !nrm || n == 0 || stride < 3) return fail(c, IMLS_ERR_ARG, "bad cloud pointer/size/stride");
+    std::vector<float> h(6 * n);
+    for (size_t i = 0; i < n; ++i) {
+        const float* p = xyz + i * stride;
+        const float* q = nrm + i * stride;
+        h[i] = p[0]; h[n + i] = p[1]; h[2 * n + i] = p[2];
+        h[3 * n + i] = q[0]; h[4 * n + i] = q[1]; h[5 * n + i] = q[2];
+    }
+    if (!grow(dst, h.size() * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (upload)");
+    if (hipMemcpyAsync(dst.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "upload failed");
+    return IMLS_OK;
+}
+
+int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
+    int slot;
+    timed_begin(c, 1, slot);
+    int rc = build_target_index(c->stream, d_soa6, n, c->B, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch, &c->M, &c->Pl,
+                                &c->levels, c->err);
+    timed_end(c, 1, slot);
+    if (rc) return rc;
+    c->has_target = c->M > 0;
+    c->has_corr = false;
+    if (n_kept) *n_kept = (size_t)c->M;
+    return IMLS_OK;
+}
+
+int do_set_source(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept, uint32_t* kept_index) {
+    std::vector<uint32_t> kept;
+    int rc = load_source(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, &c->N, kept_index ? &kept : nullptr, c->err);
+    if (rc) return rc;
+    if (kept_index && !kept.empty()) std::memcpy(kept_index, kept.data(), kept.size() * 4);
+    c->has_source = c->N > 0;
+    c->has_corr = false;
+    if (n_kept) *n_kept = (size_t)c->N;
+    return ensure_solve(c, c->N);
+}
+
+int check_device(imls_ctx* c) {
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) return fail(c, IMLS_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    return IMLS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int imls_abi_version(void) { return IMLS_GPU_ABI_VERSION; }
+
+void imls_default_params(imls_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    // config.json shipped values (laser_odometry section)
+    p->matching_method = IMLS_MATCH_IMLS;
+    p->correspond_number = 6;
+    p->h = 1.0;
+    p->r = 3.0;
+    p->get_normals = 1;
+    p->search_number_normal = 10;
+    p->r_normal = 1.0;
+    p->use_projected_distance = 0;
+    p->r_proj = 0.8;
+    p->normal_angle_constraint = 1;
+    p->angle_diff_threshold = 30.0;
+    p->search_number = 20;
+    p->use_tensor_voting = 0;
+    p->tensor_k = 50;
+    p->tensor_sigma = 0.2;
+    p->tensor_distance_threshold = 0.6;
+    p->picp_r = 1.5;
+    p->picp_r_proj = 0.8;
+    p->picp_angle_diff_threshold = 30.0;
+    p->picp_use_projected_distance = 0;
+    p->picp_normal_angle_constraint = 1;
+    p->solve_method = IMLS_SOLVE_RANSAC;
+    p->iterations = 30;
+    p->delta_dist_threshold = 0.001;
+    p->delta_angle_threshold = 0.0001745353;
+    p->ls_threshold = 0.02;
+    p->ransac_max_iterations = 5000;
+    p->ransac_final_method = IMLS_FINAL_DRPM;
+    p->ransac_distance_threshold = 0.8;
+    p->ransac_min_inliers_percentage = 0.95;
+    p->ransac_huber_threshold = 0.648;
+    p->ransac_ls_threshold = 0.02;
+    p->drpm_threshold = 0.05;
+    p->drpm_stdev_points = 0.02;
+    p->drpm_stdev_normals = 0.05;
+    p->ransac_seed = 1;
+    p->transform_normal = 0;
+    p->max_queue_size = 1;
+}
+
+imls_ctx* imls_create(int device, const imls_params* p) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+    imls_ctx* c = new imls_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    c->stream = c->own;
+    if (hipHostMalloc((void**)&c->h_misc, 32 * sizeof(double)) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    if (const char* b = std::getenv("IMLS_BUCKET")) {
+        int v = std::atoi(b);
+        if (v >= 4 && v <= 256 && (v & (v - 1)) == 0) c->B = v;
+    }
+    imls_params d;
+    imls_default_params(&d);
+    d.solve_method = IMLS_SOLVE_LS;
+    if (imls_set_params(c, p ? p : &d) != IMLS_OK) {
+        imls_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void imls_destroy(imls_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->upload_t, &c->spt, &c->snr, &c->sscratch,
+                      &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
+    for (DevBuf* b : bufs)
+        if (b->p) (void)hipFree(b->p);
+    for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    if (c->h_trace) (void)hipHostFree(c->h_trace);
+    if (c->h_misc) (void)hipHostFree(c->h_misc);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int imls_set_params(imls_ctx* c, const imls_params* p) {
+    if (!c) return IMLS_ERR_ARG;
+    int rc = check_params(c, p);
+    if (rc) return rc;
+    c->P = *p;
+    c->kp = make_kparams(*p);
+    return IMLS_OK;
+}
+
+const char* imls_last_error(const imls_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int imls_set_stream(imls_ctx* c, void* s) {
+    if (!c) return IMLS_ERR_ARG;
+    c->stream = s ? (hipStream_t)s : c->own;
+    return IMLS_OK;
+}
+
+int imls_synchronize(imls_ctx* c) {
+    if (!c) return IMLS_ERR_ARG;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? IMLS_OK : fail(c, IMLS_ERR_DEVICE, "stream sync failed");
+}
+
+int imls_set_target(imls_ctx* c, const float* xyz, const float* nrm, size_t n, size_t stride, size_t* n_kept) {
+    if (!c) return IMLS_ERR_ARG;
+    if (int rc = check_device(c)) return rc;
+    if (int rc = upload_soa6(c, c->upload_t, xyz, nrm, n, stride)) return rc;
+    return do_set_target(c, (const float*)c->upload_t.p, n, n_kept);
+}
+
+int imls_set_target_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
+    if (!c || !d_soa6) return IMLS_ERR_ARG;
+    if (int rc = check_device(c)) return rc;
+    return do_set_target(c, d_soa6, n, n_kept);
+}
+
+int imls_set_source(imls_ctx* c, const float* xyz, const float* nrm, size_t n, size_t stride, size_t* n_kept,
+                    uint32_t* kept_index) {
+    if (!c) return IMLS_ERR_ARG;
+    if (int rc = check_device(c)) return rc;
+    if (int rc = upload_soa6(c, c->upload_s, xyz, nrm, n, stride)) return rc;
+    return do_set_source(c, (const float*)c->upload_s.p, n, n_kept, kept_index);
+}
+
+int imls_set_source_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
+    if (!c || !d_soa6) return IMLS_ERR_ARG;
+    if (int rc = check_device(c)) return rc;
+    return do_set_source(c, d_soa6, n, n_kept, nullptr);
+}
+
+int imls_project(imls_ctx* c, const double pose[16], float* x_out, float* y_out, float* n_out, uint32_t* src_index_out,
+                 size_t* n_valid, uint64_t reject[IMLS_NUM_REJ]) {
+    if (!c || !pose) return IMLS_ERR_ARG;
+    if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
+    if (int rc = check_device(c)) return rc;
+    if (int rc = ensure_solve(c, c->N)) return rc;
+    if (!grow(c->pose_tmp, 32 * 8) || !grow(c->stats, 64)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");
+    double* dpose = (double*)c->pose_tmp.p;
+    int* dzero = (int*)(dpose + 16);
+    hipMemcpyAsync(dpose, pose, 16 * 8, hipMemcpyHostToDevice, c->stream);
+    hipMemsetAsync(dzero, 0, 16, c->stream);
+    hipMemsetAsync(c->st.trace, 0, sizeof(imls_iter_trace), c->stream);
+    hipMemsetAsync(c->stats.p, 0, 64, c->stream);
+    int slot;
+    timed_begin(c, 0, slot);
+    launch_project(c->stream, tree_view(c), (const float4*)c->spt.p, (const float4*)c->snr.p, c->N, dpose, dzero, c->kp,
+                   (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p, c->st.partial1, c->st.trace,
+                   (unsigned long long*)c->stats.p);
+    timed_end(c, 0, slot);
+    std::vector<float> hs((size_t)c->N * 4), hd((size_t)c->N * 4), hn((size_t)c->N * 4);
+    imls_iter_trace tr;
+    hipMemcpyAsync(hs.data(), c->cs.p, hs.size() * 4, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(hd.data(), c->cd.p, hd.size() * 4, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(hn.data(), c->cn.p, hn.size() * 4, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(&tr, c->st.trace, sizeof(tr), hipMemcpyDeviceToHost, c->stream);
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, std::string("project: ") + hipGetErrorString(hipGetLastError()));
+    harvest_timing(c);
+    size_t k = 0;
+    for (int i = 0; i < c->N; ++i) {
+        if (hs[4 * i + 3] == 0.f) continue;
+        for (int d = 0; d < 3; ++d) {
+            if (x_out) x_out[3 * k + d] = hs[4 * i + d];
+            if (y_out) y_out[3 * k + d] = hd[4 * i + d];
+            if (n_out) n_out[3 * k + d] = hn[4 * i + d];
+        }
+        if (src_index_out) src_index_out[k] = (uint32_t)i;
+        ++k;
+    }
+    if (n_valid) *n_valid = k;
+    if (reject) std::memcpy(reject, tr.reject, sizeof(tr.reject));
+    c->has_corr = true;
+    return IMLS_OK;
+}
+
+int imls_solve(imls_ctx* c, double delta_out[16], int* ok) {
+    if (!c || !delta_out) return IMLS_ERR_ARG;
+    if (!c->has_corr) return fail(c, IMLS_ERR_STATE, "imls_project first");
+    if (int rc = check_device(c)) return rc;
+    hipMemsetAsync(c->st.done, 0, 16, c->stream);
+    int slot;
+    timed_begin(c, 2, slot);
+    launch_solve_chain(c->stream, c->N, project_blocks(c->N), c->kp, (const float4*)c->cs.p, (const float4*)c->cd.p,
+                       (const float4*)c->cn.p, nullptr, nullptr, c->st, nullptr, 0, 0);
+    timed_end(c, 2, slot);
+    hipMemcpyAsync(delta_out, c->st.delta, 16 * 8, hipMemcpyDeviceToHost, c->stream);
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "solve failed");
+    harvest_timing(c);
+    if (ok) *ok = 1;
+    return IMLS_OK;
+}
+
+int imls_solve_correspondences(imls_ctx* c, int32_t method, const double* s, const double* d, const double* n,
+                               const double* w, size_t N, double delta_out[16], int* ok) {
+    if (!c || !s || !d || !n || !delta_out) return IMLS_ERR_ARG;
+    if (method != IMLS_SOLVE_LS && method != IMLS_SOLVE_WEIGHTED_LS) return fail(c, IMLS_ERR_UNSUPPORTED, "method");
+    if (N > (size_t)0x3fffffff) return fail(c, IMLS_ERR_ARG, "N too large");
+    if (int rc = check_device(c)) return rc;
+    if (int rc = ensure_solve(c, (int)std::max<size_t>(N, 1))) return rc;
+    size_t bytes = (9 * N + N) * 8 + 64;
+    if (!grow(c->rows_d, bytes)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (rows)");
+    double* r = (double*)c->rows_d.p;
+    hipMemcpyAsync(r, s, 3 * N * 8, hipMemcpyHostToDevice, c->stream);
+    hipMemcpyAsync(r + 3 * N, d, 3 * N * 8, hipMemcpyHostToDevice, c->stream);
+    hipMemcpyAsync(r + 6 * N, n, 3 * N * 8, hipMemcpyHostToDevice, c->stream);
+    const double* dw = nullptr;
+    if (w) {
+        hipMemcpyAsync(r + 9 * N, w, N * 8, hipMemcpyHostToDevice, c->stream);
+        dw = r + 9 * N;
+    }
+    hipMemsetAsync(c->st.done, 0, 16, c->stream);
+    KParams kp = c->kp;
+    kp.solve_method = method;
+    launch_solve_chain(c->stream, (int)N, 0, kp, nullptr, nullptr, nullptr, r, dw, c->st, nullptr, 0, 1);
+    hipMemcpyAsync(delta_out, c->st.delta, 16 * 8, hipMemcpyDeviceToHost, c->stream);
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "solve failed");
+    if (ok) *ok = 1;
+    return IMLS_OK;
+}
+
+int imls_register_frame_async(imls_ctx* c) {
+    if (!c) return IMLS_ERR_ARG;
+    if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
+    if (int rc = check_device(c)) return rc;
+    if (int rc = ensure_solve(c, c->N)) return rc;
+    const int iters = c->P.iterations;
+    if (int rc = ensure_trace(c, iters)) return rc;
+    if (!grow(c->stats, 64)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");
+    static const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    hipMemcpyAsync(c->st.pose, I, sizeof(I), hipMemcpyHostToDevice, c->stream);
+    hipMemsetAsync(c->st.done, 0, 16, c->stream);
+    hipMemsetAsync(c->st.status, 0, 16, c->stream);
+    hipMemsetAsync(c->st.iters, 0, 16, c->stream);
+    hipMemsetAsync(c->trace_mem.p, 0, (size_t)std::max(iters, 1) * sizeof(imls_iter_trace), c->stream);
+    hipMemsetAsync(c->stats.p, 0, 64, c->stream);
+    imls_iter_trace* tr = (imls_iter_trace*)c->trace_mem.p;
+    const TreeView tv = tree_view(c);
+    for (int it = 0; it < iters; ++it) {
+        int slot;
+        timed_begin(c, 0, slot);
+        launch_project(c->stream, tv, (const float4*)c->spt.p, (const float4*)c->snr.p, c->N, c->st.pose, c->st.done, c->kp,
+                       (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p, c->st.partial1, tr + it,
+                       (unsigned long long*)c->stats.p);
+        timed_end(c, 0, slot);
+        timed_begin(c, 2, slot);
+        launch_solve_chain(c->stream, c->N, project_blocks(c->N), c->kp, (const float4*)c->cs.p, (const float4*)c->cd.p,
+                           (const float4*)c->cn.p, nullptr, nullptr, c->st, tr + it, 1, 0);
+        timed_end(c, 2, slot);
+    }
+    hipMemcpyAsync(c->h_misc, c->st.pose, 16 * 8, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(c->h_misc + 16, c->st.iters, 16, hipMemcpyDeviceToHost, c->stream);
+    if (iters > 0)
+        hipMemcpyAsync(c->h_trace, tr, (size_t)iters * sizeof(imls_iter_trace), hipMemcpyDeviceToHost, c->stream);
+    if (hipGetLastError() != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "launch failed");
+    c->pending = true;
+    c->pending_iters = iters;
+    c->has_corr = true;
+    return IMLS_OK;
+}
+
+int imls_register_frame_result(imls_ctx* c, double pose_out[16], int* iters_run, int* status, imls_iter_trace* trace) {
+    if (!c) return IMLS_ERR_ARG;
+    if (!c->pending) return fail(c, IMLS_ERR_STATE, "no frame pending");
+    c->pending = false;
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return fail(c, IMLS_ERR_DEVICE, std::string("frame failed: ") + hipGetErrorString(e));
+    harvest_timing(c);
+    const int* misc = (const int*)(c->h_misc + 16);
+    // misc[0] = iters, misc[?]: status lives in its own 16-B slot; fetch synchronously
+    int st = 0;
+    if (hipMemcpy(&st, c->st.status, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "status copy");
+    if (pose_out) std::memcpy(pose_out, c->h_misc, 16 * 8);
+    if (iters_run) *iters_run = misc[0];
+    if (status) *status = st;
+    if (trace && c->pending_iters > 0) std::memcpy(trace, c->h_trace, (size_t)c->pending_iters * sizeof(imls_iter_trace));
+    return IMLS_OK;
+}
+
+int imls_register_frame(imls_ctx* c, double pose_out[16], int* iters_run, int* status, imls_iter_trace* trace) {
+    int rc = imls_register_frame_async(c);
+    if (rc) return rc;
+    return imls_register_frame_result(c, pose_out, iters_run, status, trace);
+}
+
+int imls_enable_timing(imls_ctx* c, int enable) {
+    if (!c) return IMLS_ERR_ARG;
+    c->timing = enable != 0;
+    return IMLS_OK;
+}
+
+int imls_kernel_timing(imls_ctx* c, int kernel, double* total_ms, uint64_t* launches) {
+    if (!c || kernel < 0 || kernel > 2) return IMLS_ERR_ARG;
+    if (total_ms) *total_ms = c->t_ms[kernel];
+    if (launches) *launches = c->t_n[kernel];
+    return IMLS_OK;
+}
+
+int imls_reset_timing(imls_ctx* c) {
+    if (!c) return IMLS_ERR_ARG;
+    for (int k = 0; k < 3; ++k) { c->t_ms[k] = 0; c->t_n[k] = 0; c->ev_pairs[k].clear(); }
+    c->ev_used = 0;
+    return IMLS_OK;
+}
+
+int imls_index_stats(imls_ctx* c, uint64_t out[8]) {
+    if (!c || !out) return IMLS_ERR_ARG;
+    unsigned long long st[2] = {0, 0};
+    if (c->stats.p) hipMemcpy(st, c->stats.p, 16, hipMemcpyDeviceToHost);
+    out[0] = (uint64_t)c->M;
+    out[1] = (uint64_t)((c->M + c->B - 1) / c->B);
+    out[2] = (uint64_t)c->Pl;
+    out[3] = (uint64_t)c->levels;
+    out[4] = st[0];   // Σ k_q (neighbours returned to queries reaching the IMLS function)
+    out[5] = st[1];   // queries whose NN-1 was found
+    out[6] = (uint64_t)c->N;
+    out[7] = (uint64_t)c->B;
+    return IMLS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,100 @@
+// internal.h — shared declarations of the HIP IMLS-ICP path (gfx950 only).
+//
+// HBM layout (SoA-of-float4, 16-B aligned, one record per point):
+//   target, filtered order   : tpt[M]  = (x, y, z, 0)      tnr[M] = (nx, ny, nz, 0)
+//   target, Morton order     : mpt[M]  = (x, y, z, bits(filtered index))   ← leaf scans
+//   tree (implicit, complete): node i ∈ [1, P) holds the AABBs of children 2i, 2i+1 as
+//                              3 float4 (lo_l.xyz, hi_l.x | hi_l.yz, lo_r.xy | lo_r.z, hi_r.xyz);
+//                              leaf node P + b = bucket b = mpt[b·B, min((b+1)·B, M)).
+//   source, filtered order   : spt[N], snr[N] float4
+//   correspondences, per source index (uncompacted): cs[N] = (x, valid), cd[N] = (y, ·),
+//                              cn[N] = (n, ·) float4 — source order is implicit in the index.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/imls_gpu.h"
+
+namespace imlsgpu {
+
+constexpr int kBlock = 256;            // threads per block for streaming kernels
+constexpr int kProjBlock = 128;        // threads per block for the projection kernel
+constexpr int kStackDepth = 24;        // traversal stack entries per lane (tree depth ≤ 24)
+constexpr int kHistBins = 4096;        // residual histogram bins (top 12 bits of float |r|)
+constexpr int kCandCap = 8192;         // exact-select candidates handled in LDS per boundary bin
+constexpr int kNormEq = 28;            // 21 (JᵀJ upper) + 6 (Jᵀb) + 1 (row count)
+
+// Device-side per-iteration record, laid out as imls_iter_trace.
+static_assert(sizeof(imls_iter_trace) == 16 * 8 * 2 + 8 * 8, "trace layout");
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+// Parameters the kernels need, in a flat POD copied by value into launches.
+struct KParams {
+    double h2, r2, cos_unused;
+    double angle_thr_deg;
+    int K;                    // search_number
+    int angle_on;
+    int get_normals;
+    int transform_normal;
+    int correspond_number;
+    int solve_method;
+    double ls_threshold;
+    double delta_dist, delta_angle;
+};
+
+struct TreeView {
+    const float4* mpt;
+    const float4* nodes;      // 3 float4 per internal node, index 1..P-1 (entry 0 unused)
+    const float4* tpt;
+    const float4* tnr;
+    int M, B, P, levels;
+};
+
+// Solver scratch living in device memory (one per context).
+struct SolveState {
+    double* pose;             // [16] current rPose
+    double* delta;            // [16] last Δ
+    double* x0;               // [8]  first LS solution
+    int* done;                // [1]  frame finished (converged / too few / failed)
+    int* status;              // [1]  imls_frame_status
+    int* iters;               // [1]  iterations run
+    unsigned* hist;           // [kHistBins]
+    unsigned* cand_count;     // [2]
+    unsigned long long* cand_lo;   // [kCandCap*?] (key bits) pairs with row index
+    unsigned* cand_lo_row;
+    unsigned long long* cand_hi;
+    unsigned* cand_hi_row;
+    int* sel;                 // [8] select metadata: b_lo, b_hi, c_lo, c_hi, lower, upper, nvalid
+    double* partial1;         // [blocks × kNormEq] pass-1 block partials
+    double* partial2;         // [blocks × kNormEq] pass-2 block partials
+    double* keys;             // [N] |r|
+    imls_iter_trace* trace;   // [iterations]
+    int partial_cap;
+};
+
+// index.hip
+int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket,
+                       DevBuf& tpt, DevBuf& tnr, DevBuf& mpt, DevBuf& nodes, DevBuf& scratch,
+                       int* M_out, int* P_out, int* levels_out, std::string& err);
+int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, DevBuf& snr,
+                DevBuf& scratch, int* N_out, std::vector<uint32_t>* kept, std::string& err);
+
+// project.hip
+void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const float4* snr, int N,
+                    const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd,
+                    float4* cn, double* partial1, imls_iter_trace* tr, unsigned long long* nbr_stats);
+int project_blocks(int N);
+
+// solve.hip
+void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, const float4* cs,
+                        const float4* cd, const float4* cn, const double* rows_d, const double* weights,
+                        SolveState& st, imls_iter_trace* tr, int update_pose, int rows_are_double);
+int solve_blocks(int N);
+
+}  // namespace imlsgpu

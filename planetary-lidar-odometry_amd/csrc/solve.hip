@@ -1,0 +1,555 @@
+// solve.hip — the Solving step on device: SolveMotionEstimationProblemLS (solver.cpp:74-166) and
+// SolveMotionEstimationProblemWeightedLS (solver.cpp:168-220), the pose update
+// rPose = Δ·rPose (laser_odometry.cpp:619) and the convergence test (laser_odometry.cpp:628-646).
+//
+// The reference solves the N×6 point-to-plane system with Eigen ColPivHouseholderQR, twice
+// (all rows; then the rows ranked ⌊tN⌋…⌊(1−t)N⌋ by |residual|).  Here each solve is a reduction
+// of the normal equations JᵀJ (21) and Jᵀb (6) in fp64 followed by a column-pivoted Cholesky of
+// the 6×6 system — the same column pivoting and the same rank test (|R_kk| > 6·ε·max|R_ii|) as
+// ColPivHouseholderQR, since JᵀJ's Schur-complement diagonal equals QR's updated column norms².
+//
+// Trim selection is exact in the total order (|r|, row): |r| (fp64) is histogrammed on the top 12
+// bits of its float image (monotone), the two boundary bins are collected and sorted by
+// (|r| bits, row) in LDS, everything strictly between them is reduced directly.
+//
+// Launch chain per LS solve: k_solve_first (1 block) → k_resid_hist → k_collect → k_solve_final
+// (1 block).  Every kernel returns at once when the frame's `done` flag is set.
+#include <cfloat>
+
+#include "internal.h"
+
+namespace imlsgpu {
+namespace {
+
+constexpr int kFinalBlock = 1024;
+constexpr int kCollectBlocks = 128;
+
+struct Rows {
+    const float4 *cs, *cd, *cn;           // float rows from the projection (valid flag in cs.w)
+    const double *ds, *dd, *dn, *w;       // or double rows (host API), all valid
+    int is_double;
+    __device__ __forceinline__ bool get(int i, double a[6], double& b, double& wt) const {
+        double s[3], d[3], n[3];
+        if (is_double) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { s[k] = ds[3 * i + k]; d[k] = dd[3 * i + k]; n[k] = dn[3 * i + k]; }
+            wt = w ? w[i] : 1.0;
+        } else {
+            const float4 s4 = cs[i];
+            if (s4.w == 0.f) return false;
+            const float4 d4 = cd[i], n4 = cn[i];
+            s[0] = s4.x; s[1] = s4.y; s[2] = s4.z;
+            d[0] = d4.x; d[1] = d4.y; d[2] = d4.z;
+            n[0] = n4.x; n[1] = n4.y; n[2] = n4.z;
+            wt = 1.0;
+        }
+        // solver.cpp:95-103
+        a[0] = n[2] * s[1] - n[1] * s[2];
+        a[1] = n[0] * s[2] - n[2] * s[0];
+        a[2] = n[1] * s[0] - n[0] * s[1];
+        a[3] = n[0]; a[4] = n[1]; a[5] = n[2];
+        b = n[0] * (d[0] - s[0]);
+        b = b + n[1] * (d[1] - s[1]);
+        b = b + n[2] * (d[2] - s[2]);
+        return true;
+    }
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-reduce the 28 normal-equation terms of (a, b, weight, count); result valid in thread 0's
+// `out` (all threads must call).  red: [nwaves][28] LDS.
+template <int NT>
+__device__ void block_normeq(const double a[6], double b, double cnt, double* red, double out[kNormEq]) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int k = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = r; c < 6; ++c) {
+            const double v = wave_sum(a[r] * a[c]);
+            if (lane == 0) red[wv * kNormEq + k] = v;
+            ++k;
+        }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        const double v = wave_sum(a[r] * b);
+        if (lane == 0) red[wv * kNormEq + 21 + r] = v;
+    }
+    {
+        const double v = wave_sum(cnt);
+        if (lane == 0) red[wv * kNormEq + 27] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNormEq) {
+        double s = 0.0;
+        for (int w = 0; w < NT / 64; ++w) s += red[w * kNormEq + threadIdx.x];
+        out[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+// Column-pivoted Cholesky solve of the 6×6 normal equations (see file header).  Unknowns past the
+// numerical rank are set to zero (Eigen's basic solution).  Returns the rank.
+__device__ int solve6(const double* ne, double x[6]) {
+    double A[6][6], g[6];
+    int k = 0;
+    for (int r = 0; r < 6; ++r)
+        for (int c = r; c < 6; ++c) { A[r][c] = ne[k]; A[c][r] = ne[k]; ++k; }
+    for (int r = 0; r < 6; ++r) g[r] = ne[21 + r];
+    int perm[6] = {0, 1, 2, 3, 4, 5};
+    const double eps = DBL_EPSILON;
+    double maxpiv = 0.0;
+    int rank = 6;
+    for (int j = 0; j < 6; ++j) {
+        int p = j;
+        for (int q = j + 1; q < 6; ++q) if (A[q][q] > A[p][p]) p = q;
+        if (p != j) {
+            for (int c = 0; c < 6; ++c) { double t = A[j][c]; A[j][c] = A[p][c]; A[p][c] = t; }
+            for (int r = 0; r < 6; ++r) { double t = A[r][j]; A[r][j] = A[r][p]; A[r][p] = t; }
+            double t = g[j]; g[j] = g[p]; g[p] = t;
+            int ti = perm[j]; perm[j] = perm[p]; perm[p] = ti;
+        }
+        const double d = A[j][j];
+        const double rkk = d > 0 ? sqrt(d) : 0.0;
+        if (rkk > maxpiv) maxpiv = rkk;
+        if (!(rkk > eps * 6.0 * maxpiv) || !(d > 0)) { rank = j; break; }
+        A[j][j] = rkk;
+        for (int r = j + 1; r < 6; ++r) A[r][j] = A[r][j] / rkk;
+        for (int r = j + 1; r < 6; ++r)
+            for (int c = j + 1; c <= r; ++c) {
+                A[r][c] = A[r][c] - A[r][j] * A[c][j];
+                A[c][r] = A[r][c];
+            }
+    }
+    double y[6] = {0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < rank; ++r) {
+        double s = g[r];
+        for (int c = 0; c < r; ++c) s -= A[r][c] * y[c];
+        y[r] = s / A[r][r];
+    }
+    for (int r = rank - 1; r >= 0; --r) {
+        double s = y[r];
+        for (int c = r + 1; c < rank; ++c) s -= A[c][r] * y[c];
+        y[r] = s / A[r][r];
+    }
+    for (int r = 0; r < 6; ++r) x[r] = 0.0;
+    for (int r = 0; r < rank; ++r) x[perm[r]] = y[r];
+    return rank;
+}
+
+// Δ from x (solver.cpp:140-163): R = AngleAxis(‖ω‖, ω̂) (Eigen AngleAxis::toRotationMatrix), then
+// the JacobiSVD U·Vᵀ re-orthonormalisation as the polar factor (Newton iteration).
+__device__ void delta_from_x(const double x[6], double D[16]) {
+    const double wx = x[0], wy = x[1], wz = x[2];
+    double sq = wx * wx;
+    sq = sq + wy * wy;
+    sq = sq + wz * wz;
+    const double ang = sqrt(sq);
+    double ax = 0, ay = 0, az = 0;
+    if (sq > 0) { const double nr = sqrt(sq); ax = wx / nr; ay = wy / nr; az = wz / nr; }
+    const double s = sin(ang), c = cos(ang);
+    const double sx = s * ax, sy = s * ay, sz = s * az;
+    const double c1x = (1 - c) * ax, c1y = (1 - c) * ay, c1z = (1 - c) * az;
+    double R[9];
+    double tmp = c1x * ay; R[1] = tmp - sz; R[3] = tmp + sz;
+    tmp = c1x * az; R[2] = tmp + sy; R[6] = tmp - sy;
+    tmp = c1y * az; R[5] = tmp - sx; R[7] = tmp + sx;
+    R[0] = c1x * ax + c; R[4] = c1y * ay + c; R[8] = c1z * az + c;
+    for (int it = 0; it < 20; ++it) {
+        const double* a = R;
+        const double det = a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) + a[2] * (a[3] * a[7] - a[4] * a[6]);
+        if (det == 0) break;
+        const double cof[9] = {a[4] * a[8] - a[5] * a[7], a[5] * a[6] - a[3] * a[8], a[3] * a[7] - a[4] * a[6],
+                               a[2] * a[7] - a[1] * a[8], a[0] * a[8] - a[2] * a[6], a[1] * a[6] - a[0] * a[7],
+                               a[1] * a[5] - a[2] * a[4], a[2] * a[3] - a[0] * a[5], a[0] * a[4] - a[1] * a[3]};
+        double maxd = 0, n[9];
+        for (int k = 0; k < 9; ++k) { n[k] = 0.5 * (a[k] + cof[k] / det); maxd = fmax(maxd, fabs(n[k] - a[k])); }
+        for (int k = 0; k < 9; ++k) R[k] = n[k];
+        if (maxd < 1e-16) break;
+    }
+    for (int k = 0; k < 16; ++k) D[k] = 0.0;
+    for (int r = 0; r < 3; ++r) for (int cc = 0; cc < 3; ++cc) D[r * 4 + cc] = R[r * 3 + cc];
+    D[3] = x[3]; D[7] = x[4]; D[11] = x[5]; D[15] = 1.0;
+}
+
+// rPose = Δ·rPose, trace, convergence (laser_odometry.cpp:619-646); single thread.
+__device__ void finish_iteration(SolveState st, imls_iter_trace* tr, const double D[16], double nvalid, double nkept,
+                                 int update_pose, const KParams& kp) {
+    for (int k = 0; k < 16; ++k) st.delta[k] = D[k];
+    if (tr) {
+        for (int k = 0; k < 16; ++k) tr->delta[k] = D[k];
+        tr->n_valid = (unsigned long long)nvalid;
+        tr->n_kept = (unsigned long long)nkept;
+    }
+    if (!update_pose) return;
+    double Pn[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = D[i * 4 + 0] * st.pose[0 * 4 + j];
+            s = s + D[i * 4 + 1] * st.pose[1 * 4 + j];
+            s = s + D[i * 4 + 2] * st.pose[2 * 4 + j];
+            s = s + D[i * 4 + 3] * st.pose[3 * 4 + j];
+            Pn[i * 4 + j] = s;
+        }
+    for (int k = 0; k < 16; ++k) st.pose[k] = Pn[k];
+    if (tr) for (int k = 0; k < 16; ++k) tr->pose[k] = Pn[k];
+    *st.iters += 1;
+    const double dd = sqrt(D[3] * D[3] + D[7] * D[7] + D[11] * D[11]);
+    double ct = ((D[0] + D[5] + D[10]) - 1.0) / 2.0;
+    ct = fmin(1.0, fmax(ct, -1.0));
+    const double da = acos(ct);
+    if (dd < kp.delta_dist && da < kp.delta_angle) {
+        *st.status = IMLS_FRAME_CONVERGED;
+        *st.done = 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// pass 1 for double rows (host API); float rows get it fused in k_project
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows_pass1(Rows rows, int N, double* __restrict__ partial) {
+    __shared__ double red[(NT / 64) * kNormEq];
+    __shared__ double out[kNormEq];
+    const int i = blockIdx.x * NT + threadIdx.x;
+    double a[6] = {0, 0, 0, 0, 0, 0}, b = 0, wt = 1, cnt = 0;
+    if (i < N && rows.get(i, a, b, wt)) {
+        const double sw = sqrt(wt);
+        for (int k = 0; k < 6; ++k) a[k] = sw * a[k];
+        b = sw * b;
+        cnt = 1;
+    }
+    block_normeq<NT>(a, b, cnt, red, out);
+    if (threadIdx.x < kNormEq) partial[(size_t)blockIdx.x * kNormEq + threadIdx.x] = out[threadIdx.x];
+}
+
+// Reduce pass-1 partials, first solve, set up the trim; or, for WLS, the only solve.
+__global__ __launch_bounds__(256) void k_solve_first(const double* __restrict__ partial, int blocks, SolveState st,
+                                                     imls_iter_trace* tr, KParams kp, int weighted, int update_pose) {
+    if (*st.done) return;
+    __shared__ double acc[kNormEq];
+    __shared__ double part[256][kNormEq + 1];
+    const int t = threadIdx.x;
+    double loc[kNormEq];
+    for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
+    for (int b = t; b < blocks; b += 256)
+        for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
+    for (int k = 0; k < kNormEq; ++k) part[t][k] = loc[k];
+    for (int i = t; i < kHistBins; i += 256) st.hist[i] = 0u;
+    if (t < 2) st.cand_count[t] = 0u;
+    __syncthreads();
+    if (t < kNormEq) {
+        double s = 0.0;
+        for (int j = 0; j < 256; ++j) s += part[j][t];
+        acc[t] = s;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    const double nvalid = acc[27];
+    if (update_pose && nvalid < (double)kp.correspond_number) {
+        // laser_odometry.cpp:570-576: not enough correspondences → break, keep rPose
+        *st.status = IMLS_FRAME_TOO_FEW;
+        *st.done = 1;
+        if (tr) tr->n_valid = (unsigned long long)nvalid;
+        return;
+    }
+    double x[6];
+    solve6(acc, x);
+    if (weighted) {
+        double D[16];
+        delta_from_x(x, D);
+        finish_iteration(st, tr, D, nvalid, nvalid, update_pose, kp);
+        return;
+    }
+    for (int k = 0; k < 6; ++k) st.x0[k] = x[k];
+    const long long N = (long long)nvalid;
+    long long lo = (long long)(kp.ls_threshold * (double)N);
+    long long hi = (long long)((1 - kp.ls_threshold) * (double)N);
+    if (hi > N - 1) hi = N - 1;       // Q11
+    st.sel[4] = (int)lo;
+    st.sel[5] = (int)hi;
+    st.sel[6] = (int)N;
+}
+
+__device__ __forceinline__ int key_bin(double key) {
+    return (int)(__float_as_uint((float)key) >> 20);   // key ≥ 0: monotone, < 4096 for finite keys
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_resid_hist(Rows rows, int N, SolveState st, KParams kp) {
+    if (*st.done) return;
+    __shared__ unsigned h[kHistBins];
+    for (int k = threadIdx.x; k < kHistBins; k += NT) h[k] = 0u;
+    __syncthreads();
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (i < N) {
+        double a[6], b, wt;
+        double key = -1.0;
+        if (rows.get(i, a, b, wt)) {
+            double v = a[0] * st.x0[0];
+            for (int k = 1; k < 6; ++k) v = v + a[k] * st.x0[k];
+            key = fabs(v - b);
+            atomicAdd(&h[min(key_bin(key), kHistBins - 1)], 1u);
+        }
+        st.keys[i] = key;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kHistBins; k += NT)
+        if (h[k]) atomicAdd(&st.hist[k], h[k]);
+}
+
+// Find the two boundary bins, reduce rows strictly between them, collect the boundary rows.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
+    if (*st.done) return;
+    __shared__ unsigned scan[kHistBins];
+    __shared__ int meta[4];
+    __shared__ double red[(NT / 64) * kNormEq];
+    __shared__ double out[kNormEq];
+    for (int k = threadIdx.x; k < kHistBins; k += NT) scan[k] = st.hist[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const long long lo = st.sel[4], hi = st.sel[5];
+        long long cum = 0;
+        int blo = -1, bhi = -1;
+        long long clo = 0, chi = 0;
+        for (int k = 0; k < kHistBins; ++k) {
+            const long long c = scan[k];
+            if (blo < 0 && lo < cum + c) { blo = k; clo = cum; }
+            if (bhi < 0 && hi < cum + c) { bhi = k; chi = cum; }
+            cum += c;
+        }
+        meta[0] = blo; meta[1] = bhi; meta[2] = (int)clo; meta[3] = (int)chi;
+        if (blockIdx.x == 0) { st.sel[0] = blo; st.sel[1] = bhi; st.sel[2] = (int)clo; st.sel[3] = (int)chi; }
+    }
+    __syncthreads();
+    const int blo = meta[0], bhi = meta[1];
+    double acc[kNormEq];
+    for (int k = 0; k < kNormEq; ++k) acc[k] = 0.0;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < N; i += gridDim.x * NT) {
+        const double key = st.keys[i];
+        if (key < 0) continue;
+        const int bin = min(key_bin(key), kHistBins - 1);
+        if (bin > blo && bin < bhi) {
+            double a[6], b, wt;
+            rows.get(i, a, b, wt);
+            int k = 0;
+            for (int r = 0; r < 6; ++r)
+                for (int c = r; c < 6; ++c) acc[k++] += a[r] * a[c];
+            for (int r = 0; r < 6; ++r) acc[21 + r] += a[r] * b;
+            acc[27] += 1.0;
+        } else if (bin == blo || bin == bhi) {
+            const int which = (bin == blo) ? 0 : 1;
+            const unsigned pos = atomicAdd(&st.cand_count[which], 1u);
+            if (pos < (unsigned)kCandCap) {
+                unsigned long long* ck = which ? st.cand_hi : st.cand_lo;
+                unsigned* cr = which ? st.cand_hi_row : st.cand_lo_row;
+                ck[pos] = (unsigned long long)__double_as_longlong(key);
+                cr[pos] = (unsigned)i;
+            }
+        }
+    }
+    // block reduction of the 28 partial sums
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k = 0; k < kNormEq; ++k) {
+        const double v = wave_sum(acc[k]);
+        if (lane == 0) red[wv * kNormEq + k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNormEq) {
+        double s = 0.0;
+        for (int w = 0; w < NT / 64; ++w) s += red[w * kNormEq + threadIdx.x];
+        partial2[(size_t)blockIdx.x * kNormEq + threadIdx.x] = s;
+    }
+}
+
+// bitonic sort of n (power of two ≤ kCandCap) (key, row) pairs in LDS, ascending
+__device__ void bitonic(unsigned long long* k, unsigned* r, int n) {
+    for (int size = 2; size <= n; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;
+                    const bool gt = k[i] > k[j] || (k[i] == k[j] && r[i] > r[j]);
+                    if (gt == up) {
+                        unsigned long long tk = k[i]; k[i] = k[j]; k[j] = tk;
+                        unsigned tr = r[i]; r[i] = r[j]; r[j] = tr;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// Exact fallback when a boundary bin overflows kCandCap: the (key, row) at global rank `target`
+// by bisection over the key bits then over rows (slow; only for massively tied residuals).
+__device__ void rank_select(const double* keys, int N, long long target, unsigned long long* kout, unsigned* rout,
+                            unsigned long long* sh_count) {
+    unsigned long long lo = 0, hi = 0x7FF0000000000000ull;   // key bits in [0, +inf]
+    while (lo < hi) {
+        const unsigned long long mid = lo + (hi - lo) / 2;
+        if (threadIdx.x == 0) *sh_count = 0;
+        __syncthreads();
+        unsigned long long c = 0;
+        for (int i = threadIdx.x; i < N; i += blockDim.x) {
+            const double k = keys[i];
+            if (k >= 0 && (unsigned long long)__double_as_longlong(k) <= mid) ++c;
+        }
+        atomicAdd(sh_count, c);
+        __syncthreads();
+        const unsigned long long cnt = *sh_count;
+        __syncthreads();
+        if ((long long)cnt > target) hi = mid; else lo = mid + 1;
+    }
+    const unsigned long long kb = lo;
+    // rank among rows with key < kb
+    if (threadIdx.x == 0) *sh_count = 0;
+    __syncthreads();
+    unsigned long long c = 0;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const double k = keys[i];
+        if (k >= 0 && (unsigned long long)__double_as_longlong(k) < kb) ++c;
+    }
+    atomicAdd(sh_count, c);
+    __syncthreads();
+    long long need = target - (long long)*sh_count;   // index among equal keys, by row
+    __syncthreads();
+    unsigned rlo = 0, rhi = (unsigned)N;
+    while (rlo < rhi) {
+        const unsigned mid = rlo + (rhi - rlo) / 2;
+        if (threadIdx.x == 0) *sh_count = 0;
+        __syncthreads();
+        unsigned long long cc = 0;
+        for (int i = threadIdx.x; i <= (int)mid && i < N; i += blockDim.x) {
+            const double k = keys[i];
+            if (k >= 0 && (unsigned long long)__double_as_longlong(k) == kb) ++cc;
+        }
+        atomicAdd(sh_count, cc);
+        __syncthreads();
+        const long long cnt = (long long)*sh_count;
+        __syncthreads();
+        if (cnt > need) rhi = mid; else rlo = mid + 1;
+    }
+    *kout = kb;
+    *rout = rlo;
+}
+
+__device__ __forceinline__ bool pair_le(unsigned long long ka, unsigned ra, unsigned long long kb, unsigned rb) {
+    return ka < kb || (ka == kb && ra <= rb);
+}
+
+__global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, SolveState st, imls_iter_trace* tr,
+                                                            const double* __restrict__ partial2, int nparts, KParams kp,
+                                                            int update_pose) {
+    if (*st.done) return;
+    __shared__ unsigned long long ck[kCandCap];
+    __shared__ unsigned cr[kCandCap];
+    __shared__ double red[(kFinalBlock / 64) * kNormEq];
+    __shared__ double out[kNormEq];
+    __shared__ unsigned long long shc;
+    __shared__ unsigned long long selk[2];
+    __shared__ unsigned selr[2];
+    const int blo = st.sel[0], bhi = st.sel[1];
+    const long long clo = st.sel[2], chi = st.sel[3], lo = st.sel[4], hi = st.sel[5];
+    const unsigned n_lo = st.cand_count[0], n_hi = st.cand_count[1];
+    double a[6] = {0, 0, 0, 0, 0, 0}, b = 0, wt = 1, cnt = 0;
+    double accA[kNormEq];
+    for (int k = 0; k < kNormEq; ++k) accA[k] = 0.0;
+    auto add_row = [&](unsigned row) {
+        double aa[6], bb, ww;
+        rows.get((int)row, aa, bb, ww);
+        int k = 0;
+        for (int r = 0; r < 6; ++r)
+            for (int c = r; c < 6; ++c) accA[k++] += aa[r] * aa[c];
+        for (int r = 0; r < 6; ++r) accA[21 + r] += aa[r] * bb;
+        accA[27] += 1.0;
+    };
+    const bool overflow = n_lo > (unsigned)kCandCap || n_hi > (unsigned)kCandCap;
+    if (!overflow) {
+        for (int which = 0; which < 2; ++which) {
+            const unsigned n = which ? n_hi : n_lo;
+            if (which == 1 && bhi == blo) break;
+            if (n == 0) continue;
+            int np = 1;
+            while (np < (int)n) np <<= 1;
+            const unsigned long long* gk = which ? st.cand_hi : st.cand_lo;
+            const unsigned* gr = which ? st.cand_hi_row : st.cand_lo_row;
+            for (int i = threadIdx.x; i < np; i += kFinalBlock) {
+                ck[i] = i < (int)n ? gk[i] : ~0ull;
+                cr[i] = i < (int)n ? gr[i] : ~0u;
+            }
+            __syncthreads();
+            bitonic(ck, cr, np);
+            const long long base = which ? chi : clo;
+            for (int i = threadIdx.x; i < (int)n; i += kFinalBlock) {
+                const long long rank = base + i;
+                if (rank >= lo && rank <= hi) add_row(cr[i]);
+            }
+            __syncthreads();
+        }
+    } else {
+        if (threadIdx.x == 0) shc = 0;
+        rank_select(st.keys, N, lo, &selk[0], &selr[0], &shc);
+        rank_select(st.keys, N, hi, &selk[1], &selr[1], &shc);
+        __syncthreads();
+        for (int i = threadIdx.x; i < N; i += kFinalBlock) {
+            const double key = st.keys[i];
+            if (key < 0) continue;
+            const int bin = min(key_bin(key), kHistBins - 1);
+            if (bin != blo && bin != bhi) continue;   // interior rows came from k_collect
+            const unsigned long long kb = (unsigned long long)__double_as_longlong(key);
+            if (pair_le(selk[0], selr[0], kb, (unsigned)i) && pair_le(kb, (unsigned)i, selk[1], selr[1])) add_row((unsigned)i);
+        }
+    }
+    // block reduce accA
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k = 0; k < kNormEq; ++k) {
+        const double v = wave_sum(accA[k]);
+        if (lane == 0) red[wv * kNormEq + k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNormEq) {
+        double s = 0.0;
+        for (int w = 0; w < kFinalBlock / 64; ++w) s += red[w * kNormEq + threadIdx.x];
+        for (int p = 0; p < nparts; ++p) s += partial2[(size_t)p * kNormEq + threadIdx.x];
+        out[threadIdx.x] = s;
+    }
+    __syncthreads();
+    (void)a; (void)b; (void)wt; (void)cnt;
+    if (threadIdx.x != 0) return;
+    double x[6], D[16];
+    solve6(out, x);
+    delta_from_x(x, D);
+    finish_iteration(st, tr, D, (double)st.sel[6], out[27], update_pose, kp);
+}
+
+}  // namespace
+
+int solve_blocks(int N) { return (N + kBlock - 1) / kBlock; }
+
+void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, const float4* cs, const float4* cd,
+                        const float4* cn, const double* rows_d, const double* weights, SolveState& st,
+                        imls_iter_trace* tr, int update_pose, int rows_are_double) {
+    Rows rows{cs, cd, cn, nullptr, nullptr, nullptr, weights, rows_are_double};
+    if (rows_are_double) {
+        rows.ds = rows_d;
+        rows.dd = rows_d + 3 * (size_t)N;
+        rows.dn = rows_d + 6 * (size_t)N;
+        blocks1 = solve_blocks(N);
+        k_rows_pass1<kBlock><<<blocks1, kBlock, 0, s>>>(rows, N, st.partial1);
+    }
+    const int weighted = kp.solve_method == IMLS_SOLVE_WEIGHTED_LS;
+    k_solve_first<<<1, 256, 0, s>>>(st.partial1, blocks1, st, tr, kp, weighted, update_pose);
+    if (weighted) return;
+    k_resid_hist<kBlock><<<solve_blocks(N), kBlock, 0, s>>>(rows, N, st, kp);
+    const int cb = std::max(1, std::min(kCollectBlocks, (N + kBlock * 4 - 1) / (kBlock * 4)));
+    k_collect<kBlock><<<cb, kBlock, 0, s>>>(rows, N, st, st.partial2);
+    k_solve_final<<<1, kFinalBlock, 0, s>>>(rows, N, st, tr, st.partial2, cb, kp, update_pose);
+}
+
+}  // namespace imlsgpu

@@ -1,0 +1,271 @@
+"""CPU tests of the oracle (test infrastructure): golden vectors, the independent numpy
+restatement, glibc rand() itself, and the analytic known-answer tests of SURVEY.md Appendix A.4.
+Parity status of the oracle: unpinned (no reference fixtures exist; see oracle/imls_oracle.h)."""
+import ctypes
+import math
+import pathlib
+
+import numpy as np
+import pytest
+
+import imls_np
+import oracle_ctypes as oc
+from planetary_lidar_odometry_amd import _abi, config, synth
+
+GOLDEN = pathlib.Path(__file__).resolve().parent / "golden"
+
+
+def golden(name):
+    return dict(np.load(GOLDEN / f"{name}.npz"))
+
+
+def gparams(iters=10):
+    p = config.bench_params(iters)
+    p.delta_dist_threshold = 0.001
+    p.delta_angle_threshold = 0.0001745353
+    return p
+
+
+@pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair"])
+def test_oracle_reproduces_golden(name):
+    g = golden(name)
+    p = gparams()
+    for k in (0, 1):
+        x, y, n, idx, rej = oc.project(g["src"], g["tgt"], g[f"pose{k}"], p)
+        assert np.array_equal(idx, g[f"idx{k}"])
+        assert np.array_equal(rej, g[f"rej{k}"])
+        assert np.array_equal(x, g[f"x{k}"]) and np.array_equal(y, g[f"y{k}"]) and np.array_equal(n, g[f"n{k}"])
+        ok, D = oc.solve(_abi.IMLS_SOLVE_LS, x, y, n, p)
+        assert ok and np.abs(D - g[f"ls{k}"]).max() < 1e-12
+    fr = oc.register_frame(g["src"], g["tgt"], p)
+    assert fr["iters"] == int(g["frame_iters"]) and fr["status"] == int(g["frame_status"])
+    assert np.abs(fr["pose"] - g["frame_pose"]).max() < 1e-12
+
+
+def test_golden_frame_recovers_true_pose():
+    g = golden("vlp16_pair")
+    err_t = np.linalg.norm(g["frame_pose"][:3, 3] - g["true_pose"][:3, 3])
+    assert err_t < 0.1, err_t
+
+
+def test_nan_points_are_filtered():
+    g = golden("vlp16_pair")
+    # the golden source carries one NaN x (point 3): dropped (imls_icp.cpp:58-78).  A NaN y
+    # drops one more; a NaN NORMAL is not filtered (pcl::isFinite checks xyz only, Q8).
+    p = gparams()
+    _, _, _, idx_a, rej_a = oc.project(g["src"], g["tgt"], np.eye(4), p)
+    assert int(rej_a.sum()) + len(idx_a) == g["src"].shape[1] - 1
+    src = g["src"].copy()
+    src[1, 5] = np.nan
+    _, _, _, idx_b, rej_b = oc.project(src, g["tgt"], np.eye(4), p)
+    assert int(rej_b.sum()) + len(idx_b) == g["src"].shape[1] - 2
+    src = g["src"].copy()
+    src[4, 5] = np.nan
+    _, _, _, idx_c, rej_c = oc.project(src, g["tgt"], np.eye(4), p)
+    assert int(rej_c.sum()) + len(idx_c) == g["src"].shape[1] - 1
+
+
+def test_glibc_rand_restatement_matches_libc():
+    libc = ctypes.CDLL("libc.so.6")
+    for seed in (1, 12345, 2**31 + 7):
+        libc.srand(ctypes.c_uint(seed))
+        want = [libc.rand() for _ in range(500)]
+        got = oc.rand_sequence(seed, 500)
+        assert list(got) == want
+
+
+def test_exact_knn_matches_bruteforce():
+    rng = np.random.default_rng(3)
+    tgt = np.zeros((6, 3000), np.float32)
+    tgt[:3] = rng.uniform(-5, 5, (3, 3000))
+    tgt[5] = 1
+    q = rng.uniform(-5, 5, (3, 200)).astype(np.float32)
+    q[:, 0] = tgt[:3, 17]            # exact duplicate: self-match semantics
+    for allow in (0, 1):
+        d2, idx = oc.knn(tgt, q, 20, 1.5, allow)
+        for j in range(q.shape[1]):
+            d = imls_np.exact_d2(q[:, j].astype(np.float64), tgt[:3].T)
+            m = d <= 1.5 * 1.5
+            if not allow:
+                m &= d > np.finfo(np.float64).eps
+            cand = np.nonzero(m)[0]
+            order = cand[np.lexsort((cand, d[cand]))][:20]
+            assert np.array_equal(idx[j, :len(order)], order)
+            assert np.all(idx[j, len(order):] == -1) and np.all(np.isinf(d2[j, len(order):]))
+            assert np.array_equal(d2[j, :len(order)], d[order])
+    d2, idx = oc.knn(tgt, q[:, :1], 1, 1.5, 0)
+    assert idx[0, 0] != 17           # NN-1 without ALLOW_SELF_MATCH skips the zero-distance point
+
+
+# ------------------------------------------------------------------------------------------------
+# Analytic known-answer tests
+# ------------------------------------------------------------------------------------------------
+def plane_map(spacing=0.1, half=3.0, seed=0):
+    rng = np.random.default_rng(seed)
+    g = np.arange(-half, half + 1e-9, spacing)
+    X, Y = np.meshgrid(g, g)
+    X = X + rng.uniform(-0.01, 0.01, X.shape)
+    Y = Y + rng.uniform(-0.01, 0.01, Y.shape)
+    n = X.size
+    t = np.zeros((6, n), np.float32)
+    t[0], t[1], t[5] = X.ravel(), Y.ravel(), 1.0
+    return t
+
+
+def src_points(pts, normals=None):
+    pts = np.atleast_2d(np.asarray(pts, np.float32))
+    s = np.zeros((6, len(pts)), np.float32)
+    s[:3] = pts.T
+    s[3:] = (np.asarray(normals, np.float32).T if normals is not None else np.array([[0], [0], [1]], np.float32))
+    return s
+
+
+def test_kat_plane_height():
+    tgt = plane_map()
+    p = gparams()
+    z0 = 0.35
+    x, y, n, idx, rej = oc.project(src_points([[0.123, -0.07, z0]]), tgt, np.eye(4), p)
+    assert len(idx) == 1
+    # height = z0·Σw/(Σw+1e-5) ⇒ y_z = z0 − height = z0·1e-5/(Σw+1e-5)
+    q = np.array([0.123, -0.07, z0], np.float32).astype(np.float64)
+    d = imls_np.exact_d2(q, tgt[:3].T)
+    order = np.lexsort((np.arange(d.size), d))[:20]
+    hmax = math.sqrt(d[order[19]]) / 3
+    w = np.exp(-d[order] / hmax / hmax)
+    height = float(np.sum(w * z0)) / (float(np.sum(w)) + 1e-5)
+    assert abs(float(y[0, 2]) - np.float32(z0 - height)) <= 1e-7
+    assert abs(float(y[0, 2]) - z0 * 1e-5 / (float(np.sum(w)) + 1e-5)) <= 1e-7   # the Q4 bias, analytically
+
+
+def test_kat_pure_translation_ls():
+    rng = np.random.default_rng(5)
+    t = np.array([0.31, -0.12, 0.05])
+    s, n = [], []
+    for axis in range(3):
+        for _ in range(40):
+            pnt = rng.uniform(-10, 10, 3)
+            nv = np.zeros(3)
+            nv[axis] = 1
+            s.append(pnt)
+            n.append(nv)
+    s, n = np.array(s), np.array(n)
+    d = s + t
+    p = gparams()
+    ok, D = oc.solve(_abi.IMLS_SOLVE_LS, s, d, n, p)
+    assert ok
+    assert np.abs(D[:3, 3] - t).max() < 1e-12
+    assert np.abs(D[:3, :3] - np.eye(3)).max() < 1e-12
+
+
+@pytest.mark.parametrize("N,kept", [(6, 6), (7, 7), (50, 49), (51, 49), (100, 97)])
+def test_kat_trimmed_ls_rank_bounds(N, kept):
+    lo, hi = int(0.02 * N), min(int((1 - 0.02) * N), N - 1)
+    assert hi - lo + 1 == kept
+    rng = np.random.default_rng(N)
+    s = rng.uniform(-5, 5, (N, 3))
+    n = rng.normal(size=(N, 3))
+    n /= np.linalg.norm(n, axis=1, keepdims=True)
+    d = s + 0.05 * rng.normal(size=(N, 3))
+    ok, D = oc.solve(_abi.IMLS_SOLVE_LS, s, d, n, gparams())
+    D2, k2 = imls_np.solve_ls(s, d, n, 0.02)
+    assert ok and k2 == kept
+    assert np.abs(D - D2).max() < 1e-9
+
+
+def test_kat_gates_nn_distance():
+    p = gparams()
+    # map: three points on z = 0 plus the NN candidate; h = 1 → d² = h² passes, just above fails
+    base = np.zeros((6, 4), np.float32)
+    base[5] = 1
+    for eps, expect_valid in ((0.0, True), (1e-6, False)):
+        t = base.copy()
+        t[0] = [1.0 + eps, 1.5 + eps, 1.6, 1.7]
+        t[1] = [0.0, 0.4, -0.4, 0.0]
+        x, y, n, idx, rej = oc.project(src_points([[0, 0, 0]]), t, np.eye(4), p)
+        assert (len(idx) == 1) == expect_valid, (eps, rej)
+        if not expect_valid:
+            assert rej[_abi.REJECT_NAMES.index("too_far")] == 1
+
+
+def test_kat_gates_angle_and_mls_count():
+    p = gparams()
+    t = np.zeros((6, 3), np.float32)
+    t[0] = [0.1, 0.2, -0.15]
+    t[1] = [0.0, 0.1, 0.12]
+
+    def with_angle(deg):
+        a = math.radians(deg)
+        tt = t.copy()
+        tt[3], tt[5] = math.sin(a), math.cos(a)
+        return tt
+
+    _, _, _, idx, rej = oc.project(src_points([[0, 0, 0.05]]), with_angle(29.9), np.eye(4), p)
+    assert len(idx) == 1
+    _, _, _, idx, rej = oc.project(src_points([[0, 0, 0.05]]), with_angle(30.1), np.eye(4), p)
+    assert len(idx) == 0 and rej[_abi.REJECT_NAMES.index("normal_constraint")] == 1
+    # |S| = 2 → MLS failure
+    _, _, _, idx, rej = oc.project(src_points([[0, 0, 0.05]]), t[:, :2].copy(), np.eye(4), p)
+    assert len(idx) == 0 and rej[_abi.REJECT_NAMES.index("mls_fail")] == 1
+
+
+def test_kat_hmax_quirk_indexes_sorted_list():
+    """Q3: h_max = √L[|S|−1]/3 uses the sorted candidate list, not the accepted set."""
+    p = gparams()
+    t = np.zeros((6, 5), np.float32)
+    t[0] = [0.1, 0.2, 0.3, 0.4, 0.5]
+    t[5] = 1.0
+    # the second-nearest point's normal violates the angle gate → S = {0, 2, 3, 4}
+    t[3, 1], t[5, 1] = 1.0, 0.0
+    q = np.array([0.0, 0.0, 0.02], np.float32)
+    x, y, n, idx, rej = oc.project(src_points([q]), t, np.eye(4), p)
+    assert len(idx) == 1
+    qd = q.astype(np.float64)
+    d = imls_np.exact_d2(qd, t[:3].T)
+    hmax = math.sqrt(d[3]) / 3              # L[|S|−1] = L[3] (not the 4th accepted, which is L[4])
+    S = [0, 2, 3, 4]
+    w = np.exp(-d[S] / hmax / hmax)
+    height = float(np.sum(w * qd[2])) / (float(np.sum(w)) + 1e-5)
+    assert float(y[0, 2]) == np.float32(qd[2] - height)
+
+
+def test_colpiv_qr_basic_solution_3x6():
+    rng = np.random.default_rng(11)
+    A = rng.normal(size=(3, 6))
+    b = rng.normal(size=3)
+    x = oc.colpiv_qr_solve(A, b)
+    assert np.abs(A @ x - b).max() < 1e-12
+    assert np.count_nonzero(x) == 3          # basic solution: non-pivot unknowns are zero
+    # full-rank overdetermined: equals the least-squares solution
+    A = rng.normal(size=(40, 6))
+    b = rng.normal(size=40)
+    x = oc.colpiv_qr_solve(A, b)
+    assert np.abs(x - np.linalg.lstsq(A, b, rcond=None)[0]).max() < 1e-12
+
+
+def test_delta_from_x_is_rodrigues():
+    from scipy.spatial.transform import Rotation
+    for x in ([0, 0, 0, 1, 2, 3], [0.01, -0.02, 0.3, 0, 0, 0], [1.0, 0.5, -0.25, 0.1, 0.1, 0.1]):
+        D = oc.delta_from_x(np.array(x, float))
+        assert np.abs(D[:3, :3] - Rotation.from_rotvec(x[:3]).as_matrix()).max() < 1e-14
+        assert np.array_equal(D[:3, 3], np.array(x[3:], float))
+
+
+def test_ransac_variants_run_and_are_deterministic():
+    g = golden("vlp16_pair")
+    s, d, n = g["x1"], g["y1"], g["n1"]
+    p = gparams()
+    for final in (_abi.IMLS_FINAL_LS, _abi.IMLS_FINAL_WEIGHTED_LS, _abi.IMLS_FINAL_DRPM):
+        p.ransac_final_method = final
+        ok1, D1 = oc.solve(_abi.IMLS_SOLVE_RANSAC, s, d, n, p)
+        ok2, D2 = oc.solve(_abi.IMLS_SOLVE_RANSAC, s, d, n, p)
+        okl, DL = oc.solve(_abi.IMLS_SOLVE_LS, s, d, n, p)
+        assert ok1 and ok2 and np.array_equal(D1, D2)
+        assert np.abs(D1[:3, 3] - DL[:3, 3]).max() < 0.05
+
+
+def test_weighted_ls_matches_numpy():
+    g = golden("vlp16_pair")
+    s, d, n = g["x0"].astype(np.float64), g["y0"].astype(np.float64), g["n0"].astype(np.float64)
+    w = np.random.default_rng(2).uniform(0.1, 1.0, len(s))
+    ok, D = oc.solve(_abi.IMLS_SOLVE_WEIGHTED_LS, s, d, n, gparams(), weights=w)
+    assert ok and np.abs(D - imls_np.solve_wls(s, d, n, w)).max() < 1e-9
