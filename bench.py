@@ -138,6 +138,8 @@ def main():
     idx_ms, idx_n = ctx.kernel_timing(1)
     sol_ms, sol_n = ctx.kernel_timing(2)
     stats = ctx.index_stats()
+    trav = ctx.traversal_stats()
+    log(f"[rank {rank}] traversal (last frame, {args.iters} iterations): {trav}")
     bytes_launch = algorithmic_bytes_per_launch(stats, res["trace"], args.iters)
     avg_proj_s = proj_ms / max(proj_n, 1) / 1e3
     achieved = bytes_launch / avg_proj_s / 1e9 if avg_proj_s > 0 else 0.0
@@ -206,6 +208,7 @@ def main():
             "projection": proj_ms / max(args.steps, 1),
             "solve_chain": sol_ms / max(args.steps, 1),
         },
+        "traversal_per_launch": {k: v / args.iters for k, v in trav.items()},
         "cpu_baseline": cpu,
         "final_pose_error_cm": float(err * 100),
     }

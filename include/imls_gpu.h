@@ -225,6 +225,10 @@ int imls_reset_timing(imls_ctx* ctx);
 /* Sizes of the last built index (for roofline accounting): points, leaves, tree levels,
  * total neighbours visited in the last projection (Σ k_q), queries passing the NN/angle gates. */
 int imls_index_stats(imls_ctx* ctx, uint64_t out[8]);
+/* Counters accumulated since the last frame start / projection (diagnostics): Σ k_q, NN-1 found,
+ * leaves visited (per wave), inner nodes visited (per wave), waves, uncertified queries re-run
+ * exactly, 0, 0. */
+int imls_traversal_stats(imls_ctx* ctx, uint64_t out[8]);
 
 #ifdef __cplusplus
 }

@@ -114,6 +114,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_kernel_timing": (C.c_int, [VP, C.c_int, P(C.c_double), P(C.c_uint64)]),
         "imls_reset_timing": (C.c_int, [VP]),
         "imls_index_stats": (C.c_int, [VP, VP]),
+        "imls_traversal_stats": (C.c_int, [VP, VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -128,7 +129,7 @@ ABI_SYMBOLS = (
     "imls_set_target_device", "imls_set_source_device", "imls_project", "imls_solve",
     "imls_solve_correspondences", "imls_register_frame", "imls_register_frame_async",
     "imls_register_frame_result", "imls_enable_timing", "imls_kernel_timing", "imls_reset_timing",
-    "imls_index_stats",
+    "imls_index_stats", "imls_traversal_stats",
 )
 
 _LIB = None

@@ -22,11 +22,15 @@ struct imls_ctx {
     std::string err;
     int B = 32;
     // target
-    DevBuf tpt, tnr, mpt, nodes, tscratch, upload_t;
+    DevBuf tpt, tnr, mpt, nodes, tscratch, treescratch, permbuf, upload_t;
     int M = 0, Pl = 0, levels = 0;
     bool has_target = false;
     // source
-    DevBuf spt, snr, sscratch, upload_s;
+    DevBuf spt, snr, sscratch, qperm, upload_s;
+    DevBuf fb;                            // fallback query list + count
+    DevBuf prevnn;                        // per-query neighbour lists carried between ICP iterations
+    int lane_mode = 0;
+    int temporal_seed = 1;
     int N = 0;
     bool has_source = false;
     // correspondences + solver state
@@ -100,7 +104,9 @@ int check_params(imls_ctx* c, const imls_params* p) {
 int ensure_solve(imls_ctx* c, int N) {
     if (c->st_N >= N && c->st.trace) return IMLS_OK;
     size_t n = (size_t)std::max(N, 1);
-    if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
+    if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, n * 4 + 256))
+        return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
+    if (!grow(c->prevnn, n * kMaxKL * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
     const int pb = std::max(project_blocks((int)n), solve_blocks((int)n)) + 1;
     size_t bytes = 0;
     auto add = [&](size_t b) { size_t o = bytes; bytes += (b + 255) / 256 * 256; return o; };
@@ -143,6 +149,9 @@ int ensure_trace(imls_ctx* c, int iters) {
     c->trace_cap = std::max(iters, 1);
     return IMLS_OK;
 }
+
+unsigned* fb_count(imls_ctx* c) { return (unsigned*)c->fb.p; }
+unsigned* fb_list(imls_ctx* c) { return (unsigned*)c->fb.p + 64; }
 
 TreeView tree_view(imls_ctx* c) {
     TreeView t;
@@ -215,8 +224,8 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
 int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
     int slot;
     timed_begin(c, 1, slot);
-    int rc = build_target_index(c->stream, d_soa6, n, c->B, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch, &c->M, &c->Pl,
-                                &c->levels, c->err);
+    int rc = build_target_index(c->stream, d_soa6, n, c->B, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch,
+                                c->treescratch, c->permbuf, &c->M, &c->Pl, &c->levels, c->err);
     timed_end(c, 1, slot);
     if (rc) return rc;
     c->has_target = c->M > 0;
@@ -227,7 +236,8 @@ int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
 
 int do_set_source(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept, uint32_t* kept_index) {
     std::vector<uint32_t> kept;
-    int rc = load_source(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, &c->N, kept_index ? &kept : nullptr, c->err);
+    int rc = load_source(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, c->qperm, &c->N,
+                         kept_index ? &kept : nullptr, c->err);
     if (rc) return rc;
     if (kept_index && !kept.empty()) std::memcpy(kept_index, kept.data(), kept.size() * 4);
     c->has_source = c->N > 0;
@@ -308,8 +318,10 @@ imls_ctx* imls_create(int device, const imls_params* p) {
     }
     if (const char* b = std::getenv("IMLS_BUCKET")) {
         int v = std::atoi(b);
-        if (v >= 4 && v <= 256 && (v & (v - 1)) == 0) c->B = v;
+        if (v >= 4 && v <= 64 && (v & (v - 1)) == 0) c->B = v;   // a leaf is one wave-wide load
     }
+    if (const char* m = std::getenv("IMLS_TRAVERSAL")) c->lane_mode = std::string(m) == "lane";
+    if (const char* m = std::getenv("IMLS_TEMPORAL_SEED")) c->temporal_seed = std::atoi(m) != 0;
     imls_params d;
     imls_default_params(&d);
     d.solve_method = IMLS_SOLVE_LS;
@@ -324,7 +336,8 @@ void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->upload_t, &c->spt, &c->snr, &c->sscratch,
+    DevBuf* bufs[] = {&c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
+                      &c->upload_t, &c->spt, &c->snr, &c->sscratch,
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -390,18 +403,19 @@ int imls_project(imls_ctx* c, const double pose[16], float* x_out, float* y_out,
     if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
     if (int rc = check_device(c)) return rc;
     if (int rc = ensure_solve(c, c->N)) return rc;
-    if (!grow(c->pose_tmp, 32 * 8) || !grow(c->stats, 64)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");
+    if (!grow(c->pose_tmp, 32 * 8) || !grow(c->stats, 128)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");
     double* dpose = (double*)c->pose_tmp.p;
     int* dzero = (int*)(dpose + 16);
     hipMemcpyAsync(dpose, pose, 16 * 8, hipMemcpyHostToDevice, c->stream);
     hipMemsetAsync(dzero, 0, 16, c->stream);
     hipMemsetAsync(c->st.trace, 0, sizeof(imls_iter_trace), c->stream);
-    hipMemsetAsync(c->stats.p, 0, 64, c->stream);
+    hipMemsetAsync(c->stats.p, 0, 128, c->stream);
     int slot;
     timed_begin(c, 0, slot);
-    launch_project(c->stream, tree_view(c), (const float4*)c->spt.p, (const float4*)c->snr.p, c->N, dpose, dzero, c->kp,
-                   (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p, c->st.partial1, c->st.trace,
-                   (unsigned long long*)c->stats.p);
+    launch_project(c->stream, tree_view(c), (const float4*)c->spt.p, (const float4*)c->snr.p, (const unsigned*)c->qperm.p,
+                   c->N, dpose, dzero, c->kp, (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p, c->st.partial1,
+                   c->st.trace, (unsigned long long*)c->stats.p, fb_list(c), fb_count(c), c->lane_mode,
+                   (int*)c->prevnn.p, 0);
     timed_end(c, 0, slot);
     std::vector<float> hs((size_t)c->N * 4), hd((size_t)c->N * 4), hn((size_t)c->N * 4);
     imls_iter_trace tr;
@@ -480,22 +494,23 @@ int imls_register_frame_async(imls_ctx* c) {
     if (int rc = ensure_solve(c, c->N)) return rc;
     const int iters = c->P.iterations;
     if (int rc = ensure_trace(c, iters)) return rc;
-    if (!grow(c->stats, 64)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");
+    if (!grow(c->stats, 128)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");
     static const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     hipMemcpyAsync(c->st.pose, I, sizeof(I), hipMemcpyHostToDevice, c->stream);
     hipMemsetAsync(c->st.done, 0, 16, c->stream);
     hipMemsetAsync(c->st.status, 0, 16, c->stream);
     hipMemsetAsync(c->st.iters, 0, 16, c->stream);
     hipMemsetAsync(c->trace_mem.p, 0, (size_t)std::max(iters, 1) * sizeof(imls_iter_trace), c->stream);
-    hipMemsetAsync(c->stats.p, 0, 64, c->stream);
+    hipMemsetAsync(c->stats.p, 0, 128, c->stream);
     imls_iter_trace* tr = (imls_iter_trace*)c->trace_mem.p;
     const TreeView tv = tree_view(c);
     for (int it = 0; it < iters; ++it) {
         int slot;
         timed_begin(c, 0, slot);
-        launch_project(c->stream, tv, (const float4*)c->spt.p, (const float4*)c->snr.p, c->N, c->st.pose, c->st.done, c->kp,
-                       (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p, c->st.partial1, tr + it,
-                       (unsigned long long*)c->stats.p);
+        launch_project(c->stream, tv, (const float4*)c->spt.p, (const float4*)c->snr.p, (const unsigned*)c->qperm.p, c->N,
+                       c->st.pose, c->st.done, c->kp, (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p,
+                       c->st.partial1, tr + it, (unsigned long long*)c->stats.p, fb_list(c), fb_count(c), c->lane_mode,
+                       (int*)c->prevnn.p, it > 0 && c->temporal_seed);
         timed_end(c, 0, slot);
         timed_begin(c, 2, slot);
         launch_solve_chain(c->stream, c->N, project_blocks(c->N), c->kp, (const float4*)c->cs.p, (const float4*)c->cd.p,
@@ -554,6 +569,14 @@ int imls_reset_timing(imls_ctx* c) {
     if (!c) return IMLS_ERR_ARG;
     for (int k = 0; k < 3; ++k) { c->t_ms[k] = 0; c->t_n[k] = 0; c->ev_pairs[k].clear(); }
     c->ev_used = 0;
+    return IMLS_OK;
+}
+
+int imls_traversal_stats(imls_ctx* c, uint64_t out[8]) {
+    if (!c || !out) return IMLS_ERR_ARG;
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (c->stats.p) hipMemcpy(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost);
+    for (int k = 0; k < 8; ++k) out[k] = st[k];
     return IMLS_OK;
 }
 

@@ -78,14 +78,24 @@ __global__ void k_bbox_partial(const float4* __restrict__ pt, const int* __restr
 }
 
 __global__ void k_bbox_final(const float* __restrict__ part, int nparts, float* __restrict__ bbox) {
-    if (threadIdx.x != 0) return;
+    __shared__ float red[6][kBlock];
     float r[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    for (int b = 0; b < nparts; ++b)
+    for (int b = threadIdx.x; b < nparts; b += kBlock)
         for (int d = 0; d < 3; ++d) {
             r[d] = fminf(r[d], part[b * 6 + d]);
             r[3 + d] = fmaxf(r[3 + d], part[b * 6 + 3 + d]);
         }
-    for (int d = 0; d < 6; ++d) bbox[d] = r[d];
+    for (int d = 0; d < 6; ++d) red[d][threadIdx.x] = r[d];
+    __syncthreads();
+    for (int st = kBlock / 2; st > 0; st >>= 1) {
+        if (threadIdx.x < st)
+            for (int d = 0; d < 3; ++d) {
+                red[d][threadIdx.x] = fminf(red[d][threadIdx.x], red[d][threadIdx.x + st]);
+                red[3 + d][threadIdx.x] = fmaxf(red[3 + d][threadIdx.x], red[3 + d][threadIdx.x + st]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) bbox[threadIdx.x] = red[threadIdx.x][0];
 }
 
 __device__ __forceinline__ unsigned long long spread3_16(unsigned v) {
@@ -104,10 +114,12 @@ __global__ void k_morton(const float4* __restrict__ pt, const int* __restrict__ 
     if (i >= M) return;
     float4 p = pt[i];
     const float qmax = 65535.f;
-    float ex = fmaxf(bbox[3] - bbox[0], 1e-6f), ey = fmaxf(bbox[4] - bbox[1], 1e-6f), ez = fmaxf(bbox[5] - bbox[2], 1e-6f);
-    unsigned qx = (unsigned)fminf(fmaxf((p.x - bbox[0]) / ex * qmax, 0.f), qmax);
-    unsigned qy = (unsigned)fminf(fmaxf((p.y - bbox[1]) / ey * qmax, 0.f), qmax);
-    unsigned qz = (unsigned)fminf(fmaxf((p.z - bbox[2]) / ez * qmax, 0.f), qmax);
+    // isotropic cells (one scale for all axes) keep Morton buckets compact
+    const float ext = fmaxf(fmaxf(fmaxf(bbox[3] - bbox[0], bbox[4] - bbox[1]), bbox[5] - bbox[2]), 1e-6f);
+    const float sc = qmax / ext;
+    unsigned qx = (unsigned)fminf(fmaxf((p.x - bbox[0]) * sc, 0.f), qmax);
+    unsigned qy = (unsigned)fminf(fmaxf((p.y - bbox[1]) * sc, 0.f), qmax);
+    unsigned qz = (unsigned)fminf(fmaxf((p.z - bbox[2]) * sc, 0.f), qmax);
     key[i] = spread3_16(qx) | (spread3_16(qy) << 1) | (spread3_16(qz) << 2);
     val[i] = (unsigned)i;
 }
@@ -206,11 +218,38 @@ int filter_compact(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, 
     return IMLS_OK;
 }
 
+// Permutation (sorted → input index) of n float4 points by 48-bit Morton code over their bbox.
+int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf& perm, std::string& err) {
+    size_t cub_bytes = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                       (unsigned*)nullptr, (unsigned*)nullptr, n, 0, 48, s);
+    const int bb_parts = 512;
+    size_t need = 2 * (((size_t)n * 8 + 255) / 256 * 256) + (((size_t)n * 4 + 255) / 256 * 256) +
+                  ((cub_bytes + 255) / 256) * 256 + bb_parts * 24 + 1024;
+    if (!ensure(scratch, need, err) || !ensure(perm, (size_t)n * 4 + 16, err)) return IMLS_ERR_DEVICE;
+    char* p = (char*)scratch.p;
+    unsigned long long* k0 = carve<unsigned long long>(p, n);
+    unsigned long long* k1 = carve<unsigned long long>(p, n);
+    unsigned* v0 = carve<unsigned>(p, n);
+    void* cub_tmp = carve<char>(p, cub_bytes);
+    float* bbpart = carve<float>(p, bb_parts * 6);
+    float* bbox = carve<float>(p, 8);
+    int* cnt = carve<int>(p, 4);
+    hipMemcpyAsync(cnt, &n, sizeof(int), hipMemcpyHostToDevice, s);
+    int nb = std::min(bb_parts, (int)grid_for(n));
+    k_bbox_partial<<<nb, kBlock, 0, s>>>(pts, cnt, bbpart);
+    k_bbox_final<<<1, kBlock, 0, s>>>(bbpart, nb, bbox);
+    k_morton<<<grid_for(n), kBlock, 0, s>>>(pts, cnt, bbox, k0, v0);
+    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, (unsigned*)perm.p, n, 0, 48, s);
+    if (hipGetLastError() != hipSuccess) { err = "morton sort launch failed"; return IMLS_ERR_DEVICE; }
+    return IMLS_OK;
+}
+
 }  // namespace
 
 int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket, DevBuf& tpt, DevBuf& tnr,
-                       DevBuf& mpt, DevBuf& nodes, DevBuf& scratch, int* M_out, int* P_out, int* levels_out,
-                       std::string& err) {
+                       DevBuf& mpt, DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* M_out,
+                       int* P_out, int* levels_out, std::string& err) {
     if (n_in == 0 || n_in > (size_t)0x7fffffff) { err = "target size out of range"; return IMLS_ERR_ARG; }
     int M = 0;
     int rc = filter_compact(s, d_soa6, n_in, tpt, tnr, scratch, &M, nullptr, err);
@@ -222,35 +261,17 @@ int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int buck
     int P = 1, levels = 0;
     while (P < L) { P <<= 1; ++levels; }
     if (levels > kStackDepth - 1) { err = "tree too deep for the traversal stack"; return IMLS_ERR_CAPACITY; }
-    size_t cub_bytes = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                       (unsigned*)nullptr, (unsigned*)nullptr, M, 0, 48, s);
-    const int bb_parts = 512;
-    size_t need = 2 * (((size_t)M * 8 + 255) / 256 * 256) + 2 * (((size_t)M * 4 + 255) / 256 * 256) +
-                  ((cub_bytes + 255) / 256) * 256 + ((size_t)P * 24 + 255) / 256 * 256 +
-                  2 * (((size_t)P / kBlock + 1) * 24 + 256) + bb_parts * 24 + 1024;
-    if (!ensure(scratch, need, err) || !ensure(mpt, (size_t)M * 16 + 16, err) ||
+    rc = morton_perm(s, (const float4*)tpt.p, M, scratch, permbuf, err);
+    if (rc) return rc;
+    size_t need = ((size_t)P * 24 + 255) / 256 * 256 + 2 * (((size_t)P / kBlock + 1) * 24 + 256) + 1024;
+    if (!ensure(treescratch, need, err) || !ensure(mpt, (size_t)M * 16 + 16, err) ||
         !ensure(nodes, (size_t)(P + 1) * 48, err))
         return IMLS_ERR_DEVICE;
-    char* p = (char*)scratch.p;
-    unsigned long long* k0 = carve<unsigned long long>(p, M);
-    unsigned long long* k1 = carve<unsigned long long>(p, M);
-    unsigned* v0 = carve<unsigned>(p, M);
-    unsigned* v1 = carve<unsigned>(p, M);
-    void* cub_tmp = carve<char>(p, cub_bytes);
+    char* p = (char*)treescratch.p;
     float* leafbox = carve<float>(p, (size_t)P * 6);
     float* rootsA = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
     float* rootsB = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
-    float* bbpart = carve<float>(p, bb_parts * 6);
-    float* bbox = carve<float>(p, 8);
-    int* cnt = carve<int>(p, 4);
-    hipMemcpyAsync(cnt, &M, sizeof(int), hipMemcpyHostToDevice, s);
-    int nb = std::min(bb_parts, (int)grid_for(M));
-    k_bbox_partial<<<nb, kBlock, 0, s>>>((const float4*)tpt.p, cnt, bbpart);
-    k_bbox_final<<<1, 64, 0, s>>>(bbpart, nb, bbox);
-    k_morton<<<grid_for(M), kBlock, 0, s>>>((const float4*)tpt.p, cnt, bbox, k0, v0);
-    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, v1, M, 0, 48, s);
-    k_gather<<<grid_for(M), kBlock, 0, s>>>((const float4*)tpt.p, v1, M, (float4*)mpt.p);
+    k_gather<<<grid_for(M), kBlock, 0, s>>>((const float4*)tpt.p, (const unsigned*)permbuf.p, M, (float4*)mpt.p);
     k_leaf_boxes<<<grid_for(P), kBlock, 0, s>>>((const float4*)mpt.p, M, B, P, leafbox);
     // bottom-up subtree reduction, 256 boxes per block per launch
     const float* in = leafbox;
@@ -274,7 +295,7 @@ int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int buck
 }
 
 int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, DevBuf& snr, DevBuf& scratch,
-                int* N_out, std::vector<uint32_t>* kept, std::string& err) {
+                DevBuf& qperm, int* N_out, std::vector<uint32_t>* kept, std::string& err) {
     if (n_in == 0 || n_in > (size_t)0x7fffffff) { err = "source size out of range"; return IMLS_ERR_ARG; }
     DevBuf keptbuf;
     unsigned* dk = nullptr;
@@ -290,6 +311,7 @@ int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, De
     }
     if (keptbuf.p) (void)hipFree(keptbuf.p);
     *N_out = N;
+    if (!rc && N > 0) rc = morton_perm(s, (const float4*)spt.p, N, scratch, qperm, err);
     return rc;
 }
 

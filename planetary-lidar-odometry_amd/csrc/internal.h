@@ -81,14 +81,21 @@ struct SolveState {
 // index.hip
 int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket,
                        DevBuf& tpt, DevBuf& tnr, DevBuf& mpt, DevBuf& nodes, DevBuf& scratch,
-                       int* M_out, int* P_out, int* levels_out, std::string& err);
+                       DevBuf& treescratch, DevBuf& permbuf, int* M_out, int* P_out, int* levels_out,
+                       std::string& err);
+// also computes qperm: the source in Morton order (query order of the wave kernel)
 int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, DevBuf& snr,
-                DevBuf& scratch, int* N_out, std::vector<uint32_t>* kept, std::string& err);
+                DevBuf& scratch, DevBuf& qperm, int* N_out, std::vector<uint32_t>* kept, std::string& err);
 
 // project.hip
-void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const float4* snr, int N,
-                    const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd,
-                    float4* cn, double* partial1, imls_iter_trace* tr, unsigned long long* nbr_stats);
+// k_project_wave (+ the exact k_project_lane fallback for uncertified queries); lane_mode runs
+// every query through k_project_lane.  partial1 receives project_blocks(N) slabs.
+void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const float4* snr,
+                    const unsigned* qperm, int N, const double* pose, const int* done, const KParams& kp,
+                    float4* cs, float4* cd, float4* cn, double* partial1, imls_iter_trace* tr,
+                    unsigned long long* nbr_stats, unsigned* fb_list, unsigned* fb_count, int lane_mode,
+                    int* prevnn, int use_prev);   // prevnn: [kMaxKL][N] list positions across iterations
+constexpr int kMaxKL = 36;
 int project_blocks(int N);
 
 // solve.hip

@@ -1,23 +1,29 @@
-// project.hip — fused transform + matching kernel: the GPU form of one ICP iteration's
-// Matching step (laser_odometry.cpp:527-549 → IMLSICPMatcher::ProjSourcePtToSurface,
-// imls_icp.cpp:496-745 → ImplicitMLSFunction, imls_icp.cpp:301-483).
+// project.hip — fused transform + matching kernels: the GPU form of one ICP iteration's Matching
+// step (laser_odometry.cpp:527-549 → IMLSICPMatcher::ProjSourcePtToSurface, imls_icp.cpp:496-745
+// → ImplicitMLSFunction, imls_icp.cpp:301-483).
 //
-// One lane per source point:
-//   1. x = float(rPose·[p;1])  (double, the reference's evaluation order, no FMA)
-//   2. one traversal of the target tree collecting, in registers,
-//        NN-1 : nearest map point within r with d² > DBL_EPSILON   (knn K=1, no self match,
-//               imls_icp.cpp:605-607)
-//        L    : the K nearest within r, sorted by (d², index)      (knn K=search_number,
-//               ALLOW_SELF_MATCH, imls_icp.cpp:372-375)
-//      Candidates are screened with an fp32 distance against the current bound (× (1+2e-6)
-//      slack, so no exact candidate is ever screened out) and ranked by the exact fp64 distance
-//      ((dx²+dy²)+dz², the libnabo metric), so the neighbour sets equal the oracle's.
-//   3. the gates of imls_icp.cpp:612-717 in the reference order, the IMLS height with the
-//      h_max quirk (Q3) and the 1e-5 bias (Q4), y = float(x − height·n_NN).
-//   4. outputs per source index (source order is the index; compaction is separate), reject
-//      counters, and the pass-1 normal-equation partials of the LS solve (solver.cpp:89-107)
-//      reduced per block: 21 JᵀJ + 6 Jᵀb + count, fp64.
-// Compiled with -ffp-contract=off: every fp64 expression is evaluated as written.
+// k_project_wave (the hot kernel) — wave-coherent ("packet") traversal:
+//   * a wave owns 64 queries taken in Morton order of the source scan, so they are neighbours;
+//   * ONE traversal per wave of the target tree: the node index and the LDS stack are
+//     wave-uniform (node records come through the scalar cache), a child is entered when any
+//     lane's box distance is within that lane's bound (ballot), near-first by lane majority;
+//   * a leaf (B ≤ 64 Morton-consecutive map points) is ONE coalesced float4 load, each point is
+//     broadcast to all lanes by v_readlane and tested against each lane's own list;
+//   * per lane, a register top-(K+4) list keyed by the fp32 distance (query-relative, FMA);
+//   * then the exact stage: fp64 distances ((dx²+dy²)+dz², the libnabo metric, no FMA) of the
+//     list, sorted by (d², index), the radius filter (d² ≤ r², inclusive), NN-1 = first entry
+//     with d² > DBL_EPSILON (no self match, imls_icp.cpp:605-607), L = first K
+//     (ALLOW_SELF_MATCH, imls_icp.cpp:372-375);
+//   * CERTIFICATION: every map point outside the list has d²₆₄ ≥ W/(1+3.1e-7), W = the list's
+//     worst fp32 key (|d²₃₂ − d²₆₄| ≤ 5·2⁻²⁴·d²); the result is exact iff the largest exact
+//     distance it relies on is < W/(1+4e-7).  Uncertified queries (near-ties at the list edge,
+//     > K+4 duplicates) are appended to a list that k_project_lane re-runs exactly.
+// k_project_lane — one lane per query, exact fp64 list during the traversal (the fallback,
+// and the IMLS_TRAVERSAL=lane reference mode).
+// Both end in the same gates (imls_icp.cpp:612-717 in order), IMLS height with the h_max quirk
+// (Q3) and the 1e-5 bias (Q4), y = float(x − height·n_NN), and the pass-1 normal-equation
+// partials of the LS solve (solver.cpp:89-107): 21 JᵀJ + 6 Jᵀb + count per block, fp64.
+// Compiled with -ffp-contract=off: every fp64 expression evaluates as written.
 #include <cfloat>
 
 #include "internal.h"
@@ -26,16 +32,30 @@ namespace imlsgpu {
 namespace {
 
 constexpr double kInfD = __builtin_huge_val();
+constexpr float kInfF = __builtin_huge_valf();
+constexpr int kWaveBlock = 256;
+constexpr int kFallbackBlocks = 64;
+constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
+constexpr double kCertSlack = 1.0 + 4e-7;
 
 __device__ __forceinline__ bool lessp(double da, int ia, double db, int ib) {
     return da < db || (da == db && ia < ib);
 }
 
 __device__ __forceinline__ float box_d2(const float q[3], float lx, float ly, float lz, float hx, float hy, float hz) {
-    float vx = fmaxf(fmaxf(lx - q[0], q[0] - hx), 0.f);
-    float vy = fmaxf(fmaxf(ly - q[1], q[1] - hy), 0.f);
-    float vz = fmaxf(fmaxf(lz - q[2], q[2] - hz), 0.f);
+    const float vx = fmaxf(fmaxf(lx - q[0], q[0] - hx), 0.f);
+    const float vy = fmaxf(fmaxf(ly - q[1], q[1] - hy), 0.f);
+    const float vz = fmaxf(fmaxf(lz - q[2], q[2] - hz), 0.f);
     return __builtin_fmaf(vx, vx, __builtin_fmaf(vy, vy, vz * vz));
+}
+
+// exact libnabo metric on float storage
+__device__ __forceinline__ double exact_d2(const double xd[3], float px, float py, float pz) {
+    const double dx = xd[0] - (double)px, dy = xd[1] - (double)py, dz = xd[2] - (double)pz;
+    double d2 = dx * dx;
+    d2 = d2 + dy * dy;
+    d2 = d2 + dz * dz;
+    return d2;
 }
 
 // imls_icp.cpp:442-451 / 681-692: acos(ns·n/(|ns||n|))·180/π > threshold; NaN passes (Q8).
@@ -49,9 +69,32 @@ __device__ __forceinline__ bool angle_reject(const double ns[3], double n0, doub
     double b = n0 * n0;
     b = b + n1 * n1;
     b = b + n2 * n2;
-    double ca = dot / (sqrt(a) * sqrt(b));
-    double angle = acos(ca) * 180.0 / M_PI;
+    const double ca = dot / (sqrt(a) * sqrt(b));
+    const double angle = acos(ca) * 180.0 / M_PI;
     return angle > thr;
+}
+
+template <int KL>
+__device__ __forceinline__ bool contains(const int (&lp)[KL], int pos) {
+    bool f = false;
+#pragma unroll
+    for (int k = 0; k < KL; ++k) f |= lp[k] == pos;
+    return f;
+}
+
+// Insert (d, pos) into the ascending top-KL list (precondition: d < lk[KL−1]).
+template <int KL>
+__device__ __forceinline__ void insert_top(float (&lk)[KL], int (&lp)[KL], float d, int pos) {
+    bool prev = true;   // prev = d < lk[k] (old value), i.e. the shift decision of slot k+1
+#pragma unroll
+    for (int k = KL - 1; k >= 0; --k) {
+        const bool sh = (k > 0) ? (d < lk[(k > 0) ? k - 1 : 0]) : false;
+        const float nk = sh ? lk[(k > 0) ? k - 1 : 0] : fminf(d, lk[k]);
+        const int np = sh ? lp[(k > 0) ? k - 1 : 0] : (prev ? pos : lp[k]);
+        lk[k] = nk;
+        lp[k] = np;
+        prev = sh;
+    }
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -60,232 +103,113 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-template <int KCAP>
-__global__ __launch_bounds__(kProjBlock) void k_project(TreeView t, const float4* __restrict__ spt,
-                                                        const float4* __restrict__ snr, int N,
-                                                        const double* __restrict__ pose, const int* __restrict__ done,
-                                                        KParams kp, float4* __restrict__ cs, float4* __restrict__ cd,
-                                                        float4* __restrict__ cn, double* __restrict__ partial1,
-                                                        imls_iter_trace* __restrict__ tr,
-                                                        unsigned long long* __restrict__ nbr_stats) {
-    if (done && *done) return;
-    __shared__ uint2 stack[kStackDepth][kProjBlock];
-    __shared__ double red[kProjBlock / 64][kNormEq];
-    __shared__ unsigned rej_s[IMLS_NUM_REJ + 3];
-    const int tid = threadIdx.x;
-    if (tid < IMLS_NUM_REJ + 3) rej_s[tid] = 0;
-    __syncthreads();
-
-    const int i = blockIdx.x * kProjBlock + tid;
-    const bool active = i < N;
-    int cat = -2;
-    float xf[3] = {0, 0, 0}, yf[3] = {0, 0, 0}, nf[3] = {0, 0, 0};
-    int kq = 0, nn_found = 0;
-    if (active) {
-        double T[12];
+// x = float(rPose·[p;1]) and the (optionally rotated) source normal (laser_odometry.cpp:527-549)
+__device__ __forceinline__ void transform_query(const double* __restrict__ pose, float4 p, float4 nsv, int rot_normal,
+                                                float xf[3], double ns[3]) {
+    double T[12];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) T[k] = pose[k];
-        const float4 p = spt[i];
-        const float4 nsv = snr[i];
-        const double pd[3] = {p.x, p.y, p.z};
+    for (int k = 0; k < 12; ++k) T[k] = pose[k];
+    const double pd[3] = {p.x, p.y, p.z};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        double v = T[r * 4 + 0] * pd[0];
+        v = v + T[r * 4 + 1] * pd[1];
+        v = v + T[r * 4 + 2] * pd[2];
+        v = v + T[r * 4 + 3] * 1.0;
+        xf[r] = (float)v;
+    }
+    if (rot_normal) {
+        const double nd[3] = {nsv.x, nsv.y, nsv.z};
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-            double v = T[r * 4 + 0] * pd[0];
-            v = v + T[r * 4 + 1] * pd[1];
-            v = v + T[r * 4 + 2] * pd[2];
-            v = v + T[r * 4 + 3] * 1.0;
-            xf[r] = (float)v;
+            double v = T[r * 4 + 0] * nd[0];
+            v = v + T[r * 4 + 1] * nd[1];
+            v = v + T[r * 4 + 2] * nd[2];
+            ns[r] = (double)(float)v;
         }
-        float nsf[3] = {nsv.x, nsv.y, nsv.z};
-        if (kp.transform_normal) {
-            const double nd[3] = {nsv.x, nsv.y, nsv.z};
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                double v = T[r * 4 + 0] * nd[0];
-                v = v + T[r * 4 + 1] * nd[1];
-                v = v + T[r * 4 + 2] * nd[2];
-                nsf[r] = (float)v;
-            }
-        }
-        const double xd[3] = {xf[0], xf[1], xf[2]};
-        const double ns[3] = {nsf[0], nsf[1], nsf[2]};
-
-        // ---------------- traversal: NN-1 + sorted K list ----------------
-        const int K = kp.K;
-        double ld[KCAP];
-        int li[KCAP];
-#pragma unroll
-        for (int j = 0; j < KCAP; ++j) {
-            const bool sentinel = j < KCAP - K;   // capacity K inside KCAP registers
-            ld[j] = sentinel ? -1.0 : kInfD;
-            li[j] = sentinel ? -1 : 0x7fffffff;
-        }
-        double d1 = kInfD;
-        int i1 = 0x7fffffff;
-        const double r2 = kp.r2;
-        double bnd = r2;
-        float bf = (float)bnd * (1.0f + 2e-6f) + 1e-30f;
-
-        int node = 1, sp = 0;
-        const int P = t.P, B = t.B, M = t.M;
-        while (true) {
-            if (node < P) {
-                const float4* rec = t.nodes + 3 * (size_t)node;
-                const float4 a = rec[0], b = rec[1], c = rec[2];
-                const float dl = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
-                const float dr = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
-                const bool vl = dl <= bf, vr = dr <= bf;
-                if (vl && vr) {
-                    const bool lfirst = dl <= dr;
-                    stack[sp][tid] = make_uint2(lfirst ? 2 * node + 1 : 2 * node, __float_as_uint(lfirst ? dr : dl));
-                    ++sp;
-                    node = lfirst ? 2 * node : 2 * node + 1;
-                    continue;
-                }
-                node = vl ? 2 * node : (vr ? 2 * node + 1 : 0);
-                if (node) continue;
-            } else {
-                const int bucket = node - P;
-                const int s0 = bucket * B, e0 = min(s0 + B, M);
-                for (int k = s0; k < e0; ++k) {
-                    const float4 q = t.mpt[k];
-                    const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
-                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                    if (d32 > bf) continue;
-                    const double dx = xd[0] - (double)q.x, dy = xd[1] - (double)q.y, dz = xd[2] - (double)q.z;
-                    double d2 = dx * dx;
-                    d2 = d2 + dy * dy;
-                    d2 = d2 + dz * dz;
-                    if (!(d2 <= r2)) continue;
-                    const int oi = (int)__float_as_uint(q.w);
-                    bool changed = false;
-                    if (d2 > DBL_EPSILON && lessp(d2, oi, d1, i1)) { d1 = d2; i1 = oi; changed = true; }
-                    if (lessp(d2, oi, ld[KCAP - 1], li[KCAP - 1])) {
-                        bool prev = true;
-#pragma unroll
-                        for (int j = KCAP - 1; j >= 0; --j) {
-                            const bool sh = (j > 0) ? lessp(d2, oi, ld[j - 1], li[j - 1]) : false;
-                            const double nd = sh ? ld[(j > 0) ? j - 1 : 0] : (prev ? d2 : ld[j]);
-                            const int ni = sh ? li[(j > 0) ? j - 1 : 0] : (prev ? oi : li[j]);
-                            ld[j] = nd;
-                            li[j] = ni;
-                            prev = sh;
-                        }
-                        changed = true;
-                    }
-                    if (changed) {
-                        bnd = fmin(r2, fmax(ld[KCAP - 1], d1));
-                        bf = (float)bnd * (1.0f + 2e-6f) + 1e-30f;
-                    }
-                }
-                node = 0;
-            }
-            // pop
-            while (sp > 0) {
-                --sp;
-                const uint2 e = stack[sp][tid];
-                if (__uint_as_float(e.y) <= bf) { node = (int)e.x; break; }
-            }
-            if (!node) break;
-        }
-
-        // ---------------- gates (imls_icp.cpp:612-717) ----------------
-        nn_found = i1 != 0x7fffffff;
-        double nn[3] = {0, 0, 0};
-        if (!nn_found) {
-            cat = IMLS_REJ_TOO_FAR;                  // InvalidIndex → counted as too far (Q18)
-        } else if (d1 > kp.h2) {
-            cat = IMLS_REJ_TOO_FAR;
-        } else if (!kp.get_normals) {
-            cat = IMLS_REJ_INVALID_NORMAL;           // recompute path under libnabo semantics (Q1)
-        } else {
-            const float4 n4 = t.tnr[i1];
-            nn[0] = n4.x; nn[1] = n4.y; nn[2] = n4.z;
-            if (!(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) {
-                cat = IMLS_REJ_INVALID_NORMAL;
-            } else if (kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg)) {
-                cat = IMLS_REJ_NORMAL_CONSTRAINT;
-            } else {
-                // ImplicitMLSFunction: walk L in order, keep finite-d², finite-normal, angle-ok
-                unsigned acc = 0u;
-                int nacc = 0;
-#pragma unroll
-                for (int j = 0; j < KCAP; ++j) {
-                    if (j >= KCAP - K && ld[j] < kInfD) {
-                        ++kq;
-                        const float4 qn = t.tnr[li[j]];
-                        bool ok = isfinite(qn.x) && isfinite(qn.y) && isfinite(qn.z);
-                        if (ok && kp.angle_on) ok = !angle_reject(ns, qn.x, qn.y, qn.z, kp.angle_thr_deg);
-                        if (ok) { acc |= 1u << j; ++nacc; }
-                    }
-                }
-                if (nacc < 3) {
-                    cat = IMLS_REJ_MLS_FAIL;
-                } else {
-                    const int target = KCAP - K + nacc - 1;   // Q3: index into L, not into S
-                    double dsel = 0.0;
-#pragma unroll
-                    for (int j = 0; j < KCAP; ++j) dsel = (j == target) ? ld[j] : dsel;
-                    const double hmax = sqrt(dsel) / 3;
-                    double wsum = 0.0, psum = 0.0;
-#pragma unroll
-                    for (int j = 0; j < KCAP; ++j) {
-                        if (acc & (1u << j)) {
-                            const float4 qp = t.tpt[li[j]];
-                            const float4 qn = t.tnr[li[j]];
-                            const double dx = xd[0] - (double)qp.x, dy = xd[1] - (double)qp.y, dz = xd[2] - (double)qp.z;
-                            double dn = dx * dx;
-                            dn = dn + dy * dy;
-                            dn = dn + dz * dz;
-                            const double w = exp(-dn / hmax / hmax);
-                            double pr = (w * dx) * (double)qn.x;
-                            pr = pr + (w * dy) * (double)qn.y;
-                            pr = pr + (w * dz) * (double)qn.z;
-                            wsum += w;
-                            psum += pr;
-                        }
-                    }
-                    const double height = psum / (wsum + 1e-5);
-                    if (isnan(height) || isinf(height)) {
-                        cat = IMLS_REJ_NAN_INF_HEIGHT;
-                    } else {
-                        yf[0] = (float)(xd[0] - height * nn[0]);
-                        yf[1] = (float)(xd[1] - height * nn[1]);
-                        yf[2] = (float)(xd[2] - height * nn[2]);
-                        nf[0] = (float)nn[0]; nf[1] = (float)nn[1]; nf[2] = (float)nn[2];
-                        cat = -1;
-                    }
-                }
-            }
-        }
-        cs[i] = make_float4(xf[0], xf[1], xf[2], cat == -1 ? 1.f : 0.f);
-        cd[i] = make_float4(yf[0], yf[1], yf[2], 0.f);
-        cn[i] = make_float4(nf[0], nf[1], nf[2], 0.f);
+    } else {
+        ns[0] = nsv.x; ns[1] = nsv.y; ns[2] = nsv.z;
     }
+}
 
-    // ---------------- counters ----------------
-    if (cat >= 0) atomicAdd(&rej_s[cat], 1u);
-    if (active) {
-        if (kq) atomicAdd(&rej_s[IMLS_NUM_REJ], (unsigned)kq);
-        if (nn_found) atomicAdd(&rej_s[IMLS_NUM_REJ + 1], 1u);
+// Gates + ImplicitMLSFunction + projection for one query given its exact neighbour list
+// L = (ld[j], li[j]) for j ∈ [first, first+cnt) sorted by (d², index) and its NN-1 (d1, i1).
+// Returns the reject category or −1 (valid, yf/nf filled).  kq counts the returned neighbours.
+template <int CAP>
+__device__ int finish_query(const float xf[3], const double ns[3], const double (&ld)[CAP], const int (&li)[CAP],
+                            int first, int cnt, double d1, int i1, const TreeView& t, const KParams& kp, float yf[3],
+                            float nf[3], int& kq) {
+    if (i1 < 0) return IMLS_REJ_TOO_FAR;                      // InvalidIndex → counted as too far (Q18)
+    if (d1 > kp.h2) return IMLS_REJ_TOO_FAR;                  // imls_icp.cpp:620
+    if (!kp.get_normals) return IMLS_REJ_INVALID_NORMAL;      // recompute branch under libnabo semantics (Q1)
+    const float4 n4 = t.tnr[i1];
+    const double nn[3] = {n4.x, n4.y, n4.z};
+    if (!(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) return IMLS_REJ_INVALID_NORMAL;
+    if (kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg)) return IMLS_REJ_NORMAL_CONSTRAINT;
+    const double xd[3] = {xf[0], xf[1], xf[2]};
+    unsigned long long acc = 0ull;
+    int nacc = 0;
+#pragma unroll
+    for (int j = 0; j < CAP; ++j) {
+        if (j >= first && j < first + cnt) {
+            ++kq;
+            const float4 qn = t.tnr[li[j]];
+            bool ok = isfinite(qn.x) && isfinite(qn.y) && isfinite(qn.z);
+            if (ok && kp.angle_on) ok = !angle_reject(ns, qn.x, qn.y, qn.z, kp.angle_thr_deg);
+            if (ok) { acc |= 1ull << j; ++nacc; }
+        }
     }
+    if (nacc < 3) return IMLS_REJ_MLS_FAIL;                   // imls_icp.cpp:463-466
+    const int target = first + nacc - 1;                      // Q3: index into L, not into S
+    double dsel = 0.0;
+#pragma unroll
+    for (int j = 0; j < CAP; ++j) dsel = (j == target) ? ld[j] : dsel;
+    const double hmax = sqrt(dsel) / 3;
+    double wsum = 0.0, psum = 0.0;
+#pragma unroll
+    for (int j = 0; j < CAP; ++j) {
+        if (acc & (1ull << j)) {
+            const float4 qp = t.tpt[li[j]];
+            const float4 qn = t.tnr[li[j]];
+            const double dx = xd[0] - (double)qp.x, dy = xd[1] - (double)qp.y, dz = xd[2] - (double)qp.z;
+            double dn = dx * dx;
+            dn = dn + dy * dy;
+            dn = dn + dz * dz;
+            const double w = exp(-dn / hmax / hmax);
+            double pr = (w * dx) * (double)qn.x;
+            pr = pr + (w * dy) * (double)qn.y;
+            pr = pr + (w * dz) * (double)qn.z;
+            wsum += w;
+            psum += pr;
+        }
+    }
+    const double height = psum / (wsum + 1e-5);               // Q4
+    if (isnan(height) || isinf(height)) return IMLS_REJ_NAN_INF_HEIGHT;
+    yf[0] = (float)(xd[0] - height * nn[0]);                  // imls_icp.cpp:719-729
+    yf[1] = (float)(xd[1] - height * nn[1]);
+    yf[2] = (float)(xd[2] - height * nn[2]);
+    nf[0] = (float)nn[0]; nf[1] = (float)nn[1]; nf[2] = (float)nn[2];
+    return -1;
+}
 
-    // ---------------- pass-1 normal equations (solver.cpp:89-107 as JᵀJ, Jᵀb) ----------------
-    double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
-    if (cat == -1) {
-        const double s0 = xf[0], s1 = xf[1], s2 = xf[2];
-        const double d0 = yf[0], d1_ = yf[1], d2_ = yf[2];
-        const double n0 = nf[0], n1 = nf[1], n2 = nf[2];
-        a[0] = n2 * s1 - n1 * s2;
-        a[1] = n0 * s2 - n2 * s0;
-        a[2] = n1 * s0 - n0 * s1;
-        a[3] = n0; a[4] = n1; a[5] = n2;
-        bb = n0 * (d0 - s0);
-        bb = bb + n1 * (d1_ - s1);
-        bb = bb + n2 * (d2_ - s2);
-        one = 1.0;
-    }
-    const int lane = tid & 63, wv = tid >> 6;
+// Row of the point-to-plane system for a valid correspondence (solver.cpp:95-103).
+__device__ __forceinline__ void plane_row(const float xf[3], const float yf[3], const float nf[3], double a[6], double& b) {
+    const double s0 = xf[0], s1 = xf[1], s2 = xf[2];
+    const double d0 = yf[0], d1 = yf[1], d2 = yf[2];
+    const double n0 = nf[0], n1 = nf[1], n2 = nf[2];
+    a[0] = n2 * s1 - n1 * s2;
+    a[1] = n0 * s2 - n2 * s0;
+    a[2] = n1 * s0 - n0 * s1;
+    a[3] = n0; a[4] = n1; a[5] = n2;
+    b = n0 * (d0 - s0);
+    b = b + n1 * (d1 - s1);
+    b = b + n2 * (d2 - s2);
+}
+
+// Block-reduce the 28 normal-equation terms into out[0..27] (valid in threads < 28 after return).
+template <int NT>
+__device__ void block_normeq(const double a[6], double b, double one, double (*red)[kNormEq], double* out) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int k = 0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
@@ -298,7 +222,7 @@ __global__ __launch_bounds__(kProjBlock) void k_project(TreeView t, const float4
     }
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-        const double v = wave_sum(a[r] * bb);
+        const double v = wave_sum(a[r] * b);
         if (lane == 0) red[wv][21 + r] = v;
     }
     {
@@ -306,33 +230,432 @@ __global__ __launch_bounds__(kProjBlock) void k_project(TreeView t, const float4
         if (lane == 0) red[wv][27] = v;
     }
     __syncthreads();
-    if (tid < kNormEq) {
+    if (threadIdx.x < kNormEq) {
         double s = 0.0;
 #pragma unroll
-        for (int w = 0; w < kProjBlock / 64; ++w) s += red[w][tid];
-        partial1[(size_t)blockIdx.x * kNormEq + tid] = s;
+        for (int w = 0; w < NT / 64; ++w) s += red[w][threadIdx.x];
+        out[threadIdx.x] = s;
     }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void store_result(int i, int cat, const float xf[3], const float yf[3], const float nf[3],
+                                             float4* cs, float4* cd, float4* cn) {
+    cs[i] = make_float4(xf[0], xf[1], xf[2], cat == -1 ? 1.f : 0.f);
+    cd[i] = make_float4(yf[0], yf[1], yf[2], 0.f);
+    cn[i] = make_float4(nf[0], nf[1], nf[2], 0.f);
+}
+
+// =============================================================================================
+// Packet traversal (hot kernel)
+// =============================================================================================
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) void k_project_wave(TreeView t, const float4* __restrict__ spt,
+                                                             const float4* __restrict__ snr,
+                                                             const unsigned* __restrict__ qperm, int N,
+                                                             const double* __restrict__ pose,
+                                                             const int* __restrict__ done, KParams kp,
+                                                             float4* __restrict__ cs, float4* __restrict__ cd,
+                                                             float4* __restrict__ cn, double* __restrict__ partial1,
+                                                             imls_iter_trace* __restrict__ tr,
+                                                             unsigned long long* __restrict__ nbr_stats,
+                                                             unsigned* __restrict__ fb_list,
+                                                             unsigned* __restrict__ fb_count,
+                                                             int* __restrict__ prevnn, int use_prev) {
+    if (done && *done) return;
+    __shared__ int wstack[kWaveBlock / 64][kStackDepth];
+    __shared__ double red[kWaveBlock / 64][kNormEq];
+    __shared__ double out[kNormEq];
+    __shared__ unsigned rej_s[IMLS_NUM_REJ + 3];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (tid < IMLS_NUM_REJ + 3) rej_s[tid] = 0;
+    __syncthreads();
+
+    const int slot = blockIdx.x * kWaveBlock + tid;
+    const bool active = slot < N;
+    const int i = active ? (int)qperm[slot] : 0;
+    float xf[3] = {0.f, 0.f, 0.f};
+    double ns[3] = {0, 0, 0};
+    if (active) transform_query(pose, spt[i], snr[i], kp.transform_normal, xf, ns);
+
+    // ---------------- wave traversal, fp32 keys ----------------
+    float lk[KL];
+    int lp[KL];
+#pragma unroll
+    for (int j = 0; j < KL; ++j) { lk[j] = kInfF; lp[j] = -1; }
+    const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
+    float bnd = active ? r2s : -1.0f;
+    const int P = t.P, B = t.B, M = t.M;
+    // seed pass (per lane): greedy descent to the nearest leaf and fill the list from it, so that
+    // every lane enters the wave traversal with a tight bound (otherwise a lane with a non-full
+    // list keeps the r-ball bound and drags the whole wave through every node within r of it)
+    int seed = -1;
+    if (active && use_prev) {
+        // temporal seed: the previous ICP iteration's list for this query (same frame, slightly
+        // different pose) — re-evaluated at the new position it is a near-tight bound
+#pragma unroll
+        for (int j = 0; j < KL; ++j) {
+            const int pos = prevnn[(size_t)j * N + slot];
+            if (pos >= 0) {
+                const float4 q = t.mpt[pos];
+                const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
+                const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                if (d32 <= bnd && d32 < lk[KL - 1]) {
+                    insert_top<KL>(lk, lp, d32, pos);
+                    bnd = fminf(r2s, lk[KL - 1]);
+                }
+            }
+        }
+    } else if (active) {
+        int n = 1;
+        while (n < P) {
+            const float4* rec = t.nodes + 3 * (size_t)n;
+            const float4 a = rec[0], b = rec[1], c = rec[2];
+            const float dl = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+            const float dr = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
+            n = dl <= dr ? 2 * n : 2 * n + 1;
+        }
+        seed = n - P;
+        const int base = seed * B, cnt = min(B, M - base);
+        for (int j = 0; j < cnt; ++j) {
+            const float4 q = t.mpt[base + j];
+            const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
+            const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+            if (d32 <= bnd && d32 < lk[KL - 1]) {
+                insert_top<KL>(lk, lp, d32, base + j);
+                bnd = fminf(r2s, lk[KL - 1]);
+            }
+        }
+    }
+    unsigned n_inner = 0, n_leaf = 0;
+    int node = 1, sp = 0;
+    while (true) {
+        if (node < P) {
+            ++n_inner;
+            const float4* rec = t.nodes + 3 * (size_t)node;
+            const float4 a = rec[0], b = rec[1], c = rec[2];
+            const float dl = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+            const float dr = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
+            const float bs = bnd * kBoxSlack;
+            const bool nl = dl <= bs, nr = dr <= bs;
+            const unsigned long long ml = __ballot(nl), mr = __ballot(nr);
+            if (ml && mr) {
+                const unsigned long long pl = __ballot((nl || nr) && dl <= dr);
+                const bool lf = 2 * __popcll(pl) >= __popcll(ml | mr);
+                wstack[wv][sp] = lf ? 2 * node + 1 : 2 * node;
+                ++sp;
+                node = lf ? 2 * node : 2 * node + 1;
+                continue;
+            }
+            if (ml) { node = 2 * node; continue; }
+            if (mr) { node = 2 * node + 1; continue; }
+        } else {
+            ++n_leaf;
+            const int leaf = node - P;
+            const int base = leaf * B;
+            const int cnt = min(B, M - base);
+            const float lb = (leaf == seed) ? -1.0f : r2s;     // the greedy seed leaf is already in the list
+            float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (lane < cnt) mine = t.mpt[base + lane];
+            for (int j = 0; j < cnt; ++j) {
+                const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
+                const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.y), j));
+                const float pz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.z), j));
+                const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
+                const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                if (d32 <= lb && d32 < lk[KL - 1] && !contains<KL>(lp, base + j)) {
+                    insert_top<KL>(lk, lp, d32, base + j);
+                    bnd = fminf(r2s, lk[KL - 1]);
+                }
+            }
+        }
+        // pop: re-check each stacked node against the (shrunken) lane bounds
+        node = 0;
+        while (sp > 0) {
+            --sp;
+            const int n = wstack[wv][sp];
+            const float4* rec = t.nodes + 3 * (size_t)(n >> 1);
+            float d;
+            if (n & 1) {
+                const float4 b = rec[1], c = rec[2];
+                d = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
+            } else {
+                const float4 a = rec[0], b = rec[1];
+                d = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+            }
+            if (__ballot(d <= bnd * kBoxSlack)) { node = n; break; }
+        }
+        if (!node) break;
+    }
+
+    if (active && prevnn) {
+#pragma unroll
+        for (int j = 0; j < KL; ++j) prevnn[(size_t)j * N + slot] = lp[j];   // seeds the next iteration
+    }
+
+    // ---------------- exact stage: fp64 re-rank + certification ----------------
+    const double xd[3] = {xf[0], xf[1], xf[2]};
+    double ed[KL];
+    int eo[KL];
+    const float W = lk[KL - 1];
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+        if (lk[j] < kInfF) {
+            const float4 q = t.mpt[lp[j]];
+            ed[j] = exact_d2(xd, q.x, q.y, q.z);
+            eo[j] = (int)__float_as_uint(q.w);
+        } else {
+            ed[j] = kInfD;
+            eo[j] = 0x7fffffff;
+        }
+    }
+    // odd-even transposition sort by (d², index); the fp32 order is already nearly exact
+    bool swapped = true;
+    while (__any(swapped)) {
+        swapped = false;
+#pragma unroll
+        for (int par = 0; par < 2; ++par) {
+#pragma unroll
+            for (int j = par; j + 1 < KL; j += 2) {
+                const bool sw = lessp(ed[j + 1], eo[j + 1], ed[j], eo[j]);
+                const double td = ed[j];
+                const int to = eo[j];
+                ed[j] = sw ? ed[j + 1] : ed[j];
+                eo[j] = sw ? eo[j + 1] : eo[j];
+                ed[j + 1] = sw ? td : ed[j + 1];
+                eo[j + 1] = sw ? to : eo[j + 1];
+                swapped |= sw;
+            }
+        }
+    }
+    const double r2 = kp.r2;
+    const int K = kp.K;
+    int cnt_r = 0;
+    double d1 = kInfD, dK = 0.0;
+    int i1 = -1;
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+        const bool in = ed[j] <= r2;
+        cnt_r += in ? 1 : 0;
+        if (in && i1 < 0 && ed[j] > DBL_EPSILON) { d1 = ed[j]; i1 = eo[j]; }
+        if (j == K - 1) dK = ed[j];
+    }
+    const bool full = W < kInfF;
+    double need = cnt_r >= K ? dK : r2;
+    bool cert = true;
+    if (full) {
+        if (i1 < 0) cert = false;
+        else need = fmax(need, d1);
+        cert = cert && (need < (double)W / kCertSlack);
+    }
+    const int kq_cnt = min(K, cnt_r);
+
+    int cat = -2, kq = 0;
+    float yf[3] = {0, 0, 0}, nf[3] = {0, 0, 0};
+    if (active) {
+        if (!cert) {
+            const unsigned pos = atomicAdd(fb_count, 1u);
+            fb_list[pos] = (unsigned)i;
+            cat = -3;                                         // deferred to k_project_lane
+        } else {
+            cat = finish_query<KL>(xf, ns, ed, eo, 0, kq_cnt, d1, i1, t, kp, yf, nf, kq);
+            store_result(i, cat, xf, yf, nf, cs, cd, cn);
+        }
+    }
+    if (cat >= 0) atomicAdd(&rej_s[cat], 1u);
+    if (active && cat != -3) {
+        if (kq) atomicAdd(&rej_s[IMLS_NUM_REJ], (unsigned)kq);
+        if (i1 >= 0) atomicAdd(&rej_s[IMLS_NUM_REJ + 1], 1u);
+    }
+    double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
+    if (cat == -1) { plane_row(xf, yf, nf, a, bb); one = 1.0; }
+    block_normeq<kWaveBlock>(a, bb, one, red, out);
+    if (tid < kNormEq) partial1[(size_t)blockIdx.x * kNormEq + tid] = out[tid];
+    if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
+    if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
+        atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
+    if (nbr_stats && lane == 0) {
+        atomicAdd(&nbr_stats[2], (unsigned long long)n_leaf);
+        atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
+        atomicAdd(&nbr_stats[4], 1ull);
+    }
+    if (nbr_stats && cat == -3) atomicAdd(&nbr_stats[5], 1ull);
+}
+
+// =============================================================================================
+// Per-lane exact traversal (fallback for uncertified queries; IMLS_TRAVERSAL=lane mode)
+// =============================================================================================
+template <int KCAP>
+__global__ __launch_bounds__(kProjBlock) void k_project_lane(TreeView t, const float4* __restrict__ spt,
+                                                             const float4* __restrict__ snr,
+                                                             const unsigned* __restrict__ qlist,
+                                                             const unsigned* __restrict__ qcount, int N,
+                                                             const double* __restrict__ pose,
+                                                             const int* __restrict__ done, KParams kp,
+                                                             float4* __restrict__ cs, float4* __restrict__ cd,
+                                                             float4* __restrict__ cn, double* __restrict__ partial1,
+                                                             imls_iter_trace* __restrict__ tr,
+                                                             unsigned long long* __restrict__ nbr_stats) {
+    if (done && *done) return;
+    __shared__ uint2 stack[kStackDepth][kProjBlock];
+    __shared__ double red[kProjBlock / 64][kNormEq];
+    __shared__ double out[kNormEq];
+    __shared__ unsigned rej_s[IMLS_NUM_REJ + 3];
+    const int tid = threadIdx.x;
+    if (tid < IMLS_NUM_REJ + 3) rej_s[tid] = 0;
+    __syncthreads();
+    const int total = qlist ? (int)*qcount : N;
+    double acc_out = 0.0;   // thread tid < 28 accumulates its normal-equation term over rounds
+    for (int base = blockIdx.x * kProjBlock; base < total; base += gridDim.x * kProjBlock) {
+        const int q = base + tid;
+        const bool active = q < total;
+        const int i = active ? (qlist ? (int)qlist[q] : q) : 0;
+        int cat = -2, kq = 0, nn_found = 0;
+        float xf[3] = {0, 0, 0}, yf[3] = {0, 0, 0}, nf[3] = {0, 0, 0};
+        if (active) {
+            double ns[3];
+            transform_query(pose, spt[i], snr[i], kp.transform_normal, xf, ns);
+            const double xd[3] = {xf[0], xf[1], xf[2]};
+            const int K = kp.K;
+            double ld[KCAP];
+            int li[KCAP];
+#pragma unroll
+            for (int j = 0; j < KCAP; ++j) {
+                const bool sentinel = j < KCAP - K;           // capacity K inside KCAP registers
+                ld[j] = sentinel ? -1.0 : kInfD;
+                li[j] = sentinel ? -1 : 0x7fffffff;
+            }
+            double d1 = kInfD;
+            int i1 = 0x7fffffff;
+            const double r2 = kp.r2;
+            float bf = (float)r2 * kBoxSlack + 1e-30f;
+            int node = 1, sp = 0;
+            const int P = t.P, B = t.B, M = t.M;
+            while (true) {
+                if (node < P) {
+                    const float4* rec = t.nodes + 3 * (size_t)node;
+                    const float4 a = rec[0], b = rec[1], c = rec[2];
+                    const float dl = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+                    const float dr = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
+                    const bool vl = dl <= bf, vr = dr <= bf;
+                    if (vl && vr) {
+                        const bool lfirst = dl <= dr;
+                        stack[sp][tid] = make_uint2(lfirst ? 2 * node + 1 : 2 * node, __float_as_uint(lfirst ? dr : dl));
+                        ++sp;
+                        node = lfirst ? 2 * node : 2 * node + 1;
+                        continue;
+                    }
+                    node = vl ? 2 * node : (vr ? 2 * node + 1 : 0);
+                    if (node) continue;
+                } else {
+                    const int s0 = (node - P) * B, e0 = min(s0 + B, M);
+                    for (int k = s0; k < e0; ++k) {
+                        const float4 q4 = t.mpt[k];
+                        const float ex = q4.x - xf[0], ey = q4.y - xf[1], ez = q4.z - xf[2];
+                        const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                        if (d32 > bf) continue;
+                        const double d2 = exact_d2(xd, q4.x, q4.y, q4.z);
+                        if (!(d2 <= r2)) continue;
+                        const int oi = (int)__float_as_uint(q4.w);
+                        bool changed = false;
+                        if (d2 > DBL_EPSILON && lessp(d2, oi, d1, i1)) { d1 = d2; i1 = oi; changed = true; }
+                        if (lessp(d2, oi, ld[KCAP - 1], li[KCAP - 1])) {
+                            bool prev = true;
+#pragma unroll
+                            for (int j = KCAP - 1; j >= 0; --j) {
+                                const bool sh = (j > 0) ? lessp(d2, oi, ld[(j > 0) ? j - 1 : 0], li[(j > 0) ? j - 1 : 0]) : false;
+                                const double nd = sh ? ld[(j > 0) ? j - 1 : 0] : (prev ? d2 : ld[j]);
+                                const int ni = sh ? li[(j > 0) ? j - 1 : 0] : (prev ? oi : li[j]);
+                                ld[j] = nd;
+                                li[j] = ni;
+                                prev = sh;
+                            }
+                            changed = true;
+                        }
+                        if (changed) bf = (float)fmin(r2, fmax(ld[KCAP - 1], d1)) * kBoxSlack + 1e-30f;
+                    }
+                    node = 0;
+                }
+                while (sp > 0) {
+                    --sp;
+                    const uint2 e = stack[sp][tid];
+                    if (__uint_as_float(e.y) <= bf) { node = (int)e.x; break; }
+                }
+                if (!node) break;
+            }
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < KCAP; ++j) cnt += (j >= KCAP - K && ld[j] < kInfD) ? 1 : 0;
+            nn_found = i1 != 0x7fffffff;
+            cat = finish_query<KCAP>(xf, ns, ld, li, KCAP - K, cnt, d1, nn_found ? i1 : -1, t, kp, yf, nf, kq);
+            store_result(i, cat, xf, yf, nf, cs, cd, cn);
+        }
+        if (cat >= 0) atomicAdd(&rej_s[cat], 1u);
+        if (active) {
+            if (kq) atomicAdd(&rej_s[IMLS_NUM_REJ], (unsigned)kq);
+            if (nn_found) atomicAdd(&rej_s[IMLS_NUM_REJ + 1], 1u);
+        }
+        double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
+        if (cat == -1) { plane_row(xf, yf, nf, a, bb); one = 1.0; }
+        block_normeq<kProjBlock>(a, bb, one, red, out);
+        if (tid < kNormEq) acc_out += out[tid];
+    }
+    __syncthreads();
+    if (tid < kNormEq) partial1[(size_t)blockIdx.x * kNormEq + tid] = acc_out;
     if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
 }
 
+template <int KCAP>
+void launch_lane(hipStream_t s, int blocks, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qlist,
+                 const unsigned* qcount, int N, const double* pose, const int* done, const KParams& kp, float4* cs,
+                 float4* cd, float4* cn, double* partial1, imls_iter_trace* tr, unsigned long long* stats) {
+    k_project_lane<KCAP><<<blocks, kProjBlock, 0, s>>>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1,
+                                                       tr, stats);
+}
+
+template <int KL>
+void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qperm,
+                 int N, const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd, float4* cn,
+                 double* partial1, imls_iter_trace* tr, unsigned long long* stats, unsigned* fb_list, unsigned* fb_count,
+                 int* prevnn, int use_prev) {
+    k_project_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats,
+                                                     fb_list, fb_count, prevnn, use_prev);
+}
+
 }  // namespace
 
-int project_blocks(int N) { return (N + kProjBlock - 1) / kProjBlock; }
+int project_blocks(int N) { return (N + kWaveBlock - 1) / kWaveBlock + kFallbackBlocks; }
 
-void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const float4* snr, int N, const double* pose,
-                    const int* done, const KParams& kp, float4* cs, float4* cd, float4* cn, double* partial1,
-                    imls_iter_trace* tr, unsigned long long* nbr_stats) {
-    const int blocks = project_blocks(N);
-    if (kp.K <= 8)
-        k_project<8><<<blocks, kProjBlock, 0, s>>>(t, spt, snr, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats);
-    else if (kp.K <= 16)
-        k_project<16><<<blocks, kProjBlock, 0, s>>>(t, spt, snr, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats);
-    else if (kp.K <= 20)
-        k_project<20><<<blocks, kProjBlock, 0, s>>>(t, spt, snr, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats);
-    else
-        k_project<32><<<blocks, kProjBlock, 0, s>>>(t, spt, snr, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats);
+void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qperm,
+                    int N, const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd, float4* cn,
+                    double* partial1, imls_iter_trace* tr, unsigned long long* stats, unsigned* fb_list,
+                    unsigned* fb_count, int lane_mode, int* prevnn, int use_prev) {
+    const int wblocks = (N + kWaveBlock - 1) / kWaveBlock;
+    double* p_fb = partial1 + (size_t)wblocks * kNormEq;
+    const int K = kp.K;
+    if (lane_mode) {
+        // reference mode: every query through the exact per-lane kernel (grid-stride over the
+        // fallback slabs); the wave slabs are zeroed
+        (void)hipMemsetAsync(partial1, 0, (size_t)wblocks * kNormEq * sizeof(double), s);
+        if (K <= 8) launch_lane<8>(s, kFallbackBlocks, t, spt, snr, nullptr, nullptr, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
+        else if (K <= 16) launch_lane<16>(s, kFallbackBlocks, t, spt, snr, nullptr, nullptr, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
+        else if (K <= 20) launch_lane<20>(s, kFallbackBlocks, t, spt, snr, nullptr, nullptr, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
+        else launch_lane<32>(s, kFallbackBlocks, t, spt, snr, nullptr, nullptr, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
+        return;
+    }
+    (void)hipMemsetAsync(fb_count, 0, sizeof(unsigned), s);
+    if (K <= 8) launch_wave<12>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, prevnn, use_prev);
+    else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, prevnn, use_prev);
+    else if (K <= 20) launch_wave<24>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, prevnn, use_prev);
+    else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, prevnn, use_prev);
+    // exact fallback for uncertified queries (usually none; the launch exits at once then)
+    if (K <= 8) launch_lane<8>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
+    else if (K <= 16) launch_lane<16>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
+    else if (K <= 20) launch_lane<20>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
+    else launch_lane<32>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
 }
 
 }  // namespace imlsgpu

@@ -306,27 +306,34 @@ __global__ __launch_bounds__(NT) void k_resid_hist(Rows rows, int N, SolveState 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
     if (*st.done) return;
-    __shared__ unsigned scan[kHistBins];
+    __shared__ unsigned csum[NT];
     __shared__ int meta[4];
     __shared__ double red[(NT / 64) * kNormEq];
-    __shared__ double out[kNormEq];
-    for (int k = threadIdx.x; k < kHistBins; k += NT) scan[k] = st.hist[k];
+    constexpr int kPer = kHistBins / NT;                      // bins per thread
+    unsigned loc[kPer];
+    unsigned tot = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) { loc[k] = st.hist[threadIdx.x * kPer + k]; tot += loc[k]; }
+    csum[threadIdx.x] = tot;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    for (int off = 1; off < NT; off <<= 1) {                  // inclusive Hillis-Steele scan
+        const unsigned v = threadIdx.x >= off ? csum[threadIdx.x - off] : 0u;
+        __syncthreads();
+        csum[threadIdx.x] += v;
+        __syncthreads();
+    }
+    {
         const long long lo = st.sel[4], hi = st.sel[5];
-        long long cum = 0;
-        int blo = -1, bhi = -1;
-        long long clo = 0, chi = 0;
-        for (int k = 0; k < kHistBins; ++k) {
-            const long long c = scan[k];
-            if (blo < 0 && lo < cum + c) { blo = k; clo = cum; }
-            if (bhi < 0 && hi < cum + c) { bhi = k; chi = cum; }
+        long long cum = (long long)csum[threadIdx.x] - tot;   // exclusive prefix of this chunk
+        for (int k = 0; k < kPer; ++k) {
+            const long long c = loc[k];
+            if (lo >= cum && lo < cum + c) { meta[0] = threadIdx.x * kPer + k; meta[2] = (int)cum; }
+            if (hi >= cum && hi < cum + c) { meta[1] = threadIdx.x * kPer + k; meta[3] = (int)cum; }
             cum += c;
         }
-        meta[0] = blo; meta[1] = bhi; meta[2] = (int)clo; meta[3] = (int)chi;
-        if (blockIdx.x == 0) { st.sel[0] = blo; st.sel[1] = bhi; st.sel[2] = (int)clo; st.sel[3] = (int)chi; }
     }
     __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) { st.sel[0] = meta[0]; st.sel[1] = meta[1]; st.sel[2] = meta[2]; st.sel[3] = meta[3]; }
     const int blo = meta[0], bhi = meta[1];
     double acc[kNormEq];
     for (int k = 0; k < kNormEq; ++k) acc[k] = 0.0;

@@ -184,6 +184,12 @@ class ImlsContext:
         keys = ("points", "leaves", "leaf_slots", "levels", "sum_kq", "nn_found", "queries", "bucket")
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def traversal_stats(self) -> dict:
+        out = np.zeros(8, np.uint64)
+        self._check(self.lib.imls_traversal_stats(self.ctx, _ptr(out)))
+        keys = ("sum_kq", "nn_found", "leaves_visited", "inner_visited", "waves", "uncertified")
+        return {k: int(v) for k, v in zip(keys, out)}
+
 
 # ================================================================================================
 # Reference-shaped API
