@@ -28,6 +28,7 @@ struct imls_ctx {
     // source
     DevBuf spt, snr, sscratch, qperm, upload_s;
     DevBuf fb;                            // fallback query list + count
+    DevBuf lkeys;                         // leaf first Morton keys + quantisation (seed search)
     DevBuf prevnn;                        // per-query neighbour lists carried between ICP iterations
     int lane_mode = 0;
     int temporal_seed = 1;
@@ -83,6 +84,11 @@ KParams make_kparams(const imls_params& p) {
     k.ls_threshold = p.ls_threshold;
     k.delta_dist = p.delta_dist_threshold;
     k.delta_angle = p.delta_angle_threshold;
+    k.seed_half = 2;
+    k.reseed = 0.25f;
+    if (const char* w = std::getenv("IMLS_SEED_HALF")) k.seed_half = std::atoi(w);
+    if (const char* w = std::getenv("IMLS_RESEED")) k.reseed = (float)std::atof(w);
+    if (const char* w = std::getenv("IMLS_WAVE_TRACE")) k.wave_trace = std::atoi(w);
     return k;
 }
 
@@ -106,7 +112,7 @@ int ensure_solve(imls_ctx* c, int N) {
     size_t n = (size_t)std::max(N, 1);
     if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, n * 4 + 256))
         return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
-    if (!grow(c->prevnn, n * kMaxKL * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
+    if (!grow(c->prevnn, n * (kMaxKL + 1) * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
     const int pb = std::max(project_blocks((int)n), solve_blocks((int)n)) + 1;
     size_t bytes = 0;
     auto add = [&](size_t b) { size_t o = bytes; bytes += (b + 255) / 256 * 256; return o; };
@@ -163,6 +169,9 @@ TreeView tree_view(imls_ctx* c) {
     t.B = c->B;
     t.P = c->Pl;
     t.levels = c->levels;
+    t.L = c->B > 0 ? (c->M + c->B - 1) / c->B : 0;
+    t.lkeys = (const unsigned long long*)c->lkeys.p;
+    t.qparams = c->lkeys.p ? (const float*)((const unsigned long long*)c->lkeys.p + t.L) : nullptr;
     return t;
 }
 
@@ -224,7 +233,7 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
 int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
     int slot;
     timed_begin(c, 1, slot);
-    int rc = build_target_index(c->stream, d_soa6, n, c->B, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch,
+    int rc = build_target_index(c->stream, d_soa6, n, c->B, c->lkeys, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch,
                                 c->treescratch, c->permbuf, &c->M, &c->Pl, &c->levels, c->err);
     timed_end(c, 1, slot);
     if (rc) return rc;
@@ -336,7 +345,7 @@ void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
+    DevBuf* bufs[] = {&c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
                       &c->upload_t, &c->spt, &c->snr, &c->sscratch,
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
@@ -415,7 +424,7 @@ int imls_project(imls_ctx* c, const double pose[16], float* x_out, float* y_out,
     launch_project(c->stream, tree_view(c), (const float4*)c->spt.p, (const float4*)c->snr.p, (const unsigned*)c->qperm.p,
                    c->N, dpose, dzero, c->kp, (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p, c->st.partial1,
                    c->st.trace, (unsigned long long*)c->stats.p, fb_list(c), fb_count(c), c->lane_mode,
-                   (int*)c->prevnn.p, 0);
+                   nullptr, (int*)c->prevnn.p, 0);
     timed_end(c, 0, slot);
     std::vector<float> hs((size_t)c->N * 4), hd((size_t)c->N * 4), hn((size_t)c->N * 4);
     imls_iter_trace tr;
@@ -510,7 +519,7 @@ int imls_register_frame_async(imls_ctx* c) {
         launch_project(c->stream, tv, (const float4*)c->spt.p, (const float4*)c->snr.p, (const unsigned*)c->qperm.p, c->N,
                        c->st.pose, c->st.done, c->kp, (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p,
                        c->st.partial1, tr + it, (unsigned long long*)c->stats.p, fb_list(c), fb_count(c), c->lane_mode,
-                       (int*)c->prevnn.p, it > 0 && c->temporal_seed);
+                       c->st.delta, (int*)c->prevnn.p, it > 0 && c->temporal_seed);
         timed_end(c, 0, slot);
         timed_begin(c, 2, slot);
         launch_solve_chain(c->stream, c->N, project_blocks(c->N), c->kp, (const float4*)c->cs.p, (const float4*)c->cd.p,
@@ -574,9 +583,14 @@ int imls_reset_timing(imls_ctx* c) {
 
 int imls_traversal_stats(imls_ctx* c, uint64_t out[8]) {
     if (!c || !out) return IMLS_ERR_ARG;
-    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    constexpr int kOut = 16;   // debug build: the caller passes 16 slots
+#else
+    constexpr int kOut = 8;
+#endif
+    unsigned long long st[kOut] = {};
     if (c->stats.p) hipMemcpy(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost);
-    for (int k = 0; k < 8; ++k) out[k] = st[k];
+    for (int k = 0; k < kOut; ++k) out[k] = st[k];
     return IMLS_OK;
 }
 

@@ -98,30 +98,26 @@ __global__ void k_bbox_final(const float* __restrict__ part, int nparts, float* 
     if (threadIdx.x < 6) bbox[threadIdx.x] = red[threadIdx.x][0];
 }
 
-__device__ __forceinline__ unsigned long long spread3_16(unsigned v) {
-    unsigned long long x = v & 0xFFFFull;
-    x = (x | (x << 16)) & 0x0000FF0000FFull;
-    x = (x | (x << 8)) & 0x00F00F00F00Full;
-    x = (x | (x << 4)) & 0x0C30C30C30C3ull;
-    x = (x | (x << 2)) & 0x249249249249ull;
-    return x;
+__global__ void k_qparams(const float* __restrict__ bbox, float* __restrict__ qp) {
+    if (threadIdx.x) return;
+    const float ext = fmaxf(fmaxf(fmaxf(bbox[3] - bbox[0], bbox[4] - bbox[1]), bbox[5] - bbox[2]), 1e-6f);
+    qp[0] = bbox[0]; qp[1] = bbox[1]; qp[2] = bbox[2];
+    qp[3] = 65535.f / ext;
 }
 
-__global__ void k_morton(const float4* __restrict__ pt, const int* __restrict__ count, const float* __restrict__ bbox,
+__global__ void k_morton(const float4* __restrict__ pt, const int* __restrict__ count, const float* __restrict__ qp,
                          unsigned long long* __restrict__ key, unsigned* __restrict__ val) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     int M = *count;
     if (i >= M) return;
     float4 p = pt[i];
-    const float qmax = 65535.f;
-    // isotropic cells (one scale for all axes) keep Morton buckets compact
-    const float ext = fmaxf(fmaxf(fmaxf(bbox[3] - bbox[0], bbox[4] - bbox[1]), bbox[5] - bbox[2]), 1e-6f);
-    const float sc = qmax / ext;
-    unsigned qx = (unsigned)fminf(fmaxf((p.x - bbox[0]) * sc, 0.f), qmax);
-    unsigned qy = (unsigned)fminf(fmaxf((p.y - bbox[1]) * sc, 0.f), qmax);
-    unsigned qz = (unsigned)fminf(fmaxf((p.z - bbox[2]) * sc, 0.f), qmax);
-    key[i] = spread3_16(qx) | (spread3_16(qy) << 1) | (spread3_16(qz) << 2);
+    key[i] = morton48(p.x, p.y, p.z, qp);
     val[i] = (unsigned)i;
+}
+
+__global__ void k_leaf_keys(const unsigned long long* __restrict__ sorted, int M, int B, unsigned long long* __restrict__ lk) {
+    int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l * B < M) lk[l] = sorted[(size_t)l * B];
 }
 
 __global__ void k_gather(const float4* __restrict__ pt, const unsigned* __restrict__ perm, int M, float4* __restrict__ mpt) {
@@ -219,7 +215,9 @@ int filter_compact(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, 
 }
 
 // Permutation (sorted → input index) of n float4 points by 48-bit Morton code over their bbox.
-int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf& perm, std::string& err) {
+// With lkeys: also the first key of each B-point leaf and the quantisation (seed search).
+int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf& perm, std::string& err,
+                DevBuf* lkeys = nullptr, int B = 0) {
     size_t cub_bytes = 0;
     hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                        (unsigned*)nullptr, (unsigned*)nullptr, n, 0, 48, s);
@@ -234,20 +232,26 @@ int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf
     void* cub_tmp = carve<char>(p, cub_bytes);
     float* bbpart = carve<float>(p, bb_parts * 6);
     float* bbox = carve<float>(p, 8);
+    float* qp = carve<float>(p, 4);
     int* cnt = carve<int>(p, 4);
+    const int L = B > 0 ? (n + B - 1) / B : 0;
+    if (lkeys && !ensure(*lkeys, (size_t)L * 8 + 16, err)) return IMLS_ERR_DEVICE;
+    if (lkeys) qp = (float*)((unsigned long long*)lkeys->p + L);   // qparams live after the keys
     hipMemcpyAsync(cnt, &n, sizeof(int), hipMemcpyHostToDevice, s);
     int nb = std::min(bb_parts, (int)grid_for(n));
     k_bbox_partial<<<nb, kBlock, 0, s>>>(pts, cnt, bbpart);
     k_bbox_final<<<1, kBlock, 0, s>>>(bbpart, nb, bbox);
-    k_morton<<<grid_for(n), kBlock, 0, s>>>(pts, cnt, bbox, k0, v0);
+    k_qparams<<<1, 64, 0, s>>>(bbox, qp);
+    k_morton<<<grid_for(n), kBlock, 0, s>>>(pts, cnt, qp, k0, v0);
     hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, (unsigned*)perm.p, n, 0, 48, s);
+    if (lkeys) k_leaf_keys<<<grid_for(L), kBlock, 0, s>>>(k1, n, B, (unsigned long long*)lkeys->p);
     if (hipGetLastError() != hipSuccess) { err = "morton sort launch failed"; return IMLS_ERR_DEVICE; }
     return IMLS_OK;
 }
 
 }  // namespace
 
-int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket, DevBuf& tpt, DevBuf& tnr,
+int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket, DevBuf& lkeys, DevBuf& tpt, DevBuf& tnr,
                        DevBuf& mpt, DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* M_out,
                        int* P_out, int* levels_out, std::string& err) {
     if (n_in == 0 || n_in > (size_t)0x7fffffff) { err = "target size out of range"; return IMLS_ERR_ARG; }
@@ -261,7 +265,7 @@ int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int buck
     int P = 1, levels = 0;
     while (P < L) { P <<= 1; ++levels; }
     if (levels > kStackDepth - 1) { err = "tree too deep for the traversal stack"; return IMLS_ERR_CAPACITY; }
-    rc = morton_perm(s, (const float4*)tpt.p, M, scratch, permbuf, err);
+    rc = morton_perm(s, (const float4*)tpt.p, M, scratch, permbuf, err, &lkeys, B);
     if (rc) return rc;
     size_t need = ((size_t)P * 24 + 255) / 256 * 256 + 2 * (((size_t)P / kBlock + 1) * 24 + 256) + 1024;
     if (!ensure(treescratch, need, err) || !ensure(mpt, (size_t)M * 16 + 16, err) ||

@@ -22,7 +22,7 @@ namespace imlsgpu {
 constexpr int kBlock = 256;            // threads per block for streaming kernels
 constexpr int kProjBlock = 128;        // threads per block for the projection kernel
 constexpr int kStackDepth = 24;        // traversal stack entries per lane (tree depth ≤ 24)
-constexpr int kHistBins = 4096;        // residual histogram bins (top 12 bits of float |r|)
+constexpr int kHistBins = 65536;       // residual histogram bins (top 16 bits of float |r|)
 constexpr int kCandCap = 8192;         // exact-select candidates handled in LDS per boundary bin
 constexpr int kNormEq = 28;            // 21 (JᵀJ upper) + 6 (Jᵀb) + 1 (row count)
 
@@ -46,6 +46,9 @@ struct KParams {
     int solve_method;
     double ls_threshold;
     double delta_dist, delta_angle;
+    int seed_half;            // seed pass scans the nearest leaf ± seed_half Morton neighbours
+    float reseed;             // temporal seed unless displacement² > reseed · previous worst key
+    int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
 };
 
 struct TreeView {
@@ -54,7 +57,28 @@ struct TreeView {
     const float4* tpt;
     const float4* tnr;
     int M, B, P, levels;
+    const unsigned long long* lkeys;   // [L] Morton key of each leaf's first point (seed search)
+    const float* qparams;              // [4] Morton quantisation: bbox lo xyz, scale
+    int L;                             // leaves holding points
 };
+
+// 48-bit Morton code with isotropic quantisation (one scale for all axes keeps buckets compact);
+// shared by the index build and the query-side seed search so both quantise identically.
+__device__ __forceinline__ unsigned long long spread3_16(unsigned v) {
+    unsigned long long x = v & 0xFFFFull;
+    x = (x | (x << 16)) & 0x0000FF0000FFull;
+    x = (x | (x << 8)) & 0x00F00F00F00Full;
+    x = (x | (x << 4)) & 0x0C30C30C30C3ull;
+    x = (x | (x << 2)) & 0x249249249249ull;
+    return x;
+}
+__device__ __forceinline__ unsigned long long morton48(float x, float y, float z, const float* __restrict__ qp) {
+    const float qmax = 65535.f, sc = qp[3];
+    const unsigned qx = (unsigned)fminf(fmaxf((x - qp[0]) * sc, 0.f), qmax);
+    const unsigned qy = (unsigned)fminf(fmaxf((y - qp[1]) * sc, 0.f), qmax);
+    const unsigned qz = (unsigned)fminf(fmaxf((z - qp[2]) * sc, 0.f), qmax);
+    return spread3_16(qx) | (spread3_16(qy) << 1) | (spread3_16(qz) << 2);
+}
 
 // Solver scratch living in device memory (one per context).
 struct SolveState {
@@ -79,7 +103,7 @@ struct SolveState {
 };
 
 // index.hip
-int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket,
+int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket, DevBuf& lkeys,
                        DevBuf& tpt, DevBuf& tnr, DevBuf& mpt, DevBuf& nodes, DevBuf& scratch,
                        DevBuf& treescratch, DevBuf& permbuf, int* M_out, int* P_out, int* levels_out,
                        std::string& err);
@@ -88,13 +112,13 @@ int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, De
                 DevBuf& scratch, DevBuf& qperm, int* N_out, std::vector<uint32_t>* kept, std::string& err);
 
 // project.hip
-// k_project_wave (+ the exact k_project_lane fallback for uncertified queries); lane_mode runs
-// every query through k_project_lane.  partial1 receives project_blocks(N) slabs.
+// k_knn_wave → k_finish (+ the exact k_project_lane fallback for uncertified queries); lane_mode
+// runs every query through k_project_lane.  partial1 receives project_blocks(N) slabs.
 void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const float4* snr,
                     const unsigned* qperm, int N, const double* pose, const int* done, const KParams& kp,
                     float4* cs, float4* cd, float4* cn, double* partial1, imls_iter_trace* tr,
                     unsigned long long* nbr_stats, unsigned* fb_list, unsigned* fb_count, int lane_mode,
-                    int* prevnn, int use_prev);   // prevnn: [kMaxKL][N] list positions across iterations
+                    const double* delta, int* lists, int use_prev);   // delta: last pose increment (use_prev)   // lists: [KL][N] positions + [N] worst keys, kept across iterations
 constexpr int kMaxKL = 36;
 int project_blocks(int N);
 

@@ -2,27 +2,32 @@
 // step (laser_odometry.cpp:527-549 → IMLSICPMatcher::ProjSourcePtToSurface, imls_icp.cpp:496-745
 // → ImplicitMLSFunction, imls_icp.cpp:301-483).
 //
-// k_project_wave (the hot kernel) — wave-coherent ("packet") traversal:
+// k_knn_wave (hot kernel 1) — wave-coherent ("packet") traversal of the target tree:
 //   * a wave owns 64 queries taken in Morton order of the source scan, so they are neighbours;
-//   * ONE traversal per wave of the target tree: the node index and the LDS stack are
-//     wave-uniform (node records come through the scalar cache), a child is entered when any
-//     lane's box distance is within that lane's bound (ballot), near-first by lane majority;
+//   * ONE traversal per wave: the node index and the LDS stack (node + its box, so a pop needs no
+//     memory round trip) are wave-uniform, node records come through the scalar cache; a child is
+//     entered when any lane's box distance is within that lane's bound (ballot), near-first by
+//     lane majority;
 //   * a leaf (B ≤ 64 Morton-consecutive map points) is ONE coalesced float4 load, each point is
-//     broadcast to all lanes by v_readlane and tested against each lane's own list;
-//   * per lane, a register top-(K+4) list keyed by the fp32 distance (query-relative, FMA);
-//   * then the exact stage: fp64 distances ((dx²+dy²)+dz², the libnabo metric, no FMA) of the
-//     list, sorted by (d², index), the radius filter (d² ≤ r², inclusive), NN-1 = first entry
-//     with d² > DBL_EPSILON (no self match, imls_icp.cpp:605-607), L = first K
-//     (ALLOW_SELF_MATCH, imls_icp.cpp:372-375);
-//   * CERTIFICATION: every map point outside the list has d²₆₄ ≥ W/(1+3.1e-7), W = the list's
-//     worst fp32 key (|d²₃₂ − d²₆₄| ≤ 5·2⁻²⁴·d²); the result is exact iff the largest exact
-//     distance it relies on is < W/(1+4e-7).  Uncertified queries (near-ties at the list edge,
-//     > K+4 duplicates) are appended to a list that k_project_lane re-runs exactly.
-// k_project_lane — one lane per query, exact fp64 list during the traversal (the fallback,
-// and the IMLS_TRAVERSAL=lane reference mode).
-// Both end in the same gates (imls_icp.cpp:612-717 in order), IMLS height with the h_max quirk
-// (Q3) and the 1e-5 bias (Q4), y = float(x − height·n_NN), and the pass-1 normal-equation
-// partials of the LS solve (solver.cpp:89-107): 21 JᵀJ + 6 Jᵀb + count per block, fp64.
+//     broadcast to all lanes by v_readlane and tested against each lane's register top-(K+4)
+//     list keyed by the fp32 distance;
+//   * bounds: iteration 0 seeds each lane from its nearest leaf (greedy descent); later ICP
+//     iterations prefill the list with the previous iteration's neighbours re-measured at the
+//     new pose (temporal coherence: the pose changes little), so few leaf points insert;
+//   * output: the list positions (Morton order) and the worst key W per query, to HBM.
+// k_finish (hot kernel 2) — one lane per query: the exact stage — fp64 distances
+//   ((dx²+dy²)+dz², the libnabo metric, no FMA) of the list, sorted by (d², index), the radius
+//   filter (d² ≤ r², inclusive), NN-1 = first entry with d² > DBL_EPSILON (no self match,
+//   imls_icp.cpp:605-607), L = first K (ALLOW_SELF_MATCH, imls_icp.cpp:372-375);
+//   CERTIFICATION — every map point outside the list has d²₆₄ ≥ W/(1+3.1e-7)
+//   (|d²₃₂ − d²₆₄| ≤ 5·2⁻²⁴·d²), so the result is exact iff the largest exact distance it relies
+//   on is < W/(1+4e-7); uncertified queries (near-ties at the list edge, > K+4 duplicates) are
+//   appended to a list that k_project_lane re-runs exactly.  Then the gates
+//   (imls_icp.cpp:612-717 in order), IMLS height with the h_max quirk (Q3) and the 1e-5 bias (Q4),
+//   y = float(x − height·n_NN), and the pass-1 normal-equation partials of the LS solve
+//   (solver.cpp:89-107): 21 JᵀJ + 6 Jᵀb + count per block, fp64.
+// k_project_lane — one lane per query, exact fp64 list during the traversal (the fallback, and
+// the IMLS_TRAVERSAL=lane reference mode).
 // Compiled with -ffp-contract=off: every fp64 expression evaluates as written.
 #include <cfloat>
 
@@ -35,6 +40,7 @@ constexpr double kInfD = __builtin_huge_val();
 constexpr float kInfF = __builtin_huge_valf();
 constexpr int kWaveBlock = 256;
 constexpr int kFallbackBlocks = 64;
+constexpr int kSparseLanes = 0;      // leaf processed per wanting lane when at most this many lanes want it (0: off)
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
 constexpr double kCertSlack = 1.0 + 4e-7;
 
@@ -82,7 +88,6 @@ __device__ __forceinline__ bool contains(const int (&lp)[KL], int pos) {
     return f;
 }
 
-// Insert (d, pos) into the ascending top-KL list (precondition: d < lk[KL−1]).
 template <int KL>
 __device__ __forceinline__ void insert_top(float (&lk)[KL], int (&lp)[KL], float d, int pos) {
     bool prev = true;   // prev = d < lk[k] (old value), i.e. the shift decision of slot k+1
@@ -247,39 +252,29 @@ __device__ __forceinline__ void store_result(int i, int cat, const float xf[3], 
 }
 
 // =============================================================================================
-// Packet traversal (hot kernel)
+// Packet traversal (hot kernel 1): per-query top-KL list positions + worst key
 // =============================================================================================
 template <int KL>
-__global__ __launch_bounds__(kWaveBlock) void k_project_wave(TreeView t, const float4* __restrict__ spt,
-                                                             const float4* __restrict__ snr,
-                                                             const unsigned* __restrict__ qperm, int N,
-                                                             const double* __restrict__ pose,
-                                                             const int* __restrict__ done, KParams kp,
-                                                             float4* __restrict__ cs, float4* __restrict__ cd,
-                                                             float4* __restrict__ cn, double* __restrict__ partial1,
-                                                             imls_iter_trace* __restrict__ tr,
-                                                             unsigned long long* __restrict__ nbr_stats,
-                                                             unsigned* __restrict__ fb_list,
-                                                             unsigned* __restrict__ fb_count,
-                                                             int* __restrict__ prevnn, int use_prev) {
+__global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float4* __restrict__ spt,
+                                                         const unsigned* __restrict__ qperm, int N,
+                                                         const double* __restrict__ pose,
+                                                         const int* __restrict__ done, KParams kp,
+                                                         const double* __restrict__ delta,
+                                                         int* __restrict__ lists, float* __restrict__ wlist,
+                                                         int use_prev, unsigned long long* __restrict__ nbr_stats) {
     if (done && *done) return;
-    __shared__ int wstack[kWaveBlock / 64][kStackDepth];
-    __shared__ double red[kWaveBlock / 64][kNormEq];
-    __shared__ double out[kNormEq];
-    __shared__ unsigned rej_s[IMLS_NUM_REJ + 3];
+    __shared__ int snode[kWaveBlock / 64][kStackDepth];
+    __shared__ float4 sbox[kWaveBlock / 64][kStackDepth][2];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (tid < IMLS_NUM_REJ + 3) rej_s[tid] = 0;
-    __syncthreads();
-
     const int slot = blockIdx.x * kWaveBlock + tid;
     const bool active = slot < N;
-    const int i = active ? (int)qperm[slot] : 0;
     float xf[3] = {0.f, 0.f, 0.f};
-    double ns[3] = {0, 0, 0};
-    if (active) transform_query(pose, spt[i], snr[i], kp.transform_normal, xf, ns);
-
-    // ---------------- wave traversal, fp32 keys ----------------
+    if (active) {
+        double ns[3];
+        const int i = (int)qperm[slot];
+        transform_query(pose, spt[i], make_float4(0.f, 0.f, 0.f, 0.f), 0, xf, ns);
+    }
     float lk[KL];
     int lp[KL];
 #pragma unroll
@@ -287,16 +282,30 @@ __global__ __launch_bounds__(kWaveBlock) void k_project_wave(TreeView t, const f
     const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
     float bnd = active ? r2s : -1.0f;
     const int P = t.P, B = t.B, M = t.M;
-    // seed pass (per lane): greedy descent to the nearest leaf and fill the list from it, so that
-    // every lane enters the wave traversal with a tight bound (otherwise a lane with a non-full
-    // list keeps the r-ball bound and drags the whole wave through every node within r of it)
-    int seed = -1;
+    int seed_lo = 0, seed_hi = -1;   // leaves already scanned by the seed pass (skipped below)
+    bool greedy = active && !use_prev;
     if (active && use_prev) {
-        // temporal seed: the previous ICP iteration's list for this query (same frame, slightly
-        // different pose) — re-evaluated at the new position it is a near-tight bound
+        // temporal seed only while the query moved little against its neighbourhood: the last
+        // pose increment Δ moves it by at most ‖t‖ + ‖R − I‖_F·‖x‖
+        double rf = 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const double e = delta[r * 4 + c] - (r == c ? 1.0 : 0.0);
+                rf += e * e;
+            }
+        const float tn = (float)sqrt(delta[3] * delta[3] + delta[7] * delta[7] + delta[11] * delta[11]);
+        const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
+        greedy = disp * disp > kp.reseed * wlist[slot];
+    }
+    if (active && !greedy) {
+        // prefill from the previous iteration's list re-measured at the new pose (all lanes insert
+        // in lockstep, so the list is full and the bound tight before the traversal starts; a
+        // later leaf insert must then skip points already listed)
 #pragma unroll
         for (int j = 0; j < KL; ++j) {
-            const int pos = prevnn[(size_t)j * N + slot];
+            const int pos = lists[(size_t)j * N + slot];
             if (pos >= 0) {
                 const float4 q = t.mpt[pos];
                 const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
@@ -308,28 +317,36 @@ __global__ __launch_bounds__(kWaveBlock) void k_project_wave(TreeView t, const f
             }
         }
     } else if (active) {
-        int n = 1;
-        while (n < P) {
-            const float4* rec = t.nodes + 3 * (size_t)n;
-            const float4 a = rec[0], b = rec[1], c = rec[2];
-            const float dl = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
-            const float dr = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
-            n = dl <= dr ? 2 * n : 2 * n + 1;
+        // seed: the leaf the query's own Morton key falls into (binary search over the leaves'
+        // first keys) and its Morton neighbours — Morton-near points are mostly space-near, while
+        // a greedy box-distance descent goes astray in the heavily overlapping upper-level boxes
+        const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
+        int lo = 0, hi = t.L - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (t.lkeys[mid] <= qk) lo = mid;
+            else hi = mid - 1;
         }
-        seed = n - P;
-        const int base = seed * B, cnt = min(B, M - base);
-        for (int j = 0; j < cnt; ++j) {
-            const float4 q = t.mpt[base + j];
+        seed_lo = max(0, lo - kp.seed_half);
+        seed_hi = min(t.L - 1, lo + kp.seed_half);
+        const int pend = min(M, (seed_hi + 1) * B);
+        for (int pos = seed_lo * B; pos < pend; ++pos) {
+            const float4 q = t.mpt[pos];
             const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
             const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
             if (d32 <= bnd && d32 < lk[KL - 1]) {
-                insert_top<KL>(lk, lp, d32, base + j);
+                insert_top<KL>(lk, lp, d32, pos);
                 bnd = fminf(r2s, lk[KL - 1]);
             }
         }
     }
     unsigned n_inner = 0, n_leaf = 0;
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    unsigned dbg_ev = 0, dbg_ins = 0, dbg_lane_ins = 0, dbg_useful = 0, dbg_wants = 0;
+    const float dbg_seed_bnd = lk[KL - 1];
+#endif
     int node = 1, sp = 0;
+    unsigned long long em = __ballot(active);   // lanes whose bound admits the current node's box
     while (true) {
         if (node < P) {
             ++n_inner;
@@ -343,123 +360,219 @@ __global__ __launch_bounds__(kWaveBlock) void k_project_wave(TreeView t, const f
             if (ml && mr) {
                 const unsigned long long pl = __ballot((nl || nr) && dl <= dr);
                 const bool lf = 2 * __popcll(pl) >= __popcll(ml | mr);
-                wstack[wv][sp] = lf ? 2 * node + 1 : 2 * node;
+                if (lane == 0) {
+                    snode[wv][sp] = lf ? 2 * node + 1 : 2 * node;
+                    sbox[wv][sp][0] = lf ? make_float4(b.z, b.w, c.x, c.y) : make_float4(a.x, a.y, a.z, a.w);
+                    sbox[wv][sp][1] = lf ? make_float4(c.z, c.w, 0.f, 0.f) : make_float4(b.x, b.y, 0.f, 0.f);
+                }
                 ++sp;
                 node = lf ? 2 * node : 2 * node + 1;
+                em = lf ? ml : mr;
                 continue;
             }
-            if (ml) { node = 2 * node; continue; }
-            if (mr) { node = 2 * node + 1; continue; }
+            if (ml) { node = 2 * node; em = ml; continue; }
+            if (mr) { node = 2 * node + 1; em = mr; continue; }
         } else {
             ++n_leaf;
             const int leaf = node - P;
             const int base = leaf * B;
             const int cnt = min(B, M - base);
-            const float lb = (leaf == seed) ? -1.0f : r2s;     // the greedy seed leaf is already in the list
+            const float lb = (leaf >= seed_lo && leaf <= seed_hi) ? -1.0f : r2s;
             float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
             if (lane < cnt) mine = t.mpt[base + lane];
-            for (int j = 0; j < cnt; ++j) {
-                const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
-                const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.y), j));
-                const float pz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.z), j));
-                const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
-                const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                if (d32 <= lb && d32 < lk[KL - 1] && !contains<KL>(lp, base + j)) {
-                    insert_top<KL>(lk, lp, d32, base + j);
-                    bnd = fminf(r2s, lk[KL - 1]);
+            if (kSparseLanes > 0 && __popcll(em) <= kSparseLanes) {
+                // few lanes want this leaf (spread-out queries in a dense region): per wanting
+                // lane, all leaf points are measured at once (one per lane) and only the ones
+                // under that lane's bound are handed to it, in index order
+                unsigned long long m = em;
+                while (m) {
+                    const int q = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
+                    m &= m - 1;
+                    const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[0]), q));
+                    const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[1]), q));
+                    const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[2]), q));
+                    const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fminf(lb, bnd)), q));   // lb: q's seed leaf
+                    const float ex = mine.x - qx, ey = mine.y - qy, ez = mine.z - qz;
+                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                    unsigned long long pm = __ballot(lane < cnt && d32 <= qb);
+                    while (pm) {
+                        const int j = __builtin_amdgcn_readfirstlane(__builtin_ctzll(pm));
+                        pm &= pm - 1;
+                        const float dj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d32), j));
+                        if (lane == q && dj <= bnd && dj < lk[KL - 1] && !(use_prev && contains<KL>(lp, base + j))) {
+                            insert_top<KL>(lk, lp, dj, base + j);
+                            bnd = fminf(r2s, lk[KL - 1]);
+                        }
+                    }
                 }
+            } else {
+                // points of this leaf already in the lane's (prefilled) list, as a bit mask: one
+                // lockstep pass over the list instead of a divergent membership test per point
+                unsigned long long inl = 0ull;
+                if (use_prev) {
+#pragma unroll
+                    for (int k = 0; k < KL; ++k) {
+                        const unsigned rel = (unsigned)(lp[k] - base);
+                        inl |= rel < 64u ? (1ull << rel) : 0ull;
+                    }
+                }
+                for (int j = 0; j < cnt; ++j) {
+                    const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
+                    const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.y), j));
+                    const float pz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.z), j));
+                    const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
+                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                    const bool ins = d32 <= fminf(lb, bnd) && d32 < lk[KL - 1] && !((inl >> j) & 1ull);
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                    const unsigned long long bi = __ballot(ins);
+                    dbg_ev += bi ? 1 : 0;
+                    dbg_ins += __popcll(bi);
+#endif
+                    if (ins) {
+                        insert_top<KL>(lk, lp, d32, base + j);
+                        bnd = fminf(r2s, lk[KL - 1]);
+                    }
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                    dbg_lane_ins += ins ? 1 : 0;
+#endif
+                }
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                dbg_wants += (em >> lane) & 1ull;
+                dbg_useful += 0;
+#endif
             }
         }
-        // pop: re-check each stacked node against the (shrunken) lane bounds
+        // pop: the stacked node's box is in LDS — re-check it against the shrunken lane bounds
         node = 0;
         while (sp > 0) {
             --sp;
-            const int n = wstack[wv][sp];
-            const float4* rec = t.nodes + 3 * (size_t)(n >> 1);
-            float d;
-            if (n & 1) {
-                const float4 b = rec[1], c = rec[2];
-                d = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
-            } else {
-                const float4 a = rec[0], b = rec[1];
-                d = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
-            }
-            if (__ballot(d <= bnd * kBoxSlack)) { node = n; break; }
+            const float4 b0 = sbox[wv][sp][0], b1 = sbox[wv][sp][1];
+            const float d = box_d2(xf, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y);
+            em = __ballot(d <= bnd * kBoxSlack);
+            if (em) { node = snode[wv][sp]; break; }
         }
         if (!node) break;
     }
+    if (active) {
+#pragma unroll
+        for (int j = 0; j < KL; ++j) lists[(size_t)j * N + slot] = lp[j];
+        wlist[slot] = lk[KL - 1];
+    }
+#ifdef IMLS_DEBUG_WAVE_TRACE   // debug build only (make DEBUG_WAVE_TRACE=1): insert counters
+    if (nbr_stats && lane == 0) {
+        atomicAdd(&nbr_stats[6], (unsigned long long)dbg_ev);
+        atomicAdd(&nbr_stats[7], (unsigned long long)dbg_ins);
+    }
+    if (nbr_stats && active) {
+        const float W = lk[KL - 1];
+        atomicAdd(&nbr_stats[8], (unsigned long long)dbg_wants);
+        if (dbg_seed_bnd <= 1.5f * W) atomicAdd(&nbr_stats[9], 1ull);
+        if (dbg_seed_bnd > 10.f * W) atomicAdd(&nbr_stats[10], 1ull);
+        if (W > 1.0f) atomicAdd(&nbr_stats[11], 1ull);
+        if (W == kInfF) atomicAdd(&nbr_stats[12], 1ull);
+        if (dbg_lane_ins > 100) atomicAdd(&nbr_stats[13], 1ull);
+        atomicMax(&nbr_stats[14], (unsigned long long)dbg_lane_ins);
+        if (W < 0.01f) atomicAdd(&nbr_stats[15], 1ull);
+    }
+#endif
+    if (nbr_stats && lane == 0) {
+        atomicAdd(&nbr_stats[2], (unsigned long long)n_leaf);
+        atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
+        atomicAdd(&nbr_stats[4], 1ull);
+    }
+}
 
-    if (active && prevnn) {
-#pragma unroll
-        for (int j = 0; j < KL; ++j) prevnn[(size_t)j * N + slot] = lp[j];   // seeds the next iteration
-    }
-
-    // ---------------- exact stage: fp64 re-rank + certification ----------------
-    const double xd[3] = {xf[0], xf[1], xf[2]};
-    double ed[KL];
-    int eo[KL];
-    const float W = lk[KL - 1];
-#pragma unroll
-    for (int j = 0; j < KL; ++j) {
-        if (lk[j] < kInfF) {
-            const float4 q = t.mpt[lp[j]];
-            ed[j] = exact_d2(xd, q.x, q.y, q.z);
-            eo[j] = (int)__float_as_uint(q.w);
-        } else {
-            ed[j] = kInfD;
-            eo[j] = 0x7fffffff;
-        }
-    }
-    // odd-even transposition sort by (d², index); the fp32 order is already nearly exact
-    bool swapped = true;
-    while (__any(swapped)) {
-        swapped = false;
-#pragma unroll
-        for (int par = 0; par < 2; ++par) {
-#pragma unroll
-            for (int j = par; j + 1 < KL; j += 2) {
-                const bool sw = lessp(ed[j + 1], eo[j + 1], ed[j], eo[j]);
-                const double td = ed[j];
-                const int to = eo[j];
-                ed[j] = sw ? ed[j + 1] : ed[j];
-                eo[j] = sw ? eo[j + 1] : eo[j];
-                ed[j + 1] = sw ? td : ed[j + 1];
-                eo[j + 1] = sw ? to : eo[j + 1];
-                swapped |= sw;
-            }
-        }
-    }
-    const double r2 = kp.r2;
-    const int K = kp.K;
-    int cnt_r = 0;
-    double d1 = kInfD, dK = 0.0;
-    int i1 = -1;
-#pragma unroll
-    for (int j = 0; j < KL; ++j) {
-        const bool in = ed[j] <= r2;
-        cnt_r += in ? 1 : 0;
-        if (in && i1 < 0 && ed[j] > DBL_EPSILON) { d1 = ed[j]; i1 = eo[j]; }
-        if (j == K - 1) dK = ed[j];
-    }
-    const bool full = W < kInfF;
-    double need = cnt_r >= K ? dK : r2;
-    bool cert = true;
-    if (full) {
-        if (i1 < 0) cert = false;
-        else need = fmax(need, d1);
-        cert = cert && (need < (double)W / kCertSlack);
-    }
-    const int kq_cnt = min(K, cnt_r);
-
-    int cat = -2, kq = 0;
+// =============================================================================================
+// Exact stage + gates + IMLS (hot kernel 2): one lane per query
+// =============================================================================================
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) void k_finish(TreeView t, const float4* __restrict__ spt,
+                                                       const float4* __restrict__ snr,
+                                                       const unsigned* __restrict__ qperm, int N,
+                                                       const double* __restrict__ pose,
+                                                       const int* __restrict__ done, KParams kp,
+                                                       const int* __restrict__ lists, const float* __restrict__ wlist,
+                                                       float4* __restrict__ cs, float4* __restrict__ cd,
+                                                       float4* __restrict__ cn, double* __restrict__ partial1,
+                                                       imls_iter_trace* __restrict__ tr,
+                                                       unsigned long long* __restrict__ nbr_stats,
+                                                       unsigned* __restrict__ fb_list, unsigned* __restrict__ fb_count) {
+    if (done && *done) return;
+    __shared__ double red[kWaveBlock / 64][kNormEq];
+    __shared__ double out[kNormEq];
+    __shared__ unsigned rej_s[IMLS_NUM_REJ + 3];
+    const int tid = threadIdx.x;
+    if (tid < IMLS_NUM_REJ + 3) rej_s[tid] = 0;
+    __syncthreads();
+    const int slot = blockIdx.x * kWaveBlock + tid;
+    const bool active = slot < N;
+    const int i = active ? (int)qperm[slot] : 0;
+    float xf[3] = {0.f, 0.f, 0.f};
+    double ns[3] = {0, 0, 0};
+    int cat = -2, kq = 0, i1 = -1;
     float yf[3] = {0, 0, 0}, nf[3] = {0, 0, 0};
     if (active) {
+        transform_query(pose, spt[i], snr[i], kp.transform_normal, xf, ns);
+        const double xd[3] = {xf[0], xf[1], xf[2]};
+        const float W = wlist[slot];
+        double ed[KL];
+        int eo[KL];
+#pragma unroll
+        for (int j = 0; j < KL; ++j) {
+            const int pos = lists[(size_t)j * N + slot];
+            if (pos >= 0) {
+                const float4 q = t.mpt[pos];
+                ed[j] = exact_d2(xd, q.x, q.y, q.z);
+                eo[j] = (int)__float_as_uint(q.w);
+            } else {
+                ed[j] = kInfD;
+                eo[j] = 0x7fffffff;
+            }
+        }
+        // odd-even transposition sort by (d², index); the fp32 order is already nearly exact
+        bool swapped = true;
+        while (swapped) {
+            swapped = false;
+#pragma unroll
+            for (int par = 0; par < 2; ++par) {
+#pragma unroll
+                for (int j = par; j + 1 < KL; j += 2) {
+                    const bool sw = lessp(ed[j + 1], eo[j + 1], ed[j], eo[j]);
+                    const double td = ed[j];
+                    const int to = eo[j];
+                    ed[j] = sw ? ed[j + 1] : ed[j];
+                    eo[j] = sw ? eo[j + 1] : eo[j];
+                    ed[j + 1] = sw ? td : ed[j + 1];
+                    eo[j + 1] = sw ? to : eo[j + 1];
+                    swapped |= sw;
+                }
+            }
+        }
+        const double r2 = kp.r2;
+        const int K = kp.K;
+        int cnt_r = 0;
+        double d1 = kInfD, dK = 0.0;
+#pragma unroll
+        for (int j = 0; j < KL; ++j) {
+            const bool in = ed[j] <= r2;
+            cnt_r += in ? 1 : 0;
+            if (in && i1 < 0 && ed[j] > DBL_EPSILON) { d1 = ed[j]; i1 = eo[j]; }
+            if (j == K - 1) dK = ed[j];
+        }
+        const bool full = W < kInfF;
+        double need = cnt_r >= K ? dK : r2;
+        bool cert = true;
+        if (full) {
+            if (i1 < 0) cert = false;
+            else need = fmax(need, d1);
+            cert = cert && (need < (double)W / kCertSlack);
+        }
         if (!cert) {
             const unsigned pos = atomicAdd(fb_count, 1u);
             fb_list[pos] = (unsigned)i;
             cat = -3;                                         // deferred to k_project_lane
         } else {
-            cat = finish_query<KL>(xf, ns, ed, eo, 0, kq_cnt, d1, i1, t, kp, yf, nf, kq);
+            cat = finish_query<KL>(xf, ns, ed, eo, 0, min(K, cnt_r), d1, i1, t, kp, yf, nf, kq);
             store_result(i, cat, xf, yf, nf, cs, cd, cn);
         }
     }
@@ -468,6 +581,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_project_wave(TreeView t, const f
         if (kq) atomicAdd(&rej_s[IMLS_NUM_REJ], (unsigned)kq);
         if (i1 >= 0) atomicAdd(&rej_s[IMLS_NUM_REJ + 1], 1u);
     }
+    if (cat == -3) atomicAdd(&rej_s[IMLS_NUM_REJ + 2], 1u);
     double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
     if (cat == -1) { plane_row(xf, yf, nf, a, bb); one = 1.0; }
     block_normeq<kWaveBlock>(a, bb, one, red, out);
@@ -475,12 +589,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_project_wave(TreeView t, const f
     if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
-    if (nbr_stats && lane == 0) {
-        atomicAdd(&nbr_stats[2], (unsigned long long)n_leaf);
-        atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
-        atomicAdd(&nbr_stats[4], 1ull);
-    }
-    if (nbr_stats && cat == -3) atomicAdd(&nbr_stats[5], 1ull);
+    if (nbr_stats && tid == IMLS_NUM_REJ + 2 && rej_s[tid]) atomicAdd(&nbr_stats[5], (unsigned long long)rej_s[tid]);
 }
 
 // =============================================================================================
@@ -616,13 +725,16 @@ void launch_lane(hipStream_t s, int blocks, const TreeView& t, const float4* spt
                                                        tr, stats);
 }
 
+
 template <int KL>
 void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qperm,
                  int N, const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd, float4* cn,
                  double* partial1, imls_iter_trace* tr, unsigned long long* stats, unsigned* fb_list, unsigned* fb_count,
-                 int* prevnn, int use_prev) {
-    k_project_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats,
-                                                     fb_list, fb_count, prevnn, use_prev);
+                 const double* delta, int* lists, int use_prev) {
+    float* wlist = reinterpret_cast<float*>(lists + (size_t)KL * N);
+    k_knn_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, use_prev, stats);
+    k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,
+                                               stats, fb_list, fb_count);
 }
 
 }  // namespace
@@ -632,7 +744,7 @@ int project_blocks(int N) { return (N + kWaveBlock - 1) / kWaveBlock + kFallback
 void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qperm,
                     int N, const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd, float4* cn,
                     double* partial1, imls_iter_trace* tr, unsigned long long* stats, unsigned* fb_list,
-                    unsigned* fb_count, int lane_mode, int* prevnn, int use_prev) {
+                    unsigned* fb_count, int lane_mode, const double* delta, int* lists, int use_prev) {
     const int wblocks = (N + kWaveBlock - 1) / kWaveBlock;
     double* p_fb = partial1 + (size_t)wblocks * kNormEq;
     const int K = kp.K;
@@ -647,10 +759,10 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
         return;
     }
     (void)hipMemsetAsync(fb_count, 0, sizeof(unsigned), s);
-    if (K <= 8) launch_wave<12>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, prevnn, use_prev);
-    else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, prevnn, use_prev);
-    else if (K <= 20) launch_wave<24>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, prevnn, use_prev);
-    else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, prevnn, use_prev);
+    if (K <= 8) launch_wave<12>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev);
+    else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev);
+    else if (K <= 20) launch_wave<24>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev);
+    else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev);
     // exact fallback for uncertified queries (usually none; the launch exits at once then)
     if (K <= 8) launch_lane<8>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
     else if (K <= 16) launch_lane<16>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void k_solve_first(const double* __restrict__ 
     for (int b = t; b < blocks; b += 256)
         for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
     for (int k = 0; k < kNormEq; ++k) part[t][k] = loc[k];
-    for (int i = t; i < kHistBins; i += 256) st.hist[i] = 0u;
+    for (int i = t; i < kHistBins / 4; i += 256) reinterpret_cast<uint4*>(st.hist)[i] = make_uint4(0u, 0u, 0u, 0u);
     if (t < 2) st.cand_count[t] = 0u;
     __syncthreads();
     if (t < kNormEq) {
@@ -275,16 +275,15 @@ __global__ __launch_bounds__(256) void k_solve_first(const double* __restrict__ 
     st.sel[6] = (int)N;
 }
 
+// 65536 bins on the top 16 bits of the float image of |r| (sign bit 0: 8 exponent + 7 mantissa
+// bits, 1/128-octave bins): monotone in |r|, so ranks map to bins; boundary bins stay small.
 __device__ __forceinline__ int key_bin(double key) {
-    return (int)(__float_as_uint((float)key) >> 20);   // key ≥ 0: monotone, < 4096 for finite keys
+    return (int)(__float_as_uint((float)key) >> 15);
 }
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_resid_hist(Rows rows, int N, SolveState st, KParams kp) {
     if (*st.done) return;
-    __shared__ unsigned h[kHistBins];
-    for (int k = threadIdx.x; k < kHistBins; k += NT) h[k] = 0u;
-    __syncthreads();
     const int i = blockIdx.x * NT + threadIdx.x;
     if (i < N) {
         double a[6], b, wt;
@@ -293,48 +292,55 @@ __global__ __launch_bounds__(NT) void k_resid_hist(Rows rows, int N, SolveState 
             double v = a[0] * st.x0[0];
             for (int k = 1; k < 6; ++k) v = v + a[k] * st.x0[k];
             key = fabs(v - b);
-            atomicAdd(&h[min(key_bin(key), kHistBins - 1)], 1u);
+            atomicAdd(&st.hist[min(key_bin(key), kHistBins - 1)], 1u);
         }
         st.keys[i] = key;
     }
-    __syncthreads();
-    for (int k = threadIdx.x; k < kHistBins; k += NT)
-        if (h[k]) atomicAdd(&st.hist[k], h[k]);
 }
 
-// Find the two boundary bins, reduce rows strictly between them, collect the boundary rows.
-template <int NT>
-__global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
+// One block: locate the bins holding ranks `lower` and `upper` (st.sel[4..5]) → st.sel[0..3].
+constexpr int kFindBlock = 1024;
+__global__ __launch_bounds__(kFindBlock) void k_find_bins(SolveState st) {
     if (*st.done) return;
-    __shared__ unsigned csum[NT];
-    __shared__ int meta[4];
-    __shared__ double red[(NT / 64) * kNormEq];
-    constexpr int kPer = kHistBins / NT;                      // bins per thread
+    constexpr int kPer = kHistBins / kFindBlock;
+    __shared__ unsigned csum[kFindBlock];
     unsigned loc[kPer];
     unsigned tot = 0;
+    const uint4* h4 = reinterpret_cast<const uint4*>(st.hist) + threadIdx.x * (kPer / 4);
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) { loc[k] = st.hist[threadIdx.x * kPer + k]; tot += loc[k]; }
+    for (int k = 0; k < kPer / 4; ++k) {
+        const uint4 v = h4[k];
+        loc[4 * k] = v.x; loc[4 * k + 1] = v.y; loc[4 * k + 2] = v.z; loc[4 * k + 3] = v.w;
+        tot += v.x + v.y + v.z + v.w;
+    }
     csum[threadIdx.x] = tot;
     __syncthreads();
-    for (int off = 1; off < NT; off <<= 1) {                  // inclusive Hillis-Steele scan
+    for (int off = 1; off < kFindBlock; off <<= 1) {         // inclusive Hillis-Steele scan
         const unsigned v = threadIdx.x >= off ? csum[threadIdx.x - off] : 0u;
         __syncthreads();
         csum[threadIdx.x] += v;
         __syncthreads();
     }
-    {
-        const long long lo = st.sel[4], hi = st.sel[5];
-        long long cum = (long long)csum[threadIdx.x] - tot;   // exclusive prefix of this chunk
+    const long long lo = st.sel[4], hi = st.sel[5];
+    long long cum = (long long)csum[threadIdx.x] - tot;       // exclusive prefix of this chunk
+    if (threadIdx.x == 0 && lo >= (long long)csum[kFindBlock - 1]) { st.sel[0] = -1; st.sel[2] = 0; }   // N = 0
+    if (threadIdx.x == 0 && hi >= (long long)csum[kFindBlock - 1]) { st.sel[1] = -1; st.sel[3] = 0; }
+    if (lo < cum + (long long)tot || hi < cum + (long long)tot) {
         for (int k = 0; k < kPer; ++k) {
             const long long c = loc[k];
-            if (lo >= cum && lo < cum + c) { meta[0] = threadIdx.x * kPer + k; meta[2] = (int)cum; }
-            if (hi >= cum && hi < cum + c) { meta[1] = threadIdx.x * kPer + k; meta[3] = (int)cum; }
+            if (lo >= cum && lo < cum + c) { st.sel[0] = threadIdx.x * kPer + k; st.sel[2] = (int)cum; }
+            if (hi >= cum && hi < cum + c) { st.sel[1] = threadIdx.x * kPer + k; st.sel[3] = (int)cum; }
             cum += c;
         }
     }
-    __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x == 0) { st.sel[0] = meta[0]; st.sel[1] = meta[1]; st.sel[2] = meta[2]; st.sel[3] = meta[3]; }
-    const int blo = meta[0], bhi = meta[1];
+}
+
+// Reduce rows strictly between the boundary bins; collect the boundary rows.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
+    if (*st.done) return;
+    __shared__ double red[(NT / 64) * kNormEq];
+    const int blo = st.sel[0], bhi = st.sel[1];
     double acc[kNormEq];
     for (int k = 0; k < kNormEq; ++k) acc[k] = 0.0;
     for (int i = blockIdx.x * NT + threadIdx.x; i < N; i += gridDim.x * NT) {
@@ -555,6 +561,7 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
     if (weighted) return;
     k_resid_hist<kBlock><<<solve_blocks(N), kBlock, 0, s>>>(rows, N, st, kp);
     const int cb = std::max(1, std::min(kCollectBlocks, (N + kBlock * 4 - 1) / (kBlock * 4)));
+    k_find_bins<<<1, kFindBlock, 0, s>>>(st);
     k_collect<kBlock><<<cb, kBlock, 0, s>>>(rows, N, st, st.partial2);
     k_solve_final<<<1, kFinalBlock, 0, s>>>(rows, N, st, tr, st.partial2, cb, kp, update_pose);
 }

@@ -162,8 +162,11 @@ class ImlsContext:
         self._check(self.lib.imls_register_frame_async(self.ctx))
 
     def register_frame_result(self):
+        it = max(self.params.iterations, 1)
+        trace = (_abi.ImlsIterTrace * it)()
         pose = np.zeros(16); iters = C.c_int(); status = C.c_int()
-        self._check(self.lib.imls_register_frame_result(self.ctx, _ptr(pose), C.byref(iters), C.byref(status), None))
+        self._check(self.lib.imls_register_frame_result(self.ctx, _ptr(pose), C.byref(iters), C.byref(status), trace))
+        self.last_trace = [trace[k] for k in range(iters.value)]
         return pose.reshape(4, 4), iters.value, status.value
 
     # -- instrumentation ------------------------------------------------------------------------

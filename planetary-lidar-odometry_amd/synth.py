@@ -334,6 +334,26 @@ def make_pair(model: str = "hdl64", map_scans: int = 10, scene_seed: int = 0, tr
                      noise_seed=noise_seed, scene_kind=scene_kind, start=start))
 
 
+def make_pairs(n: int, model: str = "hdl64", map_scans: int = 10, scene_seed: int = 0, traj_seed: int = 2000,
+               noise_seed: int = 1000, scene_kind: str = "urban", start: int = 30) -> list:
+    """`n` consecutive scan-to-map pairs of one trajectory (frames start … start+n−1), generating
+    each scan once: pair j registers scan start+j against scans start+j−map_scans … start+j−1
+    expressed in the frame of scan start+j−1 (same convention as make_pair)."""
+    sm = hdl64() if model == "hdl64" else vlp16()
+    scene = make_scene(scene_seed, scene_kind)
+    poses = trajectory(start + n, traj_seed)
+    scans = {k: scan(scene, sm, poses[k], noise_seed + k) for k in range(start - map_scans, start + n)}
+    out = []
+    for j in range(n):
+        k = start + j
+        Tk1_inv = np.linalg.inv(poses[k - 1])
+        target = np.concatenate([transform_cloud(scans[i], Tk1_inv @ poses[i]) for i in range(k - map_scans, k)])
+        out.append(Pair(scans[k], target, Tk1_inv @ poses[k],
+                        dict(model=model, map_scans=map_scans, scene_seed=scene_seed, traj_seed=traj_seed,
+                             noise_seed=noise_seed, scene_kind=scene_kind, start=k)))
+    return out
+
+
 def soa(cloud: np.ndarray) -> np.ndarray:
     """(6, N) float32 SoA: x, y, z, nx, ny, nz."""
     return np.stack([cloud[f] for f in ("x", "y", "z", "normal_x", "normal_y", "normal_z")]).astype(np.float32)
