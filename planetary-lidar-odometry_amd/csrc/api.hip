@@ -20,7 +20,7 @@ struct imls_ctx {
     imls_params P{};
     KParams kp{};
     std::string err;
-    int B = 32;
+    int B = 64;
     // target
     DevBuf tpt, tnr, mpt, nodes, tscratch, treescratch, permbuf, upload_t;
     int M = 0, Pl = 0, levels = 0;
@@ -84,8 +84,12 @@ KParams make_kparams(const imls_params& p) {
     k.ls_threshold = p.ls_threshold;
     k.delta_dist = p.delta_dist_threshold;
     k.delta_angle = p.delta_angle_threshold;
-    k.seed_half = 2;
+    k.seed_half = 1;
     k.reseed = 0.25f;
+    k.sparse_lanes = 32;
+    k.sparse_lanes_seed = 4;
+    if (const char* w = std::getenv("IMLS_SPARSE")) k.sparse_lanes = std::atoi(w);
+    if (const char* w = std::getenv("IMLS_SPARSE_SEED")) k.sparse_lanes_seed = std::atoi(w);
     if (const char* w = std::getenv("IMLS_SEED_HALF")) k.seed_half = std::atoi(w);
     if (const char* w = std::getenv("IMLS_RESEED")) k.reseed = (float)std::atof(w);
     if (const char* w = std::getenv("IMLS_WAVE_TRACE")) k.wave_trace = std::atoi(w);

@@ -48,6 +48,8 @@ struct KParams {
     double delta_dist, delta_angle;
     int seed_half;            // seed pass scans the nearest leaf ± seed_half Morton neighbours
     float reseed;             // temporal seed unless displacement² > reseed · previous worst key
+    int sparse_lanes;         // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
+    int sparse_lanes_seed;    // the same for waves holding freshly seeded lanes
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
 };
 

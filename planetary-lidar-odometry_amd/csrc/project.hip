@@ -40,7 +40,7 @@ constexpr double kInfD = __builtin_huge_val();
 constexpr float kInfF = __builtin_huge_valf();
 constexpr int kWaveBlock = 256;
 constexpr int kFallbackBlocks = 64;
-constexpr int kSparseLanes = 0;      // leaf processed per wanting lane when at most this many lanes want it (0: off)
+constexpr int kSeedChunk = 8;        // seed-pass points loaded per batch
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
 constexpr double kCertSlack = 1.0 + 4e-7;
 
@@ -78,14 +78,6 @@ __device__ __forceinline__ bool angle_reject(const double ns[3], double n0, doub
     const double ca = dot / (sqrt(a) * sqrt(b));
     const double angle = acos(ca) * 180.0 / M_PI;
     return angle > thr;
-}
-
-template <int KL>
-__device__ __forceinline__ bool contains(const int (&lp)[KL], int pos) {
-    bool f = false;
-#pragma unroll
-    for (int k = 0; k < KL; ++k) f |= lp[k] == pos;
-    return f;
 }
 
 template <int KL>
@@ -282,6 +274,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
     const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
     float bnd = active ? r2s : -1.0f;
     const int P = t.P, B = t.B, M = t.M;
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    const long long dbg_t0 = wall_clock64();
+#endif
     int seed_lo = 0, seed_hi = -1;   // leaves already scanned by the seed pass (skipped below)
     bool greedy = active && !use_prev;
     if (active && use_prev) {
@@ -330,13 +325,18 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
         seed_lo = max(0, lo - kp.seed_half);
         seed_hi = min(t.L - 1, lo + kp.seed_half);
         const int pend = min(M, (seed_hi + 1) * B);
-        for (int pos = seed_lo * B; pos < pend; ++pos) {
-            const float4 q = t.mpt[pos];
-            const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
-            const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-            if (d32 <= bnd && d32 < lk[KL - 1]) {
-                insert_top<KL>(lk, lp, d32, pos);
-                bnd = fminf(r2s, lk[KL - 1]);
+        for (int p0 = seed_lo * B; p0 < pend; p0 += kSeedChunk) {
+            float4 qs[kSeedChunk];   // issue the chunk's loads together, then consume them
+#pragma unroll
+            for (int k = 0; k < kSeedChunk; ++k) qs[k] = t.mpt[min(p0 + k, pend - 1)];
+#pragma unroll
+            for (int k = 0; k < kSeedChunk; ++k) {
+                const float ex = qs[k].x - xf[0], ey = qs[k].y - xf[1], ez = qs[k].z - xf[2];
+                const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                if (p0 + k < pend && d32 <= bnd && d32 < lk[KL - 1]) {
+                    insert_top<KL>(lk, lp, d32, p0 + k);
+                    bnd = fminf(r2s, lk[KL - 1]);
+                }
             }
         }
     }
@@ -344,7 +344,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
 #ifdef IMLS_DEBUG_WAVE_TRACE
     unsigned dbg_ev = 0, dbg_ins = 0, dbg_lane_ins = 0, dbg_useful = 0, dbg_wants = 0;
     const float dbg_seed_bnd = lk[KL - 1];
+    const long long dbg_t1 = wall_clock64();
 #endif
+    // waves with freshly seeded lanes insert a lot: per-lane leaf scans would serialise that
+    const int sparse_thr = __ballot(greedy) ? kp.sparse_lanes_seed : kp.sparse_lanes;
     int node = 1, sp = 0;
     unsigned long long em = __ballot(active);   // lanes whose bound admits the current node's box
     while (true) {
@@ -380,10 +383,20 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
             const float lb = (leaf >= seed_lo && leaf <= seed_hi) ? -1.0f : r2s;
             float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
             if (lane < cnt) mine = t.mpt[base + lane];
-            if (kSparseLanes > 0 && __popcll(em) <= kSparseLanes) {
+            // points of this leaf already in the lane's (prefilled) list, as a bit mask: one
+            // lockstep pass over the list instead of a divergent membership test per point
+            unsigned long long inl = 0ull;
+            if (use_prev) {
+#pragma unroll
+                for (int k = 0; k < KL; ++k) {
+                    const unsigned rel = (unsigned)(lp[k] - base);
+                    inl |= rel < 64u ? (1ull << rel) : 0ull;
+                }
+            }
+            if (__popcll(em) <= sparse_thr) {
                 // few lanes want this leaf (spread-out queries in a dense region): per wanting
                 // lane, all leaf points are measured at once (one per lane) and only the ones
-                // under that lane's bound are handed to it, in index order
+                // under that lane's bound and not yet listed are handed to it, in index order
                 unsigned long long m = em;
                 while (m) {
                     const int q = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
@@ -391,31 +404,24 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                     const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[0]), q));
                     const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[1]), q));
                     const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[2]), q));
-                    const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fminf(lb, bnd)), q));   // lb: q's seed leaf
+                    const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fminf(lb, bnd)), q));   // lb: q's seed leaves
+                    const unsigned long long inq =
+                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(inl >> 32), q) << 32) |
+                        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)inl, q);
                     const float ex = mine.x - qx, ey = mine.y - qy, ez = mine.z - qz;
                     const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                    unsigned long long pm = __ballot(lane < cnt && d32 <= qb);
+                    unsigned long long pm = __ballot(lane < cnt && d32 <= qb) & ~inq;
                     while (pm) {
                         const int j = __builtin_amdgcn_readfirstlane(__builtin_ctzll(pm));
                         pm &= pm - 1;
                         const float dj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d32), j));
-                        if (lane == q && dj <= bnd && dj < lk[KL - 1] && !(use_prev && contains<KL>(lp, base + j))) {
+                        if (lane == q && dj <= bnd && dj < lk[KL - 1]) {
                             insert_top<KL>(lk, lp, dj, base + j);
                             bnd = fminf(r2s, lk[KL - 1]);
                         }
                     }
                 }
             } else {
-                // points of this leaf already in the lane's (prefilled) list, as a bit mask: one
-                // lockstep pass over the list instead of a divergent membership test per point
-                unsigned long long inl = 0ull;
-                if (use_prev) {
-#pragma unroll
-                    for (int k = 0; k < KL; ++k) {
-                        const unsigned rel = (unsigned)(lp[k] - base);
-                        inl |= rel < 64u ? (1ull << rel) : 0ull;
-                    }
-                }
                 for (int j = 0; j < cnt; ++j) {
                     const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
                     const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.y), j));
@@ -463,16 +469,16 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
         atomicAdd(&nbr_stats[6], (unsigned long long)dbg_ev);
         atomicAdd(&nbr_stats[7], (unsigned long long)dbg_ins);
     }
-    if (nbr_stats && active) {
-        const float W = lk[KL - 1];
-        atomicAdd(&nbr_stats[8], (unsigned long long)dbg_wants);
-        if (dbg_seed_bnd <= 1.5f * W) atomicAdd(&nbr_stats[9], 1ull);
-        if (dbg_seed_bnd > 10.f * W) atomicAdd(&nbr_stats[10], 1ull);
-        if (W > 1.0f) atomicAdd(&nbr_stats[11], 1ull);
-        if (W == kInfF) atomicAdd(&nbr_stats[12], 1ull);
-        if (dbg_lane_ins > 100) atomicAdd(&nbr_stats[13], 1ull);
-        atomicMax(&nbr_stats[14], (unsigned long long)dbg_lane_ins);
-        if (W < 0.01f) atomicAdd(&nbr_stats[15], 1ull);
+    if (nbr_stats && lane == 0) {
+        const long long dbg_t2 = wall_clock64();
+        atomicAdd(&nbr_stats[8], (unsigned long long)(dbg_t1 - dbg_t0));
+        atomicMax(&nbr_stats[9], (unsigned long long)(dbg_t1 - dbg_t0));
+        atomicAdd(&nbr_stats[10], (unsigned long long)(dbg_t2 - dbg_t1));
+        atomicMax(&nbr_stats[11], (unsigned long long)(dbg_t2 - dbg_t1));
+        atomicAdd(&nbr_stats[12], (unsigned long long)n_leaf);
+        atomicMax(&nbr_stats[13], (unsigned long long)n_leaf);
+        atomicMax(&nbr_stats[14], (unsigned long long)dbg_ev);
+        atomicAdd(&nbr_stats[15], (unsigned long long)__popcll(__ballot(greedy)));
     }
 #endif
     if (nbr_stats && lane == 0) {

@@ -93,52 +93,112 @@ __device__ void block_normeq(const double a[6], double b, double cnt, double* re
     __syncthreads();
 }
 
+// Block-sum 28 per-thread values (all threads call); result in out[0..27] (LDS) after the call.
+template <int NT>
+__device__ void block_sum28(const double (&v)[kNormEq], double* red, double* out) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kNormEq; ++k) {
+        const double s = wave_sum(v[k]);
+        if (lane == 0) red[wv * kNormEq + k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNormEq) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) s += red[w * kNormEq + threadIdx.x];
+        out[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
 // Column-pivoted Cholesky solve of the 6×6 normal equations (see file header).  Unknowns past the
 // numerical rank are set to zero (Eigen's basic solution).  Returns the rank.
 __device__ int solve6(const double* ne, double x[6]) {
+    // every index below is a compile-time constant (full unroll; the pivot swap is a predicated
+    // swap over the candidate rows), so the system stays in registers — no scratch traffic
     double A[6][6], g[6];
-    int k = 0;
-    for (int r = 0; r < 6; ++r)
-        for (int c = r; c < 6; ++c) { A[r][c] = ne[k]; A[c][r] = ne[k]; ++k; }
-    for (int r = 0; r < 6; ++r) g[r] = ne[21 + r];
-    int perm[6] = {0, 1, 2, 3, 4, 5};
+    int perm[6];
+    {
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = r; c < 6; ++c) { A[r][c] = ne[k]; A[c][r] = ne[k]; ++k; }
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) { g[r] = ne[21 + r]; perm[r] = r; }
     const double eps = DBL_EPSILON;
     double maxpiv = 0.0;
     int rank = 6;
+    bool stop = false;
+#pragma unroll
     for (int j = 0; j < 6; ++j) {
-        int p = j;
-        for (int q = j + 1; q < 6; ++q) if (A[q][q] > A[p][p]) p = q;
-        if (p != j) {
-            for (int c = 0; c < 6; ++c) { double t = A[j][c]; A[j][c] = A[p][c]; A[p][c] = t; }
-            for (int r = 0; r < 6; ++r) { double t = A[r][j]; A[r][j] = A[r][p]; A[r][p] = t; }
-            double t = g[j]; g[j] = g[p]; g[p] = t;
-            int ti = perm[j]; perm[j] = perm[p]; perm[p] = ti;
-        }
-        const double d = A[j][j];
-        const double rkk = d > 0 ? sqrt(d) : 0.0;
-        if (rkk > maxpiv) maxpiv = rkk;
-        if (!(rkk > eps * 6.0 * maxpiv) || !(d > 0)) { rank = j; break; }
-        A[j][j] = rkk;
-        for (int r = j + 1; r < 6; ++r) A[r][j] = A[r][j] / rkk;
-        for (int r = j + 1; r < 6; ++r)
-            for (int c = j + 1; c <= r; ++c) {
-                A[r][c] = A[r][c] - A[r][j] * A[c][j];
-                A[c][r] = A[r][c];
+        if (!stop) {
+            int p = j;
+            double best = A[j][j];
+#pragma unroll
+            for (int q = j + 1; q < 6; ++q)
+                if (A[q][q] > best) { best = A[q][q]; p = q; }
+#pragma unroll
+            for (int q = j + 1; q < 6; ++q) {
+                if (q == p) {
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) { const double t = A[j][c]; A[j][c] = A[q][c]; A[q][c] = t; }
+#pragma unroll
+                    for (int r = 0; r < 6; ++r) { const double t = A[r][j]; A[r][j] = A[r][q]; A[r][q] = t; }
+                    const double t = g[j]; g[j] = g[q]; g[q] = t;
+                    const int ti = perm[j]; perm[j] = perm[q]; perm[q] = ti;
+                }
             }
+            const double d = A[j][j];
+            const double rkk = d > 0 ? sqrt(d) : 0.0;
+            if (rkk > maxpiv) maxpiv = rkk;
+            if (!(rkk > eps * 6.0 * maxpiv) || !(d > 0)) {
+                rank = j;
+                stop = true;
+            } else {
+                A[j][j] = rkk;
+#pragma unroll
+                for (int r = j + 1; r < 6; ++r) A[r][j] = A[r][j] / rkk;
+#pragma unroll
+                for (int r = j + 1; r < 6; ++r)
+#pragma unroll
+                    for (int c = j + 1; c <= r; ++c) {
+                        A[r][c] = A[r][c] - A[r][j] * A[c][j];
+                        A[c][r] = A[r][c];
+                    }
+            }
+        }
     }
     double y[6] = {0, 0, 0, 0, 0, 0};
-    for (int r = 0; r < rank; ++r) {
-        double s = g[r];
-        for (int c = 0; c < r; ++c) s -= A[r][c] * y[c];
-        y[r] = s / A[r][r];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        if (r < rank) {
+            double s = g[r];
+#pragma unroll
+            for (int c = 0; c < r; ++c) s -= A[r][c] * y[c];
+            y[r] = s / A[r][r];
+        }
     }
-    for (int r = rank - 1; r >= 0; --r) {
-        double s = y[r];
-        for (int c = r + 1; c < rank; ++c) s -= A[c][r] * y[c];
-        y[r] = s / A[r][r];
+#pragma unroll
+    for (int r = 5; r >= 0; --r) {
+        if (r < rank) {
+            double s = y[r];
+#pragma unroll
+            for (int c = r + 1; c < 6; ++c)
+                if (c < rank) s -= A[c][r] * y[c];
+            y[r] = s / A[r][r];
+        }
     }
-    for (int r = 0; r < 6; ++r) x[r] = 0.0;
-    for (int r = 0; r < rank; ++r) x[perm[r]] = y[r];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        double v = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+            if (r < rank && perm[r] == k) v = y[r];
+        x[k] = v;
+    }
     return rank;
 }
 
@@ -232,21 +292,17 @@ __global__ __launch_bounds__(256) void k_solve_first(const double* __restrict__ 
                                                      imls_iter_trace* tr, KParams kp, int weighted, int update_pose) {
     if (*st.done) return;
     __shared__ double acc[kNormEq];
-    __shared__ double part[256][kNormEq + 1];
+    __shared__ double red[(256 / 64) * kNormEq];
     const int t = threadIdx.x;
     double loc[kNormEq];
+#pragma unroll
     for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
     for (int b = t; b < blocks; b += 256)
+#pragma unroll
         for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
-    for (int k = 0; k < kNormEq; ++k) part[t][k] = loc[k];
     for (int i = t; i < kHistBins / 4; i += 256) reinterpret_cast<uint4*>(st.hist)[i] = make_uint4(0u, 0u, 0u, 0u);
     if (t < 2) st.cand_count[t] = 0u;
-    __syncthreads();
-    if (t < kNormEq) {
-        double s = 0.0;
-        for (int j = 0; j < 256; ++j) s += part[j][t];
-        acc[t] = s;
-    }
+    block_sum28<256>(loc, red, acc);
     __syncthreads();
     if (t != 0) return;
     const double nvalid = acc[27];
@@ -470,7 +526,6 @@ __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, S
     const int blo = st.sel[0], bhi = st.sel[1];
     const long long clo = st.sel[2], chi = st.sel[3], lo = st.sel[4], hi = st.sel[5];
     const unsigned n_lo = st.cand_count[0], n_hi = st.cand_count[1];
-    double a[6] = {0, 0, 0, 0, 0, 0}, b = 0, wt = 1, cnt = 0;
     double accA[kNormEq];
     for (int k = 0; k < kNormEq; ++k) accA[k] = 0.0;
     auto add_row = [&](unsigned row) {
@@ -519,21 +574,11 @@ __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, S
             if (pair_le(selk[0], selr[0], kb, (unsigned)i) && pair_le(kb, (unsigned)i, selk[1], selr[1])) add_row((unsigned)i);
         }
     }
-    // block reduce accA
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int k = 0; k < kNormEq; ++k) {
-        const double v = wave_sum(accA[k]);
-        if (lane == 0) red[wv * kNormEq + k] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < kNormEq) {
-        double s = 0.0;
-        for (int w = 0; w < kFinalBlock / 64; ++w) s += red[w * kNormEq + threadIdx.x];
-        for (int p = 0; p < nparts; ++p) s += partial2[(size_t)p * kNormEq + threadIdx.x];
-        out[threadIdx.x] = s;
-    }
-    __syncthreads();
-    (void)a; (void)b; (void)wt; (void)cnt;
+    // the interior partials from k_collect, then one block reduction
+    for (int q = threadIdx.x; q < nparts; q += kFinalBlock)
+#pragma unroll
+        for (int k = 0; k < kNormEq; ++k) accA[k] += partial2[(size_t)q * kNormEq + k];
+    block_sum28<kFinalBlock>(accA, red, out);
     if (threadIdx.x != 0) return;
     double x[6], D[16];
     solve6(out, x);

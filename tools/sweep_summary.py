@@ -1,5 +1,5 @@
 import csv, glob, json, pathlib
-for d in sorted(glob.glob("gpurun_out/sweep/s*_r*/")):
+for d in sorted(glob.glob("gpurun_out/sweep/*/")):
     name = pathlib.Path(d).name
     kt = pathlib.Path(d) / "run_kernel_trace.csv"
     if not kt.exists():

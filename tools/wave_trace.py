@@ -11,7 +11,7 @@ iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 pair = synth.make_pairs(1, "hdl64", map_scans=10, scene_seed=0, traj_seed=2000, noise_seed=1000)[0]
 sd = torch.from_numpy(np.ascontiguousarray(synth.soa(pair.source))).cuda()
 td = torch.from_numpy(np.ascontiguousarray(synth.soa(pair.target))).cuda()
-keys = ("sum_kq", "nn_found", "leaves", "inner", "waves", "uncertified", "insert_events", "lane_inserts", "lane_leaf_wants", "seed_good", "seed_bad10x", "W>1m2", "W_inf", "lanes_ins>100", "max_lane_ins", "W<0.01")
+keys = ("sum_kq", "nn_found", "leaves", "inner", "waves", "uncertified", "insert_events", "lane_inserts", "seed_clk_sum", "seed_clk_max", "trav_clk_sum", "trav_clk_max", "leaf_sum", "leaf_max", "events_max", "greedy_lanes")
 for iters in [int(a) for a in (sys.argv[1:] or ['1', '2', '3', '20'])]:
     c = imls_icp.ImlsContext(config.bench_params(iters), device=0)
     c.set_target_device(td.data_ptr(), pair.target.size)
