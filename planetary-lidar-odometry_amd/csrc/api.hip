@@ -166,6 +166,8 @@ unsigned* fb_list(imls_ctx* c) { return (unsigned*)c->fb.p + 64; }
 TreeView tree_view(imls_ctx* c) {
     TreeView t;
     t.mpt = (const float4*)c->mpt.p;
+    t.mnr = t.mpt ? t.mpt + c->M : nullptr;
+    t.ipos = t.mpt ? (const unsigned*)(t.mpt + 2 * (size_t)c->M) : nullptr;
     t.nodes = (const float4*)c->nodes.p;
     t.tpt = (const float4*)c->tpt.p;
     t.tnr = (const float4*)c->tnr.p;

@@ -120,12 +120,16 @@ __global__ void k_leaf_keys(const unsigned long long* __restrict__ sorted, int M
     if (l * B < M) lk[l] = sorted[(size_t)l * B];
 }
 
-__global__ void k_gather(const float4* __restrict__ pt, const unsigned* __restrict__ perm, int M, float4* __restrict__ mpt) {
+// Morton-ordered copies: mpt (xyz + original index), mnr (normals), and ipos (original → Morton)
+__global__ void k_gather(const float4* __restrict__ pt, const float4* __restrict__ nr, const unsigned* __restrict__ perm,
+                         int M, float4* __restrict__ mpt, float4* __restrict__ mnr, unsigned* __restrict__ ipos) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= M) return;
     unsigned j = perm[k];
     float4 p = pt[j];
     mpt[k] = make_float4(p.x, p.y, p.z, __uint_as_float(j));
+    mnr[k] = nr[j];
+    ipos[j] = (unsigned)k;
 }
 
 struct Box { float lo[3], hi[3]; };
@@ -268,14 +272,15 @@ int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int buck
     rc = morton_perm(s, (const float4*)tpt.p, M, scratch, permbuf, err, &lkeys, B);
     if (rc) return rc;
     size_t need = ((size_t)P * 24 + 255) / 256 * 256 + 2 * (((size_t)P / kBlock + 1) * 24 + 256) + 1024;
-    if (!ensure(treescratch, need, err) || !ensure(mpt, (size_t)M * 16 + 16, err) ||
+    if (!ensure(treescratch, need, err) || !ensure(mpt, (size_t)M * 36 + 64, err) ||
         !ensure(nodes, (size_t)(P + 1) * 48, err))
         return IMLS_ERR_DEVICE;
     char* p = (char*)treescratch.p;
     float* leafbox = carve<float>(p, (size_t)P * 6);
     float* rootsA = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
     float* rootsB = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
-    k_gather<<<grid_for(M), kBlock, 0, s>>>((const float4*)tpt.p, (const unsigned*)permbuf.p, M, (float4*)mpt.p);
+    k_gather<<<grid_for(M), kBlock, 0, s>>>((const float4*)tpt.p, (const float4*)tnr.p, (const unsigned*)permbuf.p, M,
+                                            (float4*)mpt.p, (float4*)mpt.p + M, (unsigned*)((float4*)mpt.p + 2 * (size_t)M));
     k_leaf_boxes<<<grid_for(P), kBlock, 0, s>>>((const float4*)mpt.p, M, B, P, leafbox);
     // bottom-up subtree reduction, 256 boxes per block per launch
     const float* in = leafbox;

@@ -54,7 +54,9 @@ struct KParams {
 };
 
 struct TreeView {
-    const float4* mpt;
+    const float4* mpt;        // map points in Morton order, w = original index (bits)
+    const float4* mnr;        // their normals, same order
+    const unsigned* ipos;     // original index → Morton position
     const float4* nodes;      // 3 float4 per internal node, index 1..P-1 (entry 0 unused)
     const float4* tpt;
     const float4* tnr;

@@ -130,16 +130,17 @@ __device__ __forceinline__ void transform_query(const double* __restrict__ pose,
 }
 
 // Gates + ImplicitMLSFunction + projection for one query given its exact neighbour list
-// L = (ld[j], li[j]) for j ∈ [first, first+cnt) sorted by (d², index) and its NN-1 (d1, i1).
+// L = (ld[j], lpos[j]) for j ∈ [first, first+cnt) sorted by (d², index) and its NN-1 (d1, p1);
+// positions are Morton positions (mpt/mnr: the neighbours of a query share cache lines).
 // Returns the reject category or −1 (valid, yf/nf filled).  kq counts the returned neighbours.
 template <int CAP>
-__device__ int finish_query(const float xf[3], const double ns[3], const double (&ld)[CAP], const int (&li)[CAP],
-                            int first, int cnt, double d1, int i1, const TreeView& t, const KParams& kp, float yf[3],
+__device__ int finish_query(const float xf[3], const double ns[3], const double (&ld)[CAP], const int (&lpos)[CAP],
+                            int first, int cnt, double d1, int p1, const TreeView& t, const KParams& kp, float yf[3],
                             float nf[3], int& kq) {
-    if (i1 < 0) return IMLS_REJ_TOO_FAR;                      // InvalidIndex → counted as too far (Q18)
+    if (p1 < 0) return IMLS_REJ_TOO_FAR;                      // InvalidIndex → counted as too far (Q18)
     if (d1 > kp.h2) return IMLS_REJ_TOO_FAR;                  // imls_icp.cpp:620
     if (!kp.get_normals) return IMLS_REJ_INVALID_NORMAL;      // recompute branch under libnabo semantics (Q1)
-    const float4 n4 = t.tnr[i1];
+    const float4 n4 = t.mnr[p1];
     const double nn[3] = {n4.x, n4.y, n4.z};
     if (!(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) return IMLS_REJ_INVALID_NORMAL;
     if (kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg)) return IMLS_REJ_NORMAL_CONSTRAINT;
@@ -150,7 +151,7 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
     for (int j = 0; j < CAP; ++j) {
         if (j >= first && j < first + cnt) {
             ++kq;
-            const float4 qn = t.tnr[li[j]];
+            const float4 qn = t.mnr[lpos[j]];
             bool ok = isfinite(qn.x) && isfinite(qn.y) && isfinite(qn.z);
             if (ok && kp.angle_on) ok = !angle_reject(ns, qn.x, qn.y, qn.z, kp.angle_thr_deg);
             if (ok) { acc |= 1ull << j; ++nacc; }
@@ -166,8 +167,8 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
 #pragma unroll
     for (int j = 0; j < CAP; ++j) {
         if (acc & (1ull << j)) {
-            const float4 qp = t.tpt[li[j]];
-            const float4 qn = t.tnr[li[j]];
+            const float4 qp = t.mpt[lpos[j]];
+            const float4 qn = t.mnr[lpos[j]];
             const double dx = xd[0] - (double)qp.x, dy = xd[1] - (double)qp.y, dz = xd[2] - (double)qp.z;
             double dn = dx * dx;
             dn = dn + dy * dy;
@@ -246,6 +247,11 @@ __device__ __forceinline__ void store_result(int i, int cat, const float xf[3], 
 // =============================================================================================
 // Packet traversal (hot kernel 1): per-query top-KL list positions + worst key
 // =============================================================================================
+#ifdef IMLS_DEBUG_WAVE_TRACE
+constexpr int kDbgWaves = 8192;
+__device__ unsigned g_dbg_wave[kDbgWaves][16];
+#endif
+
 template <int KL>
 __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
@@ -343,6 +349,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
     unsigned n_inner = 0, n_leaf = 0;
 #ifdef IMLS_DEBUG_WAVE_TRACE
     unsigned dbg_ev = 0, dbg_ins = 0, dbg_lane_ins = 0, dbg_useful = 0, dbg_wants = 0;
+    unsigned dbg_sparse = 0, dbg_bcast = 0, dbg_sparse_lanes = 0, dbg_sparse_ins = 0;
     const float dbg_seed_bnd = lk[KL - 1];
     const long long dbg_t1 = wall_clock64();
 #endif
@@ -393,6 +400,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                     inl |= rel < 64u ? (1ull << rel) : 0ull;
                 }
             }
+#ifdef IMLS_DEBUG_WAVE_TRACE
+            if (__popcll(em) <= sparse_thr) { ++dbg_sparse; dbg_sparse_lanes += __popcll(em); } else { ++dbg_bcast; }
+#endif
             if (__popcll(em) <= sparse_thr) {
                 // few lanes want this leaf (spread-out queries in a dense region): per wanting
                 // lane, all leaf points are measured at once (one per lane) and only the ones
@@ -416,6 +426,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                         pm &= pm - 1;
                         const float dj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d32), j));
                         if (lane == q && dj <= bnd && dj < lk[KL - 1]) {
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                            ++dbg_sparse_ins;
+#endif
                             insert_top<KL>(lk, lp, dj, base + j);
                             bnd = fminf(r2s, lk[KL - 1]);
                         }
@@ -480,6 +493,24 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
         atomicMax(&nbr_stats[14], (unsigned long long)dbg_ev);
         atomicAdd(&nbr_stats[15], (unsigned long long)__popcll(__ballot(greedy)));
     }
+    {
+        const unsigned long long gl = __ballot(greedy), wi = __ballot(active && lk[KL - 1] == kInfF),
+                                 w1 = __ballot(active && lk[KL - 1] > 1.0f);
+        float wmax = active && lk[KL - 1] < kInfF ? lk[KL - 1] : 0.f;
+        for (int o = 1; o < 64; o <<= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, o));
+        unsigned sins = dbg_sparse_ins;
+        for (int o = 1; o < 64; o <<= 1) sins += __shfl_xor(sins, o);
+        if (lane == 0) {
+            const int w = blockIdx.x * (kWaveBlock / 64) + wv;
+            if (w < kDbgWaves) {
+                unsigned* r = g_dbg_wave[w];
+                r[0] = (unsigned)(dbg_t1 - dbg_t0); r[1] = (unsigned)(wall_clock64() - dbg_t1);
+                r[2] = n_leaf; r[3] = n_inner; r[4] = dbg_ev; r[5] = dbg_sparse; r[6] = dbg_bcast;
+                r[7] = __popcll(gl); r[8] = __popcll(wi); r[9] = __popcll(w1); r[10] = __float_as_uint(wmax);
+                r[11] = dbg_sparse_lanes; r[12] = sins; r[13] = dbg_ins;
+            }
+        }
+    }
 #endif
     if (nbr_stats && lane == 0) {
         atomicAdd(&nbr_stats[2], (unsigned long long)n_leaf);
@@ -515,17 +546,18 @@ __global__ __launch_bounds__(kWaveBlock) void k_finish(TreeView t, const float4*
     const int i = active ? (int)qperm[slot] : 0;
     float xf[3] = {0.f, 0.f, 0.f};
     double ns[3] = {0, 0, 0};
-    int cat = -2, kq = 0, i1 = -1;
+    int cat = -2, kq = 0, i1 = -1, p1 = -1;
     float yf[3] = {0, 0, 0}, nf[3] = {0, 0, 0};
     if (active) {
         transform_query(pose, spt[i], snr[i], kp.transform_normal, xf, ns);
         const double xd[3] = {xf[0], xf[1], xf[2]};
         const float W = wlist[slot];
         double ed[KL];
-        int eo[KL];
+        int eo[KL], ep[KL];
 #pragma unroll
         for (int j = 0; j < KL; ++j) {
             const int pos = lists[(size_t)j * N + slot];
+            ep[j] = pos;
             if (pos >= 0) {
                 const float4 q = t.mpt[pos];
                 ed[j] = exact_d2(xd, q.x, q.y, q.z);
@@ -545,11 +577,13 @@ __global__ __launch_bounds__(kWaveBlock) void k_finish(TreeView t, const float4*
                 for (int j = par; j + 1 < KL; j += 2) {
                     const bool sw = lessp(ed[j + 1], eo[j + 1], ed[j], eo[j]);
                     const double td = ed[j];
-                    const int to = eo[j];
+                    const int to = eo[j], tp = ep[j];
                     ed[j] = sw ? ed[j + 1] : ed[j];
                     eo[j] = sw ? eo[j + 1] : eo[j];
+                    ep[j] = sw ? ep[j + 1] : ep[j];
                     ed[j + 1] = sw ? td : ed[j + 1];
                     eo[j + 1] = sw ? to : eo[j + 1];
+                    ep[j + 1] = sw ? tp : ep[j + 1];
                     swapped |= sw;
                 }
             }
@@ -562,7 +596,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_finish(TreeView t, const float4*
         for (int j = 0; j < KL; ++j) {
             const bool in = ed[j] <= r2;
             cnt_r += in ? 1 : 0;
-            if (in && i1 < 0 && ed[j] > DBL_EPSILON) { d1 = ed[j]; i1 = eo[j]; }
+            if (in && i1 < 0 && ed[j] > DBL_EPSILON) { d1 = ed[j]; i1 = eo[j]; p1 = ep[j]; }
             if (j == K - 1) dK = ed[j];
         }
         const bool full = W < kInfF;
@@ -578,7 +612,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_finish(TreeView t, const float4*
             fb_list[pos] = (unsigned)i;
             cat = -3;                                         // deferred to k_project_lane
         } else {
-            cat = finish_query<KL>(xf, ns, ed, eo, 0, min(K, cnt_r), d1, i1, t, kp, yf, nf, kq);
+            cat = finish_query<KL>(xf, ns, ed, ep, 0, min(K, cnt_r), d1, p1, t, kp, yf, nf, kq);
             store_result(i, cat, xf, yf, nf, cs, cd, cn);
         }
     }
@@ -703,7 +737,10 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(TreeView t, const f
 #pragma unroll
             for (int j = 0; j < KCAP; ++j) cnt += (j >= KCAP - K && ld[j] < kInfD) ? 1 : 0;
             nn_found = i1 != 0x7fffffff;
-            cat = finish_query<KCAP>(xf, ns, ld, li, KCAP - K, cnt, d1, nn_found ? i1 : -1, t, kp, yf, nf, kq);
+            int lpos[KCAP];
+#pragma unroll
+            for (int j = 0; j < KCAP; ++j) lpos[j] = (li[j] >= 0 && li[j] != 0x7fffffff) ? (int)t.ipos[li[j]] : 0;
+            cat = finish_query<KCAP>(xf, ns, ld, lpos, KCAP - K, cnt, d1, nn_found ? (int)t.ipos[i1] : -1, t, kp, yf, nf, kq);
             store_result(i, cat, xf, yf, nf, cs, cd, cn);
         }
         if (cat >= 0) atomicAdd(&rej_s[cat], 1u);
@@ -777,3 +814,11 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
 }
 
 }  // namespace imlsgpu
+
+#ifdef IMLS_DEBUG_WAVE_TRACE
+// debug build only: per-wave records of the last k_knn_wave launch (16 u32 per wave)
+extern "C" int imls_debug_waves(unsigned* out, int nwaves) {
+    const int n = nwaves < imlsgpu::kDbgWaves ? nwaves : imlsgpu::kDbgWaves;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(imlsgpu::g_dbg_wave), (size_t)n * 64) == hipSuccess ? n : -1;
+}
+#endif
