@@ -36,6 +36,8 @@ struct imls_ctx {
     bool has_source = false;
     // correspondences + solver state
     DevBuf cs, cd, cn, solve_mem, trace_mem, stats, rows_d, pose_tmp;
+    DevBuf ransac_mem, rng;               // RANSAC scratch + the glibc rand() state (34 words)
+    int rng_seed_state[34] = {};          // host copy of the seeded state (source of the async upload)
     SolveState st{};
     int st_N = -1, trace_cap = 0;
     bool has_corr = false;
@@ -103,8 +105,16 @@ int check_params(imls_ctx* c, const imls_params* p) {
     if (p->use_tensor_voting && !p->get_normals) return fail(c, IMLS_ERR_UNSUPPORTED, "tensor voting normals are not on the GPU path");
     if (p->use_projected_distance) return fail(c, IMLS_ERR_UNSUPPORTED, "use_projected_distance is not built on the GPU path yet");
     if (!p->get_normals && p->recompute_normal_count_mode) return fail(c, IMLS_ERR_UNSUPPORTED, "recompute-normal count mode is not on the GPU path");
-    if (p->solve_method != IMLS_SOLVE_LS && p->solve_method != IMLS_SOLVE_WEIGHTED_LS)
-        return fail(c, IMLS_ERR_UNSUPPORTED, "solve_method RANSAC is not built on the GPU path yet");
+    if (p->solve_method != IMLS_SOLVE_LS && p->solve_method != IMLS_SOLVE_WEIGHTED_LS && p->solve_method != IMLS_SOLVE_RANSAC)
+        return fail(c, IMLS_ERR_UNSUPPORTED, "solve_method must be LS, Weighted LS or RANSAC (Ceres/ICP/Teaser stay on the CPU path)");
+    if (p->solve_method == IMLS_SOLVE_RANSAC) {
+        if (p->ransac_final_method != IMLS_FINAL_LS && p->ransac_final_method != IMLS_FINAL_WEIGHTED_LS &&
+            p->ransac_final_method != IMLS_FINAL_DRPM)
+            return fail(c, IMLS_ERR_ARG, "RANSAC final_solve_method must be LS, Weighted LS or DRPM");
+        if (p->ransac_max_iterations < 1) return fail(c, IMLS_ERR_ARG, "RANSAC max_iterations < 1");
+        if (!(p->ransac_ls_threshold >= 0 && p->ransac_ls_threshold < 0.5))
+            return fail(c, IMLS_ERR_ARG, "RANSAC LS threshold must be in [0, 0.5)");
+    }
     if (p->iterations < 0) return fail(c, IMLS_ERR_ARG, "iterations < 0");
     if (!(p->ls_threshold >= 0 && p->ls_threshold < 0.5)) return fail(c, IMLS_ERR_ARG, "LS threshold must be in [0, 0.5)");
     return IMLS_OK;
@@ -148,6 +158,47 @@ int ensure_solve(imls_ctx* c, int N) {
     s.partial_cap = pb;
     c->st_N = (int)n;
     return IMLS_OK;
+}
+
+RansacParams ransac_params(const imls_params& p) {
+    RansacParams r;
+    r.max_iterations = p.ransac_max_iterations;
+    r.distance_threshold = p.ransac_distance_threshold;
+    r.min_inliers_percentage = p.ransac_min_inliers_percentage;
+    r.huber_threshold = p.ransac_huber_threshold;
+    r.final_method = p.ransac_final_method;
+    r.ls_threshold = p.ransac_ls_threshold;
+    r.drpm_threshold = p.drpm_threshold;
+    r.drpm_stdev_points = p.drpm_stdev_points;
+    r.drpm_stdev_normals = p.drpm_stdev_normals;
+    return r;
+}
+
+// RANSAC scratch for `rows` rows and the rand() state re-seeded from params.ransac_seed (per frame
+// and per stand-alone solve, as the oracle does); async on the context stream.
+int prepare_ransac(imls_ctx* c, int rows) {
+    if (c->P.solve_method != IMLS_SOLVE_RANSAC) return IMLS_OK;
+    if (!grow(c->ransac_mem, ransac_bytes(rows)) || !grow(c->rng, 34 * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (RANSAC)");
+    ransac_seed_host(c->P.ransac_seed, c->rng_seed_state);
+    hipMemcpyAsync(c->rng.p, c->rng_seed_state, 34 * 4, hipMemcpyHostToDevice, c->stream);
+    return IMLS_OK;
+}
+
+SolveLaunch solve_launch(imls_ctx* c, imls_iter_trace* tr, int update_pose) {
+    SolveLaunch L{};
+    L.N = c->N;
+    L.blocks1 = project_blocks(c->N);
+    L.kp = c->kp;
+    L.cs = (const float4*)c->cs.p;
+    L.cd = (const float4*)c->cd.p;
+    L.cn = (const float4*)c->cn.p;
+    L.st = c->st;
+    L.tr = tr;
+    L.update_pose = update_pose;
+    L.scratch = c->ransac_mem.p;
+    L.rng = (int*)c->rng.p;
+    L.ransac = ransac_params(c->P);
+    return L;
 }
 
 int ensure_trace(imls_ctx* c, int iters) {
@@ -351,7 +402,7 @@ void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
+    DevBuf* bufs[] = {&c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
                       &c->upload_t, &c->spt, &c->snr, &c->sscratch,
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
@@ -462,22 +513,26 @@ int imls_solve(imls_ctx* c, double delta_out[16], int* ok) {
     if (!c->has_corr) return fail(c, IMLS_ERR_STATE, "imls_project first");
     if (int rc = check_device(c)) return rc;
     hipMemsetAsync(c->st.done, 0, 16, c->stream);
+    hipMemsetAsync(c->st.status, 0, 16, c->stream);
+    if (int rc = prepare_ransac(c, c->N)) return rc;
     int slot;
     timed_begin(c, 2, slot);
-    launch_solve_chain(c->stream, c->N, project_blocks(c->N), c->kp, (const float4*)c->cs.p, (const float4*)c->cd.p,
-                       (const float4*)c->cn.p, nullptr, nullptr, c->st, nullptr, 0, 0);
+    launch_solve(c->stream, solve_launch(c, nullptr, 0));
     timed_end(c, 2, slot);
+    int status = 0;
     hipMemcpyAsync(delta_out, c->st.delta, 16 * 8, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(&status, c->st.status, sizeof(int), hipMemcpyDeviceToHost, c->stream);
     if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "solve failed");
     harvest_timing(c);
-    if (ok) *ok = 1;
+    if (ok) *ok = status == IMLS_FRAME_SOLVE_FAILED ? 0 : 1;
     return IMLS_OK;
 }
 
 int imls_solve_correspondences(imls_ctx* c, int32_t method, const double* s, const double* d, const double* n,
                                const double* w, size_t N, double delta_out[16], int* ok) {
     if (!c || !s || !d || !n || !delta_out) return IMLS_ERR_ARG;
-    if (method != IMLS_SOLVE_LS && method != IMLS_SOLVE_WEIGHTED_LS) return fail(c, IMLS_ERR_UNSUPPORTED, "method");
+    if (method != IMLS_SOLVE_LS && method != IMLS_SOLVE_WEIGHTED_LS && method != IMLS_SOLVE_RANSAC)
+        return fail(c, IMLS_ERR_UNSUPPORTED, "method");
     if (N > (size_t)0x3fffffff) return fail(c, IMLS_ERR_ARG, "N too large");
     if (int rc = check_device(c)) return rc;
     if (int rc = ensure_solve(c, (int)std::max<size_t>(N, 1))) return rc;
@@ -493,12 +548,26 @@ int imls_solve_correspondences(imls_ctx* c, int32_t method, const double* s, con
         dw = r + 9 * N;
     }
     hipMemsetAsync(c->st.done, 0, 16, c->stream);
-    KParams kp = c->kp;
-    kp.solve_method = method;
-    launch_solve_chain(c->stream, (int)N, 0, kp, nullptr, nullptr, nullptr, r, dw, c->st, nullptr, 0, 1);
+    hipMemsetAsync(c->st.status, 0, 16, c->stream);
+    const int saved = c->P.solve_method;
+    c->P.solve_method = method;
+    const int rc0 = prepare_ransac(c, (int)std::max<size_t>(N, 1));
+    c->P.solve_method = saved;
+    if (rc0) return rc0;
+    SolveLaunch L = solve_launch(c, nullptr, 0);
+    L.N = (int)N;
+    L.blocks1 = 0;
+    L.kp.solve_method = method;
+    L.cs = L.cd = L.cn = nullptr;
+    L.rows_d = r;
+    L.weights = dw;
+    L.rows_are_double = 1;
+    launch_solve(c->stream, L);
+    int status = 0;
     hipMemcpyAsync(delta_out, c->st.delta, 16 * 8, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(&status, c->st.status, sizeof(int), hipMemcpyDeviceToHost, c->stream);
     if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "solve failed");
-    if (ok) *ok = 1;
+    if (ok) *ok = status == IMLS_FRAME_SOLVE_FAILED ? 0 : 1;
     return IMLS_OK;
 }
 
@@ -519,6 +588,7 @@ int imls_register_frame_async(imls_ctx* c) {
     hipMemsetAsync(c->stats.p, 0, 128, c->stream);
     imls_iter_trace* tr = (imls_iter_trace*)c->trace_mem.p;
     const TreeView tv = tree_view(c);
+    if (int rc = prepare_ransac(c, c->N)) return rc;
     for (int it = 0; it < iters; ++it) {
         int slot;
         timed_begin(c, 0, slot);
@@ -528,8 +598,7 @@ int imls_register_frame_async(imls_ctx* c) {
                        c->st.delta, (int*)c->prevnn.p, it > 0 && c->temporal_seed);
         timed_end(c, 0, slot);
         timed_begin(c, 2, slot);
-        launch_solve_chain(c->stream, c->N, project_blocks(c->N), c->kp, (const float4*)c->cs.p, (const float4*)c->cd.p,
-                           (const float4*)c->cn.p, nullptr, nullptr, c->st, tr + it, 1, 0);
+        launch_solve(c->stream, solve_launch(c, tr + it, 1));
         timed_end(c, 2, slot);
     }
     hipMemcpyAsync(c->h_misc, c->st.pose, 16 * 8, hipMemcpyDeviceToHost, c->stream);

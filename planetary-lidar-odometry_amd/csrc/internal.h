@@ -122,14 +122,44 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
                     const unsigned* qperm, int N, const double* pose, const int* done, const KParams& kp,
                     float4* cs, float4* cd, float4* cn, double* partial1, imls_iter_trace* tr,
                     unsigned long long* nbr_stats, unsigned* fb_list, unsigned* fb_count, int lane_mode,
-                    const double* delta, int* lists, int use_prev);   // delta: last pose increment (use_prev)   // lists: [KL][N] positions + [N] worst keys, kept across iterations
+                    const double* delta, int* lists, int use_prev);
+// delta: last pose increment (read when use_prev); lists: [KL][N] positions + [N] worst keys,
+// kept across ICP iterations (temporal seed)
 constexpr int kMaxKL = 36;
 int project_blocks(int N);
 
 // solve.hip
 void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, const float4* cs,
                         const float4* cd, const float4* cn, const double* rows_d, const double* weights,
-                        SolveState& st, imls_iter_trace* tr, int update_pose, int rows_are_double);
+                        SolveState& st, imls_iter_trace* tr, int update_pose, int rows_are_double,
+                        const int* count = nullptr, const double* wsum = nullptr);
 int solve_blocks(int N);
+
+// ransac.hip — RANSAC (+ final LS / weighted LS / DRPM) and the solve-method dispatcher
+constexpr int kHypMax = 4096;          // hypotheses per chunk (chunks grow 16, 64, 256, 1024, 4096)
+struct RansacParams {
+    int max_iterations;
+    double distance_threshold, min_inliers_percentage, huber_threshold;
+    int final_method;                  // imls_final_method
+    double ls_threshold, drpm_threshold, drpm_stdev_points, drpm_stdev_normals;
+};
+struct SolveLaunch {
+    int N;                             // rows (float rows: source count; fp64 rows: row count)
+    int blocks1;                       // pass-1 slabs already in st.partial1 (float rows from k_finish)
+    KParams kp;
+    const float4 *cs, *cd, *cn;
+    const double* rows_d;              // fp64 rows [s 3N | d 3N | n 3N] (host API) or null
+    const double* weights;
+    SolveState st;
+    imls_iter_trace* tr;
+    int update_pose, rows_are_double;
+    const int* count;
+    void* scratch;                     // ransac_bytes(N) device bytes (RANSAC only)
+    int* rng;                          // [34] glibc rand() state, device (RANSAC only)
+    RansacParams ransac;
+};
+void launch_solve(hipStream_t s, const SolveLaunch& L);
+size_t ransac_bytes(int cap);
+void ransac_seed_host(uint32_t seed, int st[34]);
 
 }  // namespace imlsgpu

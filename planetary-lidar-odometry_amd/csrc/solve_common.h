@@ -1,0 +1,267 @@
+// solve_common.h — device helpers shared by the LS chain (solve.hip) and the RANSAC / DRPM
+// solvers (ransac.hip): the correspondence-row accessor, block reductions, the 6×6 column-pivoted
+// solve, Δ from x (Rodrigues + polar factor) and the pose update / convergence test.
+#pragma once
+#include <cfloat>
+
+#include "internal.h"
+
+namespace imlsgpu {
+
+// One correspondence row of the point-to-plane system (solver.cpp:89-107).
+struct Rows {
+    const float4 *cs, *cd, *cn;           // float rows from the projection (valid flag in cs.w)
+    const double *ds, *dd, *dn, *w;       // or double rows (host API / RANSAC inliers), all valid
+    int is_double;
+    const int* count;                     // double rows: device-side row count (rows ≥ count absent)
+    const double* wsum;                   // weights are w[i] / *wsum when set (RANSAC normalisation)
+    __device__ __forceinline__ bool get(int i, double a[6], double& b, double& wt) const {
+        double s[3], d[3], n[3];
+        if (is_double) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { s[k] = ds[3 * i + k]; d[k] = dd[3 * i + k]; n[k] = dn[3 * i + k]; }
+            if (count && i >= *count) return false;
+            wt = w ? (wsum ? w[i] / *wsum : w[i]) : 1.0;
+        } else {
+            const float4 s4 = cs[i];
+            if (s4.w == 0.f) return false;
+            const float4 d4 = cd[i], n4 = cn[i];
+            s[0] = s4.x; s[1] = s4.y; s[2] = s4.z;
+            d[0] = d4.x; d[1] = d4.y; d[2] = d4.z;
+            n[0] = n4.x; n[1] = n4.y; n[2] = n4.z;
+            wt = 1.0;
+        }
+        // solver.cpp:95-103
+        a[0] = n[2] * s[1] - n[1] * s[2];
+        a[1] = n[0] * s[2] - n[2] * s[0];
+        a[2] = n[1] * s[0] - n[0] * s[1];
+        a[3] = n[0]; a[4] = n[1]; a[5] = n[2];
+        b = n[0] * (d[0] - s[0]);
+        b = b + n[1] * (d[1] - s[1]);
+        b = b + n[2] * (d[2] - s[2]);
+        return true;
+    }
+};
+
+// pass 1 of the LS chain (weighted normal equations) on any rows; solve.hip
+void launch_rows_pass1(hipStream_t s, const Rows& rows, int N, double* partial, int blocks);
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-reduce the 28 normal-equation terms of (a, b, weight, count); result valid in thread 0's
+// `out` (all threads must call).  red: [nwaves][28] LDS.
+template <int NT>
+__device__ void block_normeq(const double a[6], double b, double cnt, double* red, double out[kNormEq]) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int k = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = r; c < 6; ++c) {
+            const double v = wave_sum(a[r] * a[c]);
+            if (lane == 0) red[wv * kNormEq + k] = v;
+            ++k;
+        }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        const double v = wave_sum(a[r] * b);
+        if (lane == 0) red[wv * kNormEq + 21 + r] = v;
+    }
+    {
+        const double v = wave_sum(cnt);
+        if (lane == 0) red[wv * kNormEq + 27] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNormEq) {
+        double s = 0.0;
+        for (int w = 0; w < NT / 64; ++w) s += red[w * kNormEq + threadIdx.x];
+        out[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+// Block-sum 28 per-thread values (all threads call); result in out[0..27] (LDS) after the call.
+template <int NT>
+__device__ void block_sum28(const double (&v)[kNormEq], double* red, double* out) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kNormEq; ++k) {
+        const double s = wave_sum(v[k]);
+        if (lane == 0) red[wv * kNormEq + k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNormEq) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) s += red[w * kNormEq + threadIdx.x];
+        out[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+// Column-pivoted Cholesky solve of the 6×6 normal equations (see file header).  Unknowns past the
+// numerical rank are set to zero (Eigen's basic solution).  Returns the rank.
+__device__ int solve6(const double* ne, double x[6]) {
+    // every index below is a compile-time constant (full unroll; the pivot swap is a predicated
+    // swap over the candidate rows), so the system stays in registers — no scratch traffic
+    double A[6][6], g[6];
+    int perm[6];
+    {
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = r; c < 6; ++c) { A[r][c] = ne[k]; A[c][r] = ne[k]; ++k; }
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) { g[r] = ne[21 + r]; perm[r] = r; }
+    const double eps = DBL_EPSILON;
+    double maxpiv = 0.0;
+    int rank = 6;
+    bool stop = false;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        if (!stop) {
+            int p = j;
+            double best = A[j][j];
+#pragma unroll
+            for (int q = j + 1; q < 6; ++q)
+                if (A[q][q] > best) { best = A[q][q]; p = q; }
+#pragma unroll
+            for (int q = j + 1; q < 6; ++q) {
+                if (q == p) {
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) { const double t = A[j][c]; A[j][c] = A[q][c]; A[q][c] = t; }
+#pragma unroll
+                    for (int r = 0; r < 6; ++r) { const double t = A[r][j]; A[r][j] = A[r][q]; A[r][q] = t; }
+                    const double t = g[j]; g[j] = g[q]; g[q] = t;
+                    const int ti = perm[j]; perm[j] = perm[q]; perm[q] = ti;
+                }
+            }
+            const double d = A[j][j];
+            const double rkk = d > 0 ? sqrt(d) : 0.0;
+            if (rkk > maxpiv) maxpiv = rkk;
+            if (!(rkk > eps * 6.0 * maxpiv) || !(d > 0)) {
+                rank = j;
+                stop = true;
+            } else {
+                A[j][j] = rkk;
+#pragma unroll
+                for (int r = j + 1; r < 6; ++r) A[r][j] = A[r][j] / rkk;
+#pragma unroll
+                for (int r = j + 1; r < 6; ++r)
+#pragma unroll
+                    for (int c = j + 1; c <= r; ++c) {
+                        A[r][c] = A[r][c] - A[r][j] * A[c][j];
+                        A[c][r] = A[r][c];
+                    }
+            }
+        }
+    }
+    double y[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        if (r < rank) {
+            double s = g[r];
+#pragma unroll
+            for (int c = 0; c < r; ++c) s -= A[r][c] * y[c];
+            y[r] = s / A[r][r];
+        }
+    }
+#pragma unroll
+    for (int r = 5; r >= 0; --r) {
+        if (r < rank) {
+            double s = y[r];
+#pragma unroll
+            for (int c = r + 1; c < 6; ++c)
+                if (c < rank) s -= A[c][r] * y[c];
+            y[r] = s / A[r][r];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        double v = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+            if (r < rank && perm[r] == k) v = y[r];
+        x[k] = v;
+    }
+    return rank;
+}
+
+// Δ from x (solver.cpp:140-163): R = AngleAxis(‖ω‖, ω̂) (Eigen AngleAxis::toRotationMatrix), then
+// the JacobiSVD U·Vᵀ re-orthonormalisation as the polar factor (Newton iteration).
+__device__ void delta_from_x(const double x[6], double D[16]) {
+    const double wx = x[0], wy = x[1], wz = x[2];
+    double sq = wx * wx;
+    sq = sq + wy * wy;
+    sq = sq + wz * wz;
+    const double ang = sqrt(sq);
+    double ax = 0, ay = 0, az = 0;
+    if (sq > 0) { const double nr = sqrt(sq); ax = wx / nr; ay = wy / nr; az = wz / nr; }
+    const double s = sin(ang), c = cos(ang);
+    const double sx = s * ax, sy = s * ay, sz = s * az;
+    const double c1x = (1 - c) * ax, c1y = (1 - c) * ay, c1z = (1 - c) * az;
+    double R[9];
+    double tmp = c1x * ay; R[1] = tmp - sz; R[3] = tmp + sz;
+    tmp = c1x * az; R[2] = tmp + sy; R[6] = tmp - sy;
+    tmp = c1y * az; R[5] = tmp - sx; R[7] = tmp + sx;
+    R[0] = c1x * ax + c; R[4] = c1y * ay + c; R[8] = c1z * az + c;
+    for (int it = 0; it < 20; ++it) {
+        const double* a = R;
+        const double det = a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) + a[2] * (a[3] * a[7] - a[4] * a[6]);
+        if (det == 0) break;
+        const double cof[9] = {a[4] * a[8] - a[5] * a[7], a[5] * a[6] - a[3] * a[8], a[3] * a[7] - a[4] * a[6],
+                               a[2] * a[7] - a[1] * a[8], a[0] * a[8] - a[2] * a[6], a[1] * a[6] - a[0] * a[7],
+                               a[1] * a[5] - a[2] * a[4], a[2] * a[3] - a[0] * a[5], a[0] * a[4] - a[1] * a[3]};
+        double maxd = 0, n[9];
+        for (int k = 0; k < 9; ++k) { n[k] = 0.5 * (a[k] + cof[k] / det); maxd = fmax(maxd, fabs(n[k] - a[k])); }
+        for (int k = 0; k < 9; ++k) R[k] = n[k];
+        if (maxd < 1e-16) break;
+    }
+    for (int k = 0; k < 16; ++k) D[k] = 0.0;
+    for (int r = 0; r < 3; ++r) for (int cc = 0; cc < 3; ++cc) D[r * 4 + cc] = R[r * 3 + cc];
+    D[3] = x[3]; D[7] = x[4]; D[11] = x[5]; D[15] = 1.0;
+}
+
+// rPose = Δ·rPose, trace, convergence (laser_odometry.cpp:619-646); single thread.
+__device__ void finish_iteration(SolveState st, imls_iter_trace* tr, const double D[16], double nvalid, double nkept,
+                                 int update_pose, const KParams& kp) {
+    for (int k = 0; k < 16; ++k) st.delta[k] = D[k];
+    if (tr) {
+        for (int k = 0; k < 16; ++k) tr->delta[k] = D[k];
+        tr->n_valid = (unsigned long long)nvalid;
+        tr->n_kept = (unsigned long long)nkept;
+    }
+    if (!update_pose) return;
+    double Pn[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = D[i * 4 + 0] * st.pose[0 * 4 + j];
+            s = s + D[i * 4 + 1] * st.pose[1 * 4 + j];
+            s = s + D[i * 4 + 2] * st.pose[2 * 4 + j];
+            s = s + D[i * 4 + 3] * st.pose[3 * 4 + j];
+            Pn[i * 4 + j] = s;
+        }
+    for (int k = 0; k < 16; ++k) st.pose[k] = Pn[k];
+    if (tr) for (int k = 0; k < 16; ++k) tr->pose[k] = Pn[k];
+    *st.iters += 1;
+    const double dd = sqrt(D[3] * D[3] + D[7] * D[7] + D[11] * D[11]);
+    double ct = ((D[0] + D[5] + D[10]) - 1.0) / 2.0;
+    ct = fmin(1.0, fmax(ct, -1.0));
+    const double da = acos(ct);
+    if (dd < kp.delta_dist && da < kp.delta_angle) {
+        *st.status = IMLS_FRAME_CONVERGED;
+        *st.done = 1;
+    }
+}
+
+
+}  // namespace
+}  // namespace imlsgpu
