@@ -153,6 +153,8 @@ def main():
     proj_ms, proj_n = tsum(0)
     idx_ms, idx_n = tsum(1)
     sol_ms, sol_n = tsum(2)
+    knn_ms, knn_n = tsum(3)
+    fin_ms, fin_n = tsum(4)
     ctx = ctxs[0]
     stats = ctx.index_stats()
     trav = ctx.traversal_stats()
@@ -171,6 +173,8 @@ def main():
             dist.destroy_process_group()
         return
 
+    # HBM traffic per projection launch from the committed PMC pass (tools/pmc_traffic.py):
+    # 2·FETCH_SIZE + WRITE_SIZE of k_knn_wave + k_finish (gfx950 FETCH_SIZE counts ½ of wide reads)
     traffic = None
     tj = pathlib.Path(args.traffic_json)
     if tj.exists():
@@ -178,7 +182,7 @@ def main():
             tdat = json.loads(tj.read_text())
             if tdat.get("queries") == stats["queries"] and tdat.get("iters") == args.iters:
                 traffic = tdat.get("bytes_per_launch")
-        except Exception:
+        except (ValueError, OSError):
             traffic = None
 
     cpu = None
@@ -216,7 +220,8 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_project (fused transform + exact radius kNN + IMLS projection + pass-1 normal equations)",
+            "kernel": "projection step = k_knn_wave (packet traversal) + k_finish (exact re-rank, gates, IMLS, "
+                      "pass-1 normal equations) + k_project_lane (fallback, normally 0 queries)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -225,6 +230,7 @@ def main():
             "algorithmic_bytes_per_launch": bytes_launch,
             "avg_launch_ms": avg_proj_s * 1e3,
             "launches": int(proj_n),
+            "kernel_avg_ms": {"k_knn_wave": knn_ms / max(knn_n, 1), "k_finish": fin_ms / max(fin_n, 1)},
             "aggregate_algorithmic_GBps": aggregate,
         },
         "breakdown_ms_per_pair": {     # summed per-pair stream time (overlaps across pairs in flight)

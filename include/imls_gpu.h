@@ -218,7 +218,8 @@ int imls_register_frame_result(imls_ctx* ctx, double pose_out[16], int* iters_ru
 /* ---- instrumentation ------------------------------------------------------------------- */
 /* When enabled, HIP events bracket every launch of the projection kernel (on the stream it is
  * launched on); imls_kernel_timing returns the accumulated milliseconds and launch count since
- * the last reset.  kernel: 0 = projection, 1 = index build (all its kernels), 2 = solve chain. */
+ * the last reset.  kernel: 0 = projection (all its kernels), 1 = index build (all its kernels),
+ * 2 = solve chain, 3 = k_knn_wave (packet traversal) alone, 4 = k_finish (exact stage) alone. */
 int imls_enable_timing(imls_ctx* ctx, int enable);
 int imls_kernel_timing(imls_ctx* ctx, int kernel, double* total_ms, uint64_t* launches);
 int imls_reset_timing(imls_ctx* ctx);

@@ -14,6 +14,8 @@
 
 using namespace imlsgpu;
 
+constexpr int kTimingKinds = 5;   // projection, index, solve chain, k_knn_wave, k_finish
+
 struct imls_ctx {
     int device = 0;
     hipStream_t own = nullptr, stream = nullptr;
@@ -50,9 +52,9 @@ struct imls_ctx {
     bool timing = false;
     std::vector<hipEvent_t> ev;
     int ev_used = 0;
-    std::vector<std::pair<int, int>> ev_pairs[3];
-    double t_ms[3] = {0, 0, 0};
-    uint64_t t_n[3] = {0, 0, 0};
+    std::vector<std::pair<int, int>> ev_pairs[kTimingKinds];
+    double t_ms[kTimingKinds] = {};
+    uint64_t t_n[kTimingKinds] = {};
 };
 
 namespace {
@@ -256,8 +258,21 @@ void timed_end(imls_ctx* c, int kind, int slot) {
     hipEventRecord(c->ev[slot + 1], c->stream);
     c->ev_pairs[kind].push_back({slot, slot + 1});
 }
+// Events around the two projection kernels (kinds 3 and 4): marks[0..2], or null when off.
+hipEvent_t* project_marks(imls_ctx* c, hipEvent_t marks[3]) {
+    if (!c->timing) return nullptr;
+    const int a = ev_pair(c), b = ev_pair(c);
+    if (a < 0 || b < 0) return nullptr;
+    marks[0] = c->ev[a];
+    marks[1] = c->ev[a + 1];
+    marks[2] = c->ev[b];
+    c->ev_pairs[3].push_back({a, a + 1});
+    c->ev_pairs[4].push_back({a + 1, b});
+    return marks;
+}
+
 void harvest_timing(imls_ctx* c) {
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < kTimingKinds; ++k) {
         for (auto& pr : c->ev_pairs[k]) {
             float ms = 0;
             if (hipEventElapsedTime(&ms, c->ev[pr.first], c->ev[pr.second]) == hipSuccess) {
@@ -477,11 +492,12 @@ int imls_project(imls_ctx* c, const double pose[16], float* x_out, float* y_out,
     hipMemsetAsync(c->st.trace, 0, sizeof(imls_iter_trace), c->stream);
     hipMemsetAsync(c->stats.p, 0, 128, c->stream);
     int slot;
+    hipEvent_t marks[3];
     timed_begin(c, 0, slot);
     launch_project(c->stream, tree_view(c), (const float4*)c->spt.p, (const float4*)c->snr.p, (const unsigned*)c->qperm.p,
                    c->N, dpose, dzero, c->kp, (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p, c->st.partial1,
                    c->st.trace, (unsigned long long*)c->stats.p, fb_list(c), fb_count(c), c->lane_mode,
-                   nullptr, (int*)c->prevnn.p, 0);
+                   nullptr, (int*)c->prevnn.p, 0, project_marks(c, marks));
     timed_end(c, 0, slot);
     std::vector<float> hs((size_t)c->N * 4), hd((size_t)c->N * 4), hn((size_t)c->N * 4);
     imls_iter_trace tr;
@@ -591,11 +607,12 @@ int imls_register_frame_async(imls_ctx* c) {
     if (int rc = prepare_ransac(c, c->N)) return rc;
     for (int it = 0; it < iters; ++it) {
         int slot;
+        hipEvent_t marks[3];
         timed_begin(c, 0, slot);
         launch_project(c->stream, tv, (const float4*)c->spt.p, (const float4*)c->snr.p, (const unsigned*)c->qperm.p, c->N,
                        c->st.pose, c->st.done, c->kp, (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p,
                        c->st.partial1, tr + it, (unsigned long long*)c->stats.p, fb_list(c), fb_count(c), c->lane_mode,
-                       c->st.delta, (int*)c->prevnn.p, it > 0 && c->temporal_seed);
+                       c->st.delta, (int*)c->prevnn.p, it > 0 && c->temporal_seed, project_marks(c, marks));
         timed_end(c, 0, slot);
         timed_begin(c, 2, slot);
         launch_solve(c->stream, solve_launch(c, tr + it, 1));
@@ -643,7 +660,7 @@ int imls_enable_timing(imls_ctx* c, int enable) {
 }
 
 int imls_kernel_timing(imls_ctx* c, int kernel, double* total_ms, uint64_t* launches) {
-    if (!c || kernel < 0 || kernel > 2) return IMLS_ERR_ARG;
+    if (!c || kernel < 0 || kernel >= kTimingKinds) return IMLS_ERR_ARG;
     if (total_ms) *total_ms = c->t_ms[kernel];
     if (launches) *launches = c->t_n[kernel];
     return IMLS_OK;
@@ -651,7 +668,7 @@ int imls_kernel_timing(imls_ctx* c, int kernel, double* total_ms, uint64_t* laun
 
 int imls_reset_timing(imls_ctx* c) {
     if (!c) return IMLS_ERR_ARG;
-    for (int k = 0; k < 3; ++k) { c->t_ms[k] = 0; c->t_n[k] = 0; c->ev_pairs[k].clear(); }
+    for (int k = 0; k < kTimingKinds; ++k) { c->t_ms[k] = 0; c->t_n[k] = 0; c->ev_pairs[k].clear(); }
     c->ev_used = 0;
     return IMLS_OK;
 }

@@ -122,9 +122,10 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
                     const unsigned* qperm, int N, const double* pose, const int* done, const KParams& kp,
                     float4* cs, float4* cd, float4* cn, double* partial1, imls_iter_trace* tr,
                     unsigned long long* nbr_stats, unsigned* fb_list, unsigned* fb_count, int lane_mode,
-                    const double* delta, int* lists, int use_prev);
+                    const double* delta, int* lists, int use_prev, hipEvent_t* marks = nullptr);
 // delta: last pose increment (read when use_prev); lists: [KL][N] positions + [N] worst keys,
-// kept across ICP iterations (temporal seed)
+// kept across ICP iterations (temporal seed); marks: 3 events recorded before k_knn_wave, between
+// it and k_finish, and after k_finish (timing), or null
 constexpr int kMaxKL = 36;
 int project_blocks(int N);
 

@@ -773,11 +773,14 @@ template <int KL>
 void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qperm,
                  int N, const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd, float4* cn,
                  double* partial1, imls_iter_trace* tr, unsigned long long* stats, unsigned* fb_list, unsigned* fb_count,
-                 const double* delta, int* lists, int use_prev) {
+                 const double* delta, int* lists, int use_prev, hipEvent_t* marks) {
     float* wlist = reinterpret_cast<float*>(lists + (size_t)KL * N);
+    if (marks) (void)hipEventRecord(marks[0], s);
     k_knn_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, use_prev, stats);
+    if (marks) (void)hipEventRecord(marks[1], s);
     k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,
                                                stats, fb_list, fb_count);
+    if (marks) (void)hipEventRecord(marks[2], s);
 }
 
 }  // namespace
@@ -787,7 +790,7 @@ int project_blocks(int N) { return (N + kWaveBlock - 1) / kWaveBlock + kFallback
 void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qperm,
                     int N, const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd, float4* cn,
                     double* partial1, imls_iter_trace* tr, unsigned long long* stats, unsigned* fb_list,
-                    unsigned* fb_count, int lane_mode, const double* delta, int* lists, int use_prev) {
+                    unsigned* fb_count, int lane_mode, const double* delta, int* lists, int use_prev, hipEvent_t* marks) {
     const int wblocks = (N + kWaveBlock - 1) / kWaveBlock;
     double* p_fb = partial1 + (size_t)wblocks * kNormEq;
     const int K = kp.K;
@@ -802,10 +805,10 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
         return;
     }
     (void)hipMemsetAsync(fb_count, 0, sizeof(unsigned), s);
-    if (K <= 8) launch_wave<12>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev);
-    else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev);
-    else if (K <= 20) launch_wave<24>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev);
-    else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev);
+    if (K <= 8) launch_wave<12>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
+    else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
+    else if (K <= 20) launch_wave<24>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
+    else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     // exact fallback for uncertified queries (usually none; the launch exits at once then)
     if (K <= 8) launch_lane<8>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
     else if (K <= 16) launch_lane<16>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
