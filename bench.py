@@ -26,6 +26,10 @@ import numpy as np
 
 ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
+# One HIP stream per pair in flight: give the runtime 8 hardware queues (its default is 4) so the
+# 4 pair streams never share a queue with each other or the runtime's own copies.  Read by the HIP
+# runtime at initialisation, i.e. before torch touches the GPU.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("IMLS_BENCH_HW_QUEUES", "8")
 import plo_amd  # noqa: E402
 
 plo_amd.load()

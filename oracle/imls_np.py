@@ -148,6 +148,43 @@ def project(src6: np.ndarray, tgt6: np.ndarray, pose: np.ndarray, p: dict):
     return as3(xs), as3(ys), as3(ns_out), np.asarray(idx, dtype=np.int64), rej
 
 
+def project_plane_icp(src6: np.ndarray, tgt6: np.ndarray, pose: np.ndarray, p: dict):
+    """plane_ICP_proj (laser_odometry.cpp:277-413), kd-tree branch: NN-1 within picp_r (no self
+    match), unfound → "no normal", no h gate, y = x − ((x−p)·n)·n."""
+    src = filter_finite(src6)
+    tgt = filter_finite(tgt6)
+    knn = ExactKnn(tgt[:3])
+    T = np.asarray(pose, dtype=np.float64).reshape(4, 4)
+    rej = np.zeros(6, dtype=np.int64)
+    xs, ys, ns_out, idx = [], [], [], []
+    for i in range(src.shape[1]):
+        pt = src[:3, i].astype(np.float64)
+        xd = np.array([((T[r, 0] * pt[0] + T[r, 1] * pt[1]) + T[r, 2] * pt[2]) + T[r, 3] for r in range(3)])
+        xf = xd.astype(np.float32)
+        x = xf.astype(np.float64)
+        ns = src[3:, i].astype(np.float64)
+        _, i1 = knn.query(x, 1, p["picp_r"], allow_self=False)
+        if i1[0] < 0:
+            rej[0] += 1
+            continue
+        q = tgt[:3, i1[0]].astype(np.float64)
+        nn = tgt[3:, i1[0]].astype(np.float64)
+        if not np.isfinite(nn).all():
+            rej[REJ_INVALID_NORMAL] += 1
+            continue
+        if p["picp_normal_angle_constraint"] and _angle_reject(ns, nn, p["picp_angle_diff_threshold"]):
+            rej[REJ_NORMAL_CONSTRAINT] += 1
+            continue
+        v = x - q
+        pd = (v[0] * nn[0] + v[1] * nn[1]) + v[2] * nn[2]
+        xs.append(xf)
+        ys.append((x - pd * nn).astype(np.float32))
+        ns_out.append(nn.astype(np.float32))
+        idx.append(i)
+    as3 = lambda a: np.asarray(a, dtype=np.float32).reshape(-1, 3)
+    return as3(xs), as3(ys), as3(ns_out), np.asarray(idx, dtype=np.int64), rej
+
+
 def plane_system(s, d, n):
     """A = [s×n, n], b = n·(d−s) (solver.cpp:89-104)."""
     s, d, n = (np.asarray(a, dtype=np.float64) for a in (s, d, n))

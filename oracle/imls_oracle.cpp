@@ -642,15 +642,17 @@ struct Matcher {
     Cloud tgt;
     KdTree tree;
 
-    // angle test shared by imls_icp.cpp:442-451 and 681-692; NaN angles pass (Q8).
-    bool angle_reject(const double ns[3], const double nn[3]) const {
+    // angle test shared by imls_icp.cpp:442-451, 681-692 and laser_odometry.cpp:373-384; NaN
+    // angles pass (Q8).
+    static bool angle_reject_thr(const double ns[3], const double nn[3], double thr) {
         double dot = (ns[0] * nn[0] + ns[1] * nn[1]) + ns[2] * nn[2];
         double n1 = std::sqrt((ns[0] * ns[0] + ns[1] * ns[1]) + ns[2] * ns[2]);
         double n2 = std::sqrt((nn[0] * nn[0] + nn[1] * nn[1]) + nn[2] * nn[2]);
         double ca = dot / (n1 * n2);
         double angle = std::acos(ca) * 180.0 / M_PI;
-        return angle > P->angle_diff_threshold;
+        return angle > thr;
     }
+    bool angle_reject(const double ns[3], const double nn[3]) const { return angle_reject_thr(ns, nn, P->angle_diff_threshold); }
 
     // ComputeNormal (imls_icp.cpp:753-794) is reached only through the recompute branch; under
     // libnabo's knn() return-value semantics (Q1) the branch rejects before calling it.
@@ -784,6 +786,45 @@ struct Matcher {
         nn_out[0] = (float)nn[0]; nn_out[1] = (float)nn[1]; nn_out[2] = (float)nn[2];
         return -1;
     }
+
+    // plane_ICP_proj's loop body (laser_odometry.cpp:312-404): NN-1 within picp.r (no self match)
+    // or, with use_projected_distance, the brute-force minimum of ‖(p−x)×n_s‖ under the
+    // reference's swapped gate ‖p−x‖ < r·r && proj < r_proj (322); no h gate (min_dist unused);
+    // unfound → "no normal" (352-357); map normal from the cloud; y = x − ((x−p)·n)·n.
+    int project_one_plane(const float xf[3], const float nsf[3], float y[3], float nn_out[3]) const {
+        double x[3] = {xf[0], xf[1], xf[2]}, ns[3] = {nsf[0], nsf[1], nsf[2]};
+        int32_t best = -1;
+        if (P->picp_use_projected_distance) {
+            std::vector<std::pair<double, int>> pd;
+            const double rr = P->picp_r * P->picp_r;
+            for (size_t j = 0; j < tgt.size(); ++j) {
+                double dx = (double)tgt.x[j] - x[0], dy = (double)tgt.y[j] - x[1], dz = (double)tgt.z[j] - x[2];
+                double cx = dy * ns[2] - dz * ns[1], cy = dz * ns[0] - dx * ns[2], cz = dx * ns[1] - dy * ns[0];
+                double proj = std::sqrt((cx * cx + cy * cy) + cz * cz);
+                double dn = std::sqrt((dx * dx + dy * dy) + dz * dz);
+                if (dn < rr && proj < P->picp_r_proj) pd.emplace_back(proj, (int)j);
+            }
+            if (pd.empty()) return IMLS_REJ_TOO_FAR;
+            best = std::min_element(pd.begin(), pd.end())->second;
+        } else {
+            KdTree::Heap h;
+            tree.knn(x, 1, P->picp_r * P->picp_r, false, h);
+            best = h.n ? h.i[0] : -1;
+        }
+        if (best < 0 || best >= (int32_t)tgt.size()) return IMLS_REJ_NO_NORMAL;
+        double p[3] = {tgt.x[best], tgt.y[best], tgt.z[best]};
+        double nn[3] = {tgt.nx[best], tgt.ny[best], tgt.nz[best]};
+        if (!finite3(nn[0], nn[1], nn[2])) return IMLS_REJ_INVALID_NORMAL;
+        if (P->picp_normal_angle_constraint && angle_reject_thr(ns, nn, P->picp_angle_diff_threshold))
+            return IMLS_REJ_NORMAL_CONSTRAINT;
+        double v[3] = {x[0] - p[0], x[1] - p[1], x[2] - p[2]};
+        double pdist = (v[0] * nn[0] + v[1] * nn[1]) + v[2] * nn[2];
+        y[0] = (float)(x[0] - pdist * nn[0]);
+        y[1] = (float)(x[1] - pdist * nn[1]);
+        y[2] = (float)(x[2] - pdist * nn[2]);
+        nn_out[0] = (float)nn[0]; nn_out[1] = (float)nn[1]; nn_out[2] = (float)nn[2];
+        return -1;
+    }
 };
 
 // x = float(pose·[p;1]) (laser_odometry.cpp:527-549): row-wise ((m0p0 + m1p1) + m2p2) + m3.
@@ -816,7 +857,7 @@ void project_all(const Matcher& m, const Cloud& src, const double T[16], bool ro
         float x[3], ns[3] = {src.nx[i], src.ny[i], src.nz[i]}, y[3], nn[3];
         transform_point(T, src.x[i], src.y[i], src.z[i], x);
         if (rot_normals) rotate_normal(T, src.nx[i], src.ny[i], src.nz[i], ns);
-        int r = m.project_one(x, ns, y, nn);
+        int r = m.P->matching_method == IMLS_MATCH_PLANE_ICP ? m.project_one_plane(x, ns, y, nn) : m.project_one(x, ns, y, nn);
         if (r >= 0) { rej[r]++; continue; }
         c.x.insert(c.x.end(), x, x + 3);
         c.y.insert(c.y.end(), y, y + 3);

@@ -88,6 +88,14 @@ KParams make_kparams(const imls_params& p) {
     k.ls_threshold = p.ls_threshold;
     k.delta_dist = p.delta_dist_threshold;
     k.delta_angle = p.delta_angle_threshold;
+    k.matcher = p.matching_method;
+    if (p.matching_method == IMLS_MATCH_PLANE_ICP) {
+        // plane_ICP_proj (laser_odometry.cpp:295-299, 346-350): NN-1 within its own r and angle gate
+        k.r2 = p.picp_r * p.picp_r;
+        k.K = 1;
+        k.angle_on = p.picp_normal_angle_constraint ? 1 : 0;
+        k.angle_thr_deg = p.picp_angle_diff_threshold;
+    }
     k.seed_half = 1;
     k.reseed = 0.25f;
     k.sparse_lanes = 32;
@@ -103,7 +111,10 @@ KParams make_kparams(const imls_params& p) {
 int check_params(imls_ctx* c, const imls_params* p) {
     if (!p) return fail(c, IMLS_ERR_ARG, "null params");
     if (p->search_number < 1 || p->search_number > 32) return fail(c, IMLS_ERR_UNSUPPORTED, "search_number must be in [1, 32]");
-    if (p->matching_method != IMLS_MATCH_IMLS) return fail(c, IMLS_ERR_UNSUPPORTED, "matching_method plane_ICP is not built on the GPU path yet");
+    if (p->matching_method != IMLS_MATCH_IMLS && p->matching_method != IMLS_MATCH_PLANE_ICP)
+        return fail(c, IMLS_ERR_ARG, "matching_method must be IMLS or plane_ICP");
+    if (p->matching_method == IMLS_MATCH_PLANE_ICP && p->picp_use_projected_distance)
+        return fail(c, IMLS_ERR_UNSUPPORTED, "plane_ICP use_projected_distance is not built on the GPU path yet");
     if (p->use_tensor_voting && !p->get_normals) return fail(c, IMLS_ERR_UNSUPPORTED, "tensor voting normals are not on the GPU path");
     if (p->use_projected_distance) return fail(c, IMLS_ERR_UNSUPPORTED, "use_projected_distance is not built on the GPU path yet");
     if (!p->get_normals && p->recompute_normal_count_mode) return fail(c, IMLS_ERR_UNSUPPORTED, "recompute-normal count mode is not on the GPU path");

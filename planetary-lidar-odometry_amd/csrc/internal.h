@@ -46,6 +46,7 @@ struct KParams {
     int solve_method;
     double ls_threshold;
     double delta_dist, delta_angle;
+    int matcher;              // imls_match_method: 0 IMLS, 1 plane_ICP (NN-1 tangent-plane projection)
     int seed_half;            // seed pass scans the nearest leaf ± seed_half Morton neighbours
     float reseed;             // temporal seed unless displacement² > reseed · previous worst key
     int sparse_lanes;         // a leaf wanted by ≤ this many lanes is scanned per lane, not per point

@@ -190,6 +190,29 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
     return -1;
 }
 
+// plane_ICP_proj's loop body after the NN-1 search (laser_odometry.cpp:352-396): unfound → "no
+// normal" (the bounds check; no h gate — min_dist is unused), map normal finite, angle gate,
+// y = x − ((x−p)·n)·n in double, stored as float.
+__device__ int finish_plane(const float xf[3], const double ns[3], int p1, const TreeView& t, const KParams& kp,
+                            float yf[3], float nf[3]) {
+    if (p1 < 0) return IMLS_REJ_NO_NORMAL;
+    const float4 n4 = t.mnr[p1];
+    const double nn[3] = {n4.x, n4.y, n4.z};
+    if (!(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) return IMLS_REJ_INVALID_NORMAL;
+    if (kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg)) return IMLS_REJ_NORMAL_CONSTRAINT;
+    const float4 q = t.mpt[p1];
+    const double xd[3] = {xf[0], xf[1], xf[2]};
+    const double v0 = xd[0] - (double)q.x, v1 = xd[1] - (double)q.y, v2 = xd[2] - (double)q.z;
+    double pd = v0 * nn[0];
+    pd = pd + v1 * nn[1];
+    pd = pd + v2 * nn[2];
+    yf[0] = (float)(xd[0] - pd * nn[0]);
+    yf[1] = (float)(xd[1] - pd * nn[1]);
+    yf[2] = (float)(xd[2] - pd * nn[2]);
+    nf[0] = (float)nn[0]; nf[1] = (float)nn[1]; nf[2] = (float)nn[2];
+    return -1;
+}
+
 // Row of the point-to-plane system for a valid correspondence (solver.cpp:95-103).
 __device__ __forceinline__ void plane_row(const float xf[3], const float yf[3], const float nf[3], double a[6], double& b) {
     const double s0 = xf[0], s1 = xf[1], s2 = xf[2];
@@ -612,7 +635,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_finish(TreeView t, const float4*
             fb_list[pos] = (unsigned)i;
             cat = -3;                                         // deferred to k_project_lane
         } else {
-            cat = finish_query<KL>(xf, ns, ed, ep, 0, min(K, cnt_r), d1, p1, t, kp, yf, nf, kq);
+            cat = kp.matcher ? finish_plane(xf, ns, p1, t, kp, yf, nf)
+                             : finish_query<KL>(xf, ns, ed, ep, 0, min(K, cnt_r), d1, p1, t, kp, yf, nf, kq);
             store_result(i, cat, xf, yf, nf, cs, cd, cn);
         }
     }
@@ -740,7 +764,9 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(TreeView t, const f
             int lpos[KCAP];
 #pragma unroll
             for (int j = 0; j < KCAP; ++j) lpos[j] = (li[j] >= 0 && li[j] != 0x7fffffff) ? (int)t.ipos[li[j]] : 0;
-            cat = finish_query<KCAP>(xf, ns, ld, lpos, KCAP - K, cnt, d1, nn_found ? (int)t.ipos[i1] : -1, t, kp, yf, nf, kq);
+            const int p1 = nn_found ? (int)t.ipos[i1] : -1;
+            cat = kp.matcher ? finish_plane(xf, ns, p1, t, kp, yf, nf)
+                             : finish_query<KCAP>(xf, ns, ld, lpos, KCAP - K, cnt, d1, p1, t, kp, yf, nf, kq);
             store_result(i, cat, xf, yf, nf, cs, cd, cn);
         }
         if (cat >= 0) atomicAdd(&rej_s[cat], 1u);

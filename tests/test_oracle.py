@@ -269,3 +269,43 @@ def test_weighted_ls_matches_numpy():
     w = np.random.default_rng(2).uniform(0.1, 1.0, len(s))
     ok, D = oc.solve(_abi.IMLS_SOLVE_WEIGHTED_LS, s, d, n, gparams(), weights=w)
     assert ok and np.abs(D - imls_np.solve_wls(s, d, n, w)).max() < 1e-9
+
+
+def picp_dict(p):
+    return dict(picp_r=p.picp_r, picp_normal_angle_constraint=p.picp_normal_angle_constraint,
+                picp_angle_diff_threshold=p.picp_angle_diff_threshold)
+
+
+@pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair"])
+@pytest.mark.parametrize("angle", [0, 1])
+def test_plane_icp_restatements_agree(name, angle):
+    """plane_ICP_proj (laser_odometry.cpp:277-413): C++ oracle vs numpy restatement, bit-exact."""
+    g = golden(name)
+    p = gparams()
+    p.matching_method = _abi.IMLS_MATCH_PLANE_ICP
+    p.picp_normal_angle_constraint = angle
+    for k in (0, 1):
+        x, y, n, idx, rej = oc.project(g["src"], g["tgt"], g[f"pose{k}"], p)
+        x2, y2, n2, idx2, rej2 = imls_np.project_plane_icp(g["src"], g["tgt"], g[f"pose{k}"], picp_dict(p))
+        assert np.array_equal(rej, rej2) and np.array_equal(idx, idx2)
+        assert np.array_equal(x, x2) and np.array_equal(y, y2) and np.array_equal(n, n2)
+        assert rej[4] == 0 and rej[5] == 0 and len(idx) > 0.5 * g["src"].shape[1]
+
+
+def test_plane_icp_kat():
+    """Analytic: a query above a z=0 plane projects straight down onto it; beyond picp.r it is
+    "no normal" (the reference's bounds check, not "too far"); the h gate does not apply."""
+    rng = np.random.default_rng(5)
+    m = 4000
+    tgt = np.zeros((6, m), np.float32)
+    tgt[0] = rng.uniform(-5, 5, m); tgt[1] = rng.uniform(-5, 5, m); tgt[5] = 1.0
+    src = np.zeros((6, 3), np.float32)
+    src[:3, 0] = (0.3, -0.2, 1.2)     # within picp.r = 1.5 of the plane but beyond h = 1: accepted
+    src[:3, 1] = (0.1, 0.4, 0.25)
+    src[:3, 2] = (0.0, 0.0, 3.0)      # nothing within 1.5 → no normal
+    src[5] = 1.0
+    p = gparams()
+    p.matching_method = _abi.IMLS_MATCH_PLANE_ICP
+    x, y, n, idx, rej = oc.project(src, tgt, np.eye(4), p)
+    assert list(idx) == [0, 1] and rej[0] == 1 and rej.sum() == 1
+    assert np.allclose(y[:, 2], 0.0, atol=1e-7) and np.allclose(y[:, :2], x[:, :2], atol=1e-7)
