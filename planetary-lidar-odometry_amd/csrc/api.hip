@@ -89,7 +89,15 @@ KParams make_kparams(const imls_params& p) {
     k.delta_dist = p.delta_dist_threshold;
     k.delta_angle = p.delta_angle_threshold;
     k.matcher = p.matching_method;
+    // projected-distance gates: IMLS ‖p−x‖ < r_proj, proj < r (imls_icp.cpp:576); plane_ICP keeps the
+    // reference's swapped gate ‖p−x‖ < r·r, proj < r_proj (laser_odometry.cpp:322)
+    k.proj = p.use_projected_distance ? 1 : 0;
+    k.gate_dist = p.r_proj;
+    k.gate_proj = p.r;
     if (p.matching_method == IMLS_MATCH_PLANE_ICP) {
+        k.proj = p.picp_use_projected_distance ? 1 : 0;
+        k.gate_dist = p.picp_r * p.picp_r;
+        k.gate_proj = p.picp_r_proj;
         // plane_ICP_proj (laser_odometry.cpp:295-299, 346-350): NN-1 within its own r and angle gate
         k.r2 = p.picp_r * p.picp_r;
         k.K = 1;
@@ -113,10 +121,7 @@ int check_params(imls_ctx* c, const imls_params* p) {
     if (p->search_number < 1 || p->search_number > 32) return fail(c, IMLS_ERR_UNSUPPORTED, "search_number must be in [1, 32]");
     if (p->matching_method != IMLS_MATCH_IMLS && p->matching_method != IMLS_MATCH_PLANE_ICP)
         return fail(c, IMLS_ERR_ARG, "matching_method must be IMLS or plane_ICP");
-    if (p->matching_method == IMLS_MATCH_PLANE_ICP && p->picp_use_projected_distance)
-        return fail(c, IMLS_ERR_UNSUPPORTED, "plane_ICP use_projected_distance is not built on the GPU path yet");
     if (p->use_tensor_voting && !p->get_normals) return fail(c, IMLS_ERR_UNSUPPORTED, "tensor voting normals are not on the GPU path");
-    if (p->use_projected_distance) return fail(c, IMLS_ERR_UNSUPPORTED, "use_projected_distance is not built on the GPU path yet");
     if (!p->get_normals && p->recompute_normal_count_mode) return fail(c, IMLS_ERR_UNSUPPORTED, "recompute-normal count mode is not on the GPU path");
     if (p->solve_method != IMLS_SOLVE_LS && p->solve_method != IMLS_SOLVE_WEIGHTED_LS && p->solve_method != IMLS_SOLVE_RANSAC)
         return fail(c, IMLS_ERR_UNSUPPORTED, "solve_method must be LS, Weighted LS or RANSAC (Ceres/ICP/Teaser stay on the CPU path)");

@@ -47,6 +47,8 @@ struct KParams {
     double ls_threshold;
     double delta_dist, delta_angle;
     int matcher;              // imls_match_method: 0 IMLS, 1 plane_ICP (NN-1 tangent-plane projection)
+    int proj;                 // projected-distance candidate rule (brute force in the reference)
+    double gate_dist, gate_proj;   // proj mode: ‖p−x‖ < gate_dist and ‖(p−x)×n_s‖ < gate_proj
     int seed_half;            // seed pass scans the nearest leaf ± seed_half Morton neighbours
     float reseed;             // temporal seed unless displacement² > reseed · previous worst key
     int sparse_lanes;         // a leaf wanted by ≤ this many lanes is scanned per lane, not per point

@@ -191,11 +191,12 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
 }
 
 // plane_ICP_proj's loop body after the NN-1 search (laser_odometry.cpp:352-396): unfound → "no
-// normal" (the bounds check; no h gate — min_dist is unused), map normal finite, angle gate,
+// normal" (the bounds check; no h gate — min_dist is unused) or, in projected-distance mode, an
+// empty candidate list → "too far" (336-340); map normal finite, angle gate,
 // y = x − ((x−p)·n)·n in double, stored as float.
 __device__ int finish_plane(const float xf[3], const double ns[3], int p1, const TreeView& t, const KParams& kp,
                             float yf[3], float nf[3]) {
-    if (p1 < 0) return IMLS_REJ_NO_NORMAL;
+    if (p1 < 0) return kp.proj ? IMLS_REJ_TOO_FAR : IMLS_REJ_NO_NORMAL;   // empty candidate list: 336-340
     const float4 n4 = t.mnr[p1];
     const double nn[3] = {n4.x, n4.y, n4.z};
     if (!(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) return IMLS_REJ_INVALID_NORMAL;
@@ -701,7 +702,11 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(TreeView t, const f
             }
             double d1 = kInfD;
             int i1 = 0x7fffffff;
-            const double r2 = kp.r2;
+            // projected-distance mode (imls_icp.cpp:338-369, 563-596; laser_odometry.cpp:316-341):
+            // candidates are the points with ‖p−x‖ < gate_dist and ‖(p−x)×n_s‖ < gate_proj, ranked by
+            // the projected distance — the tree only bounds the ‖p−x‖ ball, the list key is proj
+            const bool proj = kp.proj != 0;
+            const double r2 = proj ? kp.gate_dist * kp.gate_dist : kp.r2;
             float bf = (float)r2 * kBoxSlack + 1e-30f;
             int node = 1, sp = 0;
             const int P = t.P, B = t.B, M = t.M;
@@ -728,9 +733,29 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(TreeView t, const f
                         const float ex = q4.x - xf[0], ey = q4.y - xf[1], ez = q4.z - xf[2];
                         const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
                         if (d32 > bf) continue;
+                        const int oi = (int)__float_as_uint(q4.w);
+                        if (proj) {
+                            const double dx = (double)q4.x - xd[0], dy = (double)q4.y - xd[1], dz = (double)q4.z - xd[2];
+                            const double cx = dy * ns[2] - dz * ns[1], cy = dz * ns[0] - dx * ns[2], cz = dx * ns[1] - dy * ns[0];
+                            const double pr = sqrt((cx * cx + cy * cy) + cz * cz);
+                            const double dn = sqrt((dx * dx + dy * dy) + dz * dz);
+                            if (!(dn < kp.gate_dist && pr < kp.gate_proj)) continue;
+                            if (lessp(pr, oi, ld[KCAP - 1], li[KCAP - 1])) {
+                                bool prev = true;
+#pragma unroll
+                                for (int j = KCAP - 1; j >= 0; --j) {
+                                    const bool sh = (j > 0) ? lessp(pr, oi, ld[(j > 0) ? j - 1 : 0], li[(j > 0) ? j - 1 : 0]) : false;
+                                    const double nd = sh ? ld[(j > 0) ? j - 1 : 0] : (prev ? pr : ld[j]);
+                                    const int ni = sh ? li[(j > 0) ? j - 1 : 0] : (prev ? oi : li[j]);
+                                    ld[j] = nd;
+                                    li[j] = ni;
+                                    prev = sh;
+                                }
+                            }
+                            continue;   // fixed bound: every point of the ball is a candidate
+                        }
                         const double d2 = exact_d2(xd, q4.x, q4.y, q4.z);
                         if (!(d2 <= r2)) continue;
-                        const int oi = (int)__float_as_uint(q4.w);
                         bool changed = false;
                         if (d2 > DBL_EPSILON && lessp(d2, oi, d1, i1)) { d1 = d2; i1 = oi; changed = true; }
                         if (lessp(d2, oi, ld[KCAP - 1], li[KCAP - 1])) {
@@ -760,6 +785,14 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(TreeView t, const f
             int cnt = 0;
 #pragma unroll
             for (int j = 0; j < KCAP; ++j) cnt += (j >= KCAP - K && ld[j] < kInfD) ? 1 : 0;
+            if (proj) {
+                // NN = the minimum projected distance (min_dist = proj², imls_icp.cpp:585-588); the
+                // IMLS list holds proj² as its distances (361-365) — same candidates, same order
+                i1 = li[KCAP - K];
+                d1 = ld[KCAP - K] * ld[KCAP - K];
+#pragma unroll
+                for (int j = 0; j < KCAP; ++j) ld[j] = (j >= KCAP - K && ld[j] < kInfD) ? ld[j] * ld[j] : ld[j];
+            }
             nn_found = i1 != 0x7fffffff;
             int lpos[KCAP];
 #pragma unroll
@@ -820,7 +853,7 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
     const int wblocks = (N + kWaveBlock - 1) / kWaveBlock;
     double* p_fb = partial1 + (size_t)wblocks * kNormEq;
     const int K = kp.K;
-    if (lane_mode) {
+    if (lane_mode || kp.proj) {
         // reference mode: every query through the exact per-lane kernel (grid-stride over the
         // fallback slabs); the wave slabs are zeroed
         (void)hipMemsetAsync(partial1, 0, (size_t)wblocks * kNormEq * sizeof(double), s);

@@ -69,10 +69,3 @@ def test_plane_icp_register_frame(ctx, name, solver):
     assert np.abs(r["pose"] - want["pose"]).max() < POSE_TOL
     for t, u in zip(r["trace"], want["trace"]):
         assert t.n_valid == u.n_valid and list(t.reject) == list(u.reject)
-
-
-def test_plane_icp_projected_distance_unsupported(ctx):
-    p = picp_params()
-    p.picp_use_projected_distance = 1
-    with pytest.raises(_abi.ImlsError):
-        ctx.set_params(p)
