@@ -31,6 +31,10 @@ struct imls_ctx {
     DevBuf spt, snr, sscratch, qperm, upload_s;
     DevBuf fb;                            // fallback query list + count
     DevBuf lkeys;                         // leaf first Morton keys + quantisation (seed search)
+    DevBuf rnr;                           // recomputed map normals (count mode), Morton order
+    bool rnr_valid = false;
+    int rnr_k = -1;
+    double rnr_r = -1.0;
     DevBuf prevnn;                        // per-query neighbour lists carried between ICP iterations
     int lane_mode = 0;
     int temporal_seed = 1;
@@ -88,6 +92,9 @@ KParams make_kparams(const imls_params& p) {
     k.ls_threshold = p.ls_threshold;
     k.delta_dist = p.delta_dist_threshold;
     k.delta_angle = p.delta_angle_threshold;
+    // get_normals=false in count mode reads normals recomputed from the map (normals.hip); in the
+    // reference's own (dead, Q1) mode every candidate normal is ∞
+    if (!p.get_normals && p.recompute_normal_count_mode) k.get_normals = 1;
     k.matcher = p.matching_method;
     // projected-distance gates: IMLS ‖p−x‖ < r_proj, proj < r (imls_icp.cpp:576); plane_ICP keeps the
     // reference's swapped gate ‖p−x‖ < r·r, proj < r_proj (laser_odometry.cpp:322)
@@ -122,7 +129,8 @@ int check_params(imls_ctx* c, const imls_params* p) {
     if (p->matching_method != IMLS_MATCH_IMLS && p->matching_method != IMLS_MATCH_PLANE_ICP)
         return fail(c, IMLS_ERR_ARG, "matching_method must be IMLS or plane_ICP");
     if (p->use_tensor_voting && !p->get_normals) return fail(c, IMLS_ERR_UNSUPPORTED, "tensor voting normals are not on the GPU path");
-    if (!p->get_normals && p->recompute_normal_count_mode) return fail(c, IMLS_ERR_UNSUPPORTED, "recompute-normal count mode is not on the GPU path");
+    if (!p->get_normals && p->recompute_normal_count_mode && (p->search_number_normal < 1 || p->search_number_normal > 32))
+        return fail(c, IMLS_ERR_UNSUPPORTED, "search_number_normal must be in [1, 32]");
     if (p->solve_method != IMLS_SOLVE_LS && p->solve_method != IMLS_SOLVE_WEIGHTED_LS && p->solve_method != IMLS_SOLVE_RANSAC)
         return fail(c, IMLS_ERR_UNSUPPORTED, "solve_method must be LS, Weighted LS or RANSAC (Ceres/ICP/Teaser stay on the CPU path)");
     if (p->solve_method == IMLS_SOLVE_RANSAC) {
@@ -202,6 +210,22 @@ int prepare_ransac(imls_ctx* c, int rows) {
     return IMLS_OK;
 }
 
+TreeView tree_view(imls_ctx* c);
+
+// count mode: (re)compute the map normals once per (map, search_number_normal, r_normal)
+int ensure_map_normals(imls_ctx* c) {
+    if (c->P.get_normals || !c->P.recompute_normal_count_mode) return IMLS_OK;
+    if (c->rnr_valid && c->rnr_k == c->P.search_number_normal && c->rnr_r == c->P.r_normal) return IMLS_OK;
+    if (!grow(c->rnr, (size_t)std::max(c->M, 1) * 16)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (normals)");
+    TreeView t = tree_view(c);
+    if (launch_map_normals(c->stream, t, c->P.search_number_normal, c->P.r_normal, (float4*)c->rnr.p))
+        return fail(c, IMLS_ERR_DEVICE, "map normal launch failed");
+    c->rnr_valid = true;
+    c->rnr_k = c->P.search_number_normal;
+    c->rnr_r = c->P.r_normal;
+    return IMLS_OK;
+}
+
 SolveLaunch solve_launch(imls_ctx* c, imls_iter_trace* tr, int update_pose) {
     SolveLaunch L{};
     L.N = c->N;
@@ -236,6 +260,7 @@ TreeView tree_view(imls_ctx* c) {
     TreeView t;
     t.mpt = (const float4*)c->mpt.p;
     t.mnr = t.mpt ? t.mpt + c->M : nullptr;
+    if (!c->P.get_normals && c->P.recompute_normal_count_mode && c->rnr.p) t.mnr = (const float4*)c->rnr.p;
     t.ipos = t.mpt ? (const unsigned*)(t.mpt + 2 * (size_t)c->M) : nullptr;
     t.nodes = (const float4*)c->nodes.p;
     t.tpt = (const float4*)c->tpt.p;
@@ -326,6 +351,7 @@ int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
     timed_end(c, 1, slot);
     if (rc) return rc;
     c->has_target = c->M > 0;
+    c->rnr_valid = false;
     c->has_corr = false;
     if (n_kept) *n_kept = (size_t)c->M;
     return IMLS_OK;
@@ -433,7 +459,7 @@ void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
+    DevBuf* bufs[] = {&c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
                       &c->upload_t, &c->spt, &c->snr, &c->sscratch,
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
@@ -500,6 +526,7 @@ int imls_project(imls_ctx* c, const double pose[16], float* x_out, float* y_out,
     if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
     if (int rc = check_device(c)) return rc;
     if (int rc = ensure_solve(c, c->N)) return rc;
+    if (int rc = ensure_map_normals(c)) return rc;
     if (!grow(c->pose_tmp, 32 * 8) || !grow(c->stats, 128)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");
     double* dpose = (double*)c->pose_tmp.p;
     int* dzero = (int*)(dpose + 16);
@@ -619,6 +646,7 @@ int imls_register_frame_async(imls_ctx* c) {
     hipMemsetAsync(c->trace_mem.p, 0, (size_t)std::max(iters, 1) * sizeof(imls_iter_trace), c->stream);
     hipMemsetAsync(c->stats.p, 0, 128, c->stream);
     imls_iter_trace* tr = (imls_iter_trace*)c->trace_mem.p;
+    if (int rc = ensure_map_normals(c)) return rc;
     const TreeView tv = tree_view(c);
     if (int rc = prepare_ransac(c, c->N)) return rc;
     for (int it = 0; it < iters; ++it) {

@@ -139,6 +139,9 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
                         const int* count = nullptr, const double* wsum = nullptr);
 int solve_blocks(int N);
 
+// normals.hip — map normals recomputed from the map (get_normals=false, count mode), Morton order
+int launch_map_normals(hipStream_t s, const TreeView& t, int K, double r_normal, float4* out);
+
 // ransac.hip — RANSAC (+ final LS / weighted LS / DRPM) and the solve-method dispatcher
 constexpr int kHypMax = 4096;          // hypotheses per chunk (chunks grow 16, 64, 256, 1024, 4096)
 struct RansacParams {

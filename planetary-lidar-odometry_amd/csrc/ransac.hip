@@ -517,81 +517,6 @@ struct DrpmDev {
     double* slabs;    // [blocks × kDrpmSlab]
 };
 
-// Cyclic Jacobi on a symmetric 6×6 (ascending eigenvalues); identical sweep order to the oracle.
-__device__ void sym_eig6(const double Hin[36], double ev[6], double U[36]) {
-    double a[6][6], v[6][6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = 0; c < 6; ++c) { a[r][c] = Hin[r * 6 + c]; v[r][c] = r == c ? 1.0 : 0.0; }
-    for (int sweep = 0; sweep < 100; ++sweep) {
-        double off = 0;
-#pragma unroll
-        for (int p = 0; p < 6; ++p)
-#pragma unroll
-            for (int q = p + 1; q < 6; ++q) off += a[p][q] * a[p][q];
-        if (off < 1e-300) break;
-#pragma unroll
-        for (int p = 0; p < 6; ++p)
-#pragma unroll
-            for (int q = p + 1; q < 6; ++q) {
-                const double apq = a[p][q];
-                if (apq != 0) {
-                    const double app = a[p][p], aqq = a[q][q];
-                    const double theta = (aqq - app) / (2 * apq);
-                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
-                    const double c = 1 / sqrt(t * t + 1), s = t * c;
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) {
-                        const double akp = a[k][p], akq = a[k][q];
-                        a[k][p] = c * akp - s * akq;
-                        a[k][q] = s * akp + c * akq;
-                    }
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) {
-                        const double apk = a[p][k], aqk = a[q][k];
-                        a[p][k] = c * apk - s * aqk;
-                        a[q][k] = s * apk + c * aqk;
-                    }
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) {
-                        const double vkp = v[k][p], vkq = v[k][q];
-                        v[k][p] = c * vkp - s * vkq;
-                        v[k][q] = s * vkp + c * vkq;
-                    }
-                }
-            }
-    }
-    // ascending order, ties keep index order (std::sort on distinct diagonal values)
-    int ord[6];
-    double dg[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { ord[k] = k; dg[k] = a[k][k]; }
-#pragma unroll
-    for (int i = 1; i < 6; ++i)
-#pragma unroll
-        for (int j = i; j > 0; --j) {
-            const bool sw = dg[j] < dg[j - 1];
-            const double td = dg[j];
-            const int to = ord[j];
-            dg[j] = sw ? dg[j - 1] : dg[j];
-            ord[j] = sw ? ord[j - 1] : ord[j];
-            dg[j - 1] = sw ? td : dg[j - 1];
-            ord[j - 1] = sw ? to : ord[j - 1];
-        }
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-        ev[c] = dg[c];
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-            double val = 0;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) val = ord[c] == k ? v[r][k] : val;
-            U[c * 6 + r] = val;
-        }
-    }
-}
-
 // reduce the weighted normal equations (pass-1 slabs), eigendecompose H
 __global__ __launch_bounds__(256) void k_drpm_eig(const double* __restrict__ partial, int blocks, SolveState st, DrpmDev Dv) {
     if (*st.done) return;
@@ -612,7 +537,7 @@ __global__ __launch_bounds__(256) void k_drpm_eig(const double* __restrict__ par
     for (int q = 0; q < 36; ++q) Dv.H[q] = H[q];
     for (int r = 0; r < 6; ++r) Dv.g[r] = acc[21 + r];
     double ev[6], U[36];
-    sym_eig6(H, ev, U);
+    sym_eig<6>(H, ev, U);
     for (int q = 0; q < 36; ++q) Dv.U[q] = U[q];
     for (int r = 0; r < 6; ++r) Dv.ev[r] = ev[r];
 }

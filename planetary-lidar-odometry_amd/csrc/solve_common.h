@@ -107,7 +107,7 @@ __device__ void block_sum28(const double (&v)[kNormEq], double* red, double* out
 
 // Column-pivoted Cholesky solve of the 6×6 normal equations (see file header).  Unknowns past the
 // numerical rank are set to zero (Eigen's basic solution).  Returns the rank.
-__device__ int solve6(const double* ne, double x[6]) {
+__device__ inline int solve6(const double* ne, double x[6]) {
     // every index below is a compile-time constant (full unroll; the pivot swap is a predicated
     // swap over the candidate rows), so the system stays in registers — no scratch traffic
     double A[6][6], g[6];
@@ -197,7 +197,7 @@ __device__ int solve6(const double* ne, double x[6]) {
 
 // Δ from x (solver.cpp:140-163): R = AngleAxis(‖ω‖, ω̂) (Eigen AngleAxis::toRotationMatrix), then
 // the JacobiSVD U·Vᵀ re-orthonormalisation as the polar factor (Newton iteration).
-__device__ void delta_from_x(const double x[6], double D[16]) {
+__device__ inline void delta_from_x(const double x[6], double D[16]) {
     const double wx = x[0], wy = x[1], wz = x[2];
     double sq = wx * wx;
     sq = sq + wy * wy;
@@ -231,7 +231,7 @@ __device__ void delta_from_x(const double x[6], double D[16]) {
 }
 
 // rPose = Δ·rPose, trace, convergence (laser_odometry.cpp:619-646); single thread.
-__device__ void finish_iteration(SolveState st, imls_iter_trace* tr, const double D[16], double nvalid, double nkept,
+__device__ inline void finish_iteration(SolveState st, imls_iter_trace* tr, const double D[16], double nvalid, double nkept,
                                  int update_pose, const KParams& kp) {
     for (int k = 0; k < 16; ++k) st.delta[k] = D[k];
     if (tr) {
@@ -262,6 +262,83 @@ __device__ void finish_iteration(SolveState st, imls_iter_trace* tr, const doubl
     }
 }
 
+
+// Cyclic Jacobi on a symmetric N×N (ascending eigenvalues, eigenvectors as columns:
+// U[c·N + r]); identical sweep order to the oracle's sym_eig (Eigen SelfAdjointEigenSolver order).
+template <int N>
+__device__ void sym_eig(const double* Hin, double* ev, double* U) {
+    double a[N][N], v[N][N];
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+#pragma unroll
+        for (int c = 0; c < N; ++c) { a[r][c] = Hin[r * N + c]; v[r][c] = r == c ? 1.0 : 0.0; }
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0;
+#pragma unroll
+        for (int p = 0; p < N; ++p)
+#pragma unroll
+            for (int q = p + 1; q < N; ++q) off += a[p][q] * a[p][q];
+        if (off < 1e-300) break;
+#pragma unroll
+        for (int p = 0; p < N; ++p)
+#pragma unroll
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = a[p][q];
+                if (apq != 0) {
+                    const double app = a[p][p], aqq = a[q][q];
+                    const double theta = (aqq - app) / (2 * apq);
+                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
+                    const double c = 1 / sqrt(t * t + 1), s = t * c;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        const double akp = a[k][p], akq = a[k][q];
+                        a[k][p] = c * akp - s * akq;
+                        a[k][q] = s * akp + c * akq;
+                    }
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        const double apk = a[p][k], aqk = a[q][k];
+                        a[p][k] = c * apk - s * aqk;
+                        a[q][k] = s * apk + c * aqk;
+                    }
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        const double vkp = v[k][p], vkq = v[k][q];
+                        v[k][p] = c * vkp - s * vkq;
+                        v[k][q] = s * vkp + c * vkq;
+                    }
+                }
+            }
+    }
+    // ascending order, ties keep index order (std::sort on distinct diagonal values)
+    int ord[N];
+    double dg[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) { ord[k] = k; dg[k] = a[k][k]; }
+#pragma unroll
+    for (int i = 1; i < N; ++i)
+#pragma unroll
+        for (int j = i; j > 0; --j) {
+            const bool sw = dg[j] < dg[j - 1];
+            const double td = dg[j];
+            const int to = ord[j];
+            dg[j] = sw ? dg[j - 1] : dg[j];
+            ord[j] = sw ? ord[j - 1] : ord[j];
+            dg[j - 1] = sw ? td : dg[j - 1];
+            ord[j - 1] = sw ? to : ord[j - 1];
+        }
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+        ev[c] = dg[c];
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+            double val = 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) val = ord[c] == k ? v[r][k] : val;
+            U[c * N + r] = val;
+        }
+    }
+}
 
 }  // namespace
 }  // namespace imlsgpu
