@@ -105,6 +105,26 @@ public:
         pts.assign(kept.begin(), kept.end());
     }
 
+    // plane_ICP_proj (laser_odometry.cpp:277-413): the same contract as ProjSourcePtToSurface
+    // (in_cloud erased in order, out_cloud = y + NN-1 normal) with the plane_ICP parameters of
+    // config.json (matching_method.plane_ICP: r, use_projected_distance {enabled, r_proj},
+    // normal_angle_constraint {enabled, angle_diff_threshold}).  The reference's uninitialised
+    // tree pointer (522) and by-value pointer (279) are not reproduced: the context owns the index.
+    template <class CloudPtr>
+    void planeICPProj(CloudPtr& in_cloud, CloudPtr& ref_cloud, double r, bool use_projected_distance, double r_proj,
+                      bool normal_angle_constraint, double angle_diff_threshold, const double* pose = nullptr) {
+        imls_params p = params_;
+        p.matching_method = IMLS_MATCH_PLANE_ICP;
+        p.picp_r = r;
+        p.picp_use_projected_distance = use_projected_distance;
+        p.picp_r_proj = r_proj;
+        p.picp_normal_angle_constraint = normal_angle_constraint;
+        p.picp_angle_diff_threshold = angle_diff_threshold;
+        check(imls_set_params(ctx_, &p));
+        ProjSourcePtToSurface(in_cloud, ref_cloud, std::string(), 0, pose);
+        check(imls_set_params(ctx_, &params_));
+    }
+
     // Fused laser_odometry.cpp:524-647 for the clouds already set; pose_out = rPose.
     int registerFrame(double pose_out[16], int* iters_run = nullptr, int* status = nullptr) {
         return imls_register_frame(ctx_, pose_out, iters_run, status, nullptr);
@@ -177,6 +197,44 @@ bool SolveMotionEstimationProblemWeightedLS(IMLSICPMatcherHip& m, const Vec3List
     int ok = 0;
     if (imls_solve_correspondences(m.context(), IMLS_SOLVE_WEIGHTED_LS, s.data(), d.data(), n.data(), w.data(),
                                    source_cloud.size(), D, &ok) != IMLS_OK) return false;
+    detail::to_matrix(D, deltaTrans);
+    return ok != 0;
+}
+
+// solver.cpp:222-385 (+ 486-603 for the DRPM final): same arguments; final_solve_method is
+// config.json's string ("LS", "Weighted LS", "DRPM").  rand() is replayed on the device from
+// the context's ransac_seed (glibc's default 1 unless set), re-seeded per call.
+template <class Vec3List, class Mat4>
+bool SolveMotionEstimationProblemRANSAC(IMLSICPMatcherHip& m, const Vec3List& source_cloud, const Vec3List& ref_cloud,
+                                        const Vec3List& ref_normals, Mat4& deltaTrans, const std::string& /*timestamp*/,
+                                        const int max_iterations, const double distance_threshold,
+                                        const double min_inliers_percentage, const double huber_threshold,
+                                        const std::string& final_solve_method, const double ls_threshold,
+                                        const double drpm_threshold, const double drpm_stdev_points,
+                                        const double drpm_stdev_normals) {
+    imls_params p = m.params();
+    p.solve_method = IMLS_SOLVE_RANSAC;
+    p.ransac_max_iterations = max_iterations;
+    p.ransac_distance_threshold = distance_threshold;
+    p.ransac_min_inliers_percentage = min_inliers_percentage;
+    p.ransac_huber_threshold = huber_threshold;
+    if (final_solve_method == "LS") p.ransac_final_method = IMLS_FINAL_LS;
+    else if (final_solve_method == "Weighted LS") p.ransac_final_method = IMLS_FINAL_WEIGHTED_LS;
+    else if (final_solve_method == "DRPM") p.ransac_final_method = IMLS_FINAL_DRPM;
+    else return false;   // solver.cpp:380-384: unknown final method → false
+    p.ransac_ls_threshold = ls_threshold;
+    p.drpm_threshold = drpm_threshold;
+    p.drpm_stdev_points = drpm_stdev_points;
+    p.drpm_stdev_normals = drpm_stdev_normals;
+    if (imls_set_params(m.context(), &p) != IMLS_OK) return false;
+    std::vector<double> s, d, n;
+    detail::flatten(source_cloud, s); detail::flatten(ref_cloud, d); detail::flatten(ref_normals, n);
+    double D[16];
+    int ok = 0;
+    const int rc = imls_solve_correspondences(m.context(), IMLS_SOLVE_RANSAC, s.data(), d.data(), n.data(), nullptr,
+                                              source_cloud.size(), D, &ok);
+    imls_set_params(m.context(), &m.params());
+    if (rc != IMLS_OK) return false;
     detail::to_matrix(D, deltaTrans);
     return ok != 0;
 }

@@ -75,6 +75,9 @@ int main() {{
   m.ProjSourcePtToSurface(a, b, std::string("0"), 0, nullptr);
   std::vector<std::array<double,3>> s, d, n; double D[16];
   bool ok = imls_hip::SolveMotionEstimationProblemLS(m, s, d, n, D, "0", 0.02);
+  m.planeICPProj(a, b, 1.5, false, 0.8, true, 30.0);
+  ok = ok && imls_hip::SolveMotionEstimationProblemRANSAC(m, s, d, n, D, "0", 5000, 0.8, 0.95, 0.648, "DRPM",
+                                                        0.02, 0.05, 0.02, 0.05);
   (void)ok; (void)p; return 0; }}
 ''')
     subprocess.run(["g++", "-std=c++17", "-fsyntax-only", str(src)], check=True)
