@@ -116,6 +116,8 @@ KParams make_kparams(const imls_params& p) {
     k.sparse_lanes = 32;
     k.sparse_lanes_seed = 4;
     if (const char* w = std::getenv("IMLS_SPARSE")) k.sparse_lanes = std::atoi(w);
+    k.qwave = -1;   // auto
+    if (const char* w = std::getenv("IMLS_QWAVE")) k.qwave = std::atoi(w);
     if (const char* w = std::getenv("IMLS_SPARSE_SEED")) k.sparse_lanes_seed = std::atoi(w);
     if (const char* w = std::getenv("IMLS_SEED_HALF")) k.seed_half = std::atoi(w);
     if (const char* w = std::getenv("IMLS_RESEED")) k.reseed = (float)std::atof(w);

@@ -53,6 +53,7 @@ struct KParams {
     float reseed;             // temporal seed unless displacement² > reseed · previous worst key
     int sparse_lanes;         // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
     int sparse_lanes_seed;    // the same for waves holding freshly seeded lanes
+    int qwave;                // traversal: 0 = packets of 64 queries per wave, 1 = one wave per query
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
 };
 

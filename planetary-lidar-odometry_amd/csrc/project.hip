@@ -40,6 +40,7 @@ constexpr double kInfD = __builtin_huge_val();
 constexpr float kInfF = __builtin_huge_valf();
 constexpr int kWaveBlock = 256;
 constexpr int kFallbackBlocks = 64;
+constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query up to this many queries
 constexpr int kSeedChunk = 8;        // seed-pass points loaded per batch
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
 constexpr double kCertSlack = 1.0 + 4e-7;
@@ -372,9 +373,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
     }
     unsigned n_inner = 0, n_leaf = 0;
 #ifdef IMLS_DEBUG_WAVE_TRACE
-    unsigned dbg_ev = 0, dbg_ins = 0, dbg_lane_ins = 0, dbg_useful = 0, dbg_wants = 0;
+    unsigned dbg_ev = 0, dbg_ins = 0;
     unsigned dbg_sparse = 0, dbg_bcast = 0, dbg_sparse_lanes = 0, dbg_sparse_ins = 0;
-    const float dbg_seed_bnd = lk[KL - 1];
     const long long dbg_t1 = wall_clock64();
 #endif
     // waves with freshly seeded lanes insert a lot: per-lane leaf scans would serialise that
@@ -475,14 +475,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                         insert_top<KL>(lk, lp, d32, base + j);
                         bnd = fminf(r2s, lk[KL - 1]);
                     }
-#ifdef IMLS_DEBUG_WAVE_TRACE
-                    dbg_lane_ins += ins ? 1 : 0;
-#endif
                 }
-#ifdef IMLS_DEBUG_WAVE_TRACE
-                dbg_wants += (em >> lane) & 1ull;
-                dbg_useful += 0;
-#endif
             }
         }
         // pop: the stacked node's box is in LDS — re-check it against the shrunken lane bounds
@@ -536,6 +529,165 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
         }
     }
 #endif
+    if (nbr_stats && lane == 0) {
+        atomicAdd(&nbr_stats[2], (unsigned long long)n_leaf);
+        atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
+        atomicAdd(&nbr_stats[4], 1ull);
+    }
+}
+
+// =============================================================================================
+// One wave per query (sparse query sets, e.g. FPS-sampled scans of the config-C stream): no packet
+// union — each query walks only its own neighbourhood — and the top-KL list is spread over the
+// lanes (lane k holds entry k, sorted), so every step is wave-uniform: inner nodes are scalar
+// loads, a leaf is one coalesced load with one point per lane, an insertion is a ballot + shuffle.
+// Output contract identical to k_knn_wave (positions [KL][N], worst key W per query).
+// =============================================================================================
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const float4* __restrict__ spt,
+                                                          const unsigned* __restrict__ qperm, int N,
+                                                          const double* __restrict__ pose,
+                                                          const int* __restrict__ done, KParams kp,
+                                                          const double* __restrict__ delta,
+                                                          int* __restrict__ lists, float* __restrict__ wlist,
+                                                          int use_prev, unsigned long long* __restrict__ nbr_stats) {
+    static_assert(KL <= 64, "one list entry per lane");
+    if (done && *done) return;
+    __shared__ int snode[kWaveBlock / 64][kStackDepth];
+    __shared__ float sdist[kWaveBlock / 64][kStackDepth];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (kWaveBlock / 64) + wv);
+    if (slot >= N) return;
+    float xf[3];
+    {
+        double ns[3];
+        transform_query(pose, spt[qperm[slot]], make_float4(0.f, 0.f, 0.f, 0.f), 0, xf, ns);
+    }
+    float lkey = kInfF;     // lane k < KL: entry k of the ascending list
+    int lpos = -1;
+    const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
+    float bnd = r2s;
+    const int P = t.P, B = t.B, M = t.M;
+    // insert (c, cp): entries ordered by (key, position); the tail shifts up by one lane
+    auto insert = [&](float c, int cp) {
+        const unsigned long long before = __ballot(lane < KL && (lkey < c || (lkey == c && lpos < cp)));
+        const int at = __popcll(before);
+        const float uk = __shfl_up(lkey, 1, 64);
+        const int up = __shfl_up(lpos, 1, 64);
+        if (lane > at && lane < KL) { lkey = uk; lpos = up; }
+        if (lane == at) { lkey = c; lpos = cp; }
+        bnd = fminf(r2s, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), KL - 1)));
+    };
+    auto worst = [&]() { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), KL - 1)); };
+    int seed_lo = 0, seed_hi = -1;
+    bool greedy = !use_prev;
+    if (use_prev) {
+        double rf = 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const double e = delta[r * 4 + c] - (r == c ? 1.0 : 0.0);
+                rf += e * e;
+            }
+        const float tn = (float)sqrt(delta[3] * delta[3] + delta[7] * delta[7] + delta[11] * delta[11]);
+        const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
+        greedy = disp * disp > kp.reseed * wlist[slot];
+    }
+    if (!greedy) {
+        // prefill: previous list re-measured at the new pose
+        const int pos = lane < KL ? lists[(size_t)lane * N + slot] : -1;
+        float d = kInfF;
+        if (pos >= 0) {
+            const float4 q = t.mpt[pos];
+            const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
+            d = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+        }
+        for (int k = 0; k < KL; ++k) {
+            const int cp = __builtin_amdgcn_readlane(pos, k);
+            const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), k));
+            if (cp >= 0 && c <= bnd && c < worst()) insert(c, cp);
+        }
+    } else {
+        // seed: the leaf of the query's own Morton key ± seed_half Morton neighbours
+        const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
+        int lo = 0, hi = t.L - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (t.lkeys[mid] <= qk) lo = mid;
+            else hi = mid - 1;
+        }
+        seed_lo = max(0, lo - kp.seed_half);
+        seed_hi = min(t.L - 1, lo + kp.seed_half);
+        for (int leaf = seed_lo; leaf <= seed_hi; ++leaf) {
+            const int base = leaf * B, cnt = min(B, M - base);
+            float d = kInfF;
+            if (lane < cnt) {
+                const float4 q = t.mpt[base + lane];
+                const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
+                d = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+            }
+            unsigned long long m = __ballot(lane < cnt && d <= bnd);
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), j));
+                if (c <= bnd && c < worst()) insert(c, base + j);
+            }
+        }
+    }
+    unsigned n_inner = 0, n_leaf = 0;
+    int node = 1, sp = 0;
+    while (true) {
+        if (node < P) {
+            ++n_inner;
+            const float4* rec = t.nodes + 3 * (size_t)node;
+            const float4 a = rec[0], b = rec[1], c = rec[2];
+            const float dl = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+            const float dr = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
+            const float bs = bnd * kBoxSlack;
+            const bool nl = dl <= bs, nr = dr <= bs;
+            if (nl && nr) {
+                const bool lf = dl <= dr;
+                snode[wv][sp] = lf ? 2 * node + 1 : 2 * node;
+                sdist[wv][sp] = lf ? dr : dl;
+                ++sp;
+                node = lf ? 2 * node : 2 * node + 1;
+                continue;
+            }
+            if (nl) { node = 2 * node; continue; }
+            if (nr) { node = 2 * node + 1; continue; }
+        } else {
+            ++n_leaf;
+            const int leaf = node - P;
+            if (leaf < seed_lo || leaf > seed_hi) {
+                const int base = leaf * B, cnt = min(B, M - base);
+                float d = kInfF;
+                if (lane < cnt) {
+                    const float4 q = t.mpt[base + lane];
+                    const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
+                    d = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                }
+                unsigned long long m = __ballot(lane < cnt && d <= bnd && d < worst());
+                while (m) {
+                    const int j = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const float cd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), j));
+                    const int cp = base + j;
+                    if (cd <= bnd && cd < worst() && !__ballot(lane < KL && lpos == cp)) insert(cd, cp);
+                }
+            }
+        }
+        node = 0;
+        while (sp > 0) {
+            --sp;
+            if (sdist[wv][sp] <= bnd * kBoxSlack) { node = snode[wv][sp]; break; }
+        }
+        if (!node) break;
+    }
+    if (lane < KL) lists[(size_t)lane * N + slot] = lpos;
+    if (lane == 0) wlist[slot] = worst();
     if (nbr_stats && lane == 0) {
         atomicAdd(&nbr_stats[2], (unsigned long long)n_leaf);
         atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
@@ -835,7 +987,13 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
                  const double* delta, int* lists, int use_prev, hipEvent_t* marks) {
     float* wlist = reinterpret_cast<float*>(lists + (size_t)KL * N);
     if (marks) (void)hipEventRecord(marks[0], s);
-    k_knn_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, use_prev, stats);
+    // sparse query sets (≤ kQwaveAutoN queries, e.g. FPS-sampled frames): one wave per query;
+    // dense scans: packets of 64 Morton-coherent queries
+    if (kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN))
+        k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
+                                                                                          delta, lists, wlist, use_prev, stats);
+    else
+        k_knn_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, use_prev, stats);
     if (marks) (void)hipEventRecord(marks[1], s);
     k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,
                                                stats, fb_list, fb_count);

@@ -341,6 +341,176 @@ __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, S
     finish_iteration(st, tr, D, (double)st.sel[6], out[27], update_pose, kp);
 }
 
+// Small systems (≤ kSmallRows rows, e.g. the ≤2000-query frames of the config-C stream): the whole
+// LS solve in ONE block — reduce the pass-1 slabs, first solve, |r| keys of the valid rows into
+// LDS, bitonic sort by (|r| bits, row), ranks [lo, hi] re-reduced, second solve, pose update —
+// instead of five launches whose fixed latency dominates at this size.  Same arithmetic and the
+// same exact (|r|, row) order as the chain.
+constexpr int kSmallRows = 4096;      // rows the single-block solve holds in LDS (keys, rows, boundary candidates)
+constexpr int kSmallBlock = 256;     // 4 waves: cheap barriers for the sort and reductions
+constexpr int kSmallBins = 4096;     // LDS histogram: top 12 bits of the float image of |r| (1/16 octave)
+__device__ __forceinline__ int small_bin(unsigned long long keybits) {
+    return (int)(__float_as_uint((float)__longlong_as_double((long long)keybits)) >> 19);
+}
+#ifdef IMLS_DEBUG_WAVE_TRACE
+__device__ unsigned long long g_dbg_solve[8];
+#define DBG_STAMP(k) do { if (threadIdx.x == 0) g_dbg_solve[k] += wall_clock64() - dbg_t; dbg_t = wall_clock64(); } while (0)
+#else
+#define DBG_STAMP(k) do { } while (0)
+#endif
+__global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, const double* __restrict__ partial, int blocks,
+                                                            SolveState st, imls_iter_trace* tr, KParams kp, int weighted,
+                                                            int update_pose) {
+    if (*st.done) return;
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    long long dbg_t = wall_clock64();
+#endif
+    __shared__ unsigned long long ck[kSmallRows];
+    __shared__ unsigned cr[kSmallRows];
+    __shared__ unsigned long long qk[kSmallRows];
+    __shared__ unsigned qr[kSmallRows];
+    __shared__ unsigned hist[kSmallBins];
+    __shared__ unsigned csum[kSmallBlock];
+    __shared__ int bsel[5];
+    __shared__ int ncand;
+    __shared__ double red[(kSmallBlock / 64) * kNormEq];
+    __shared__ double acc[kNormEq];
+    __shared__ double xs[6];
+    __shared__ int nkey;
+    __shared__ int stop;
+    const int t = threadIdx.x;
+    double loc[kNormEq];
+#pragma unroll
+    for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
+    for (int b = t; b < blocks; b += kSmallBlock)
+#pragma unroll
+        for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
+    if (t == 0) { nkey = 0; stop = 0; }
+    block_sum28<kSmallBlock>(loc, red, acc);
+    DBG_STAMP(0);
+    const double nvalid = acc[27];
+    if (t == 0) {
+        double x[6];
+        if (update_pose && nvalid < (double)kp.correspond_number) {   // laser_odometry.cpp:570-576
+            *st.status = IMLS_FRAME_TOO_FEW;
+            *st.done = 1;
+            if (tr) tr->n_valid = (unsigned long long)nvalid;
+            stop = 1;
+        } else {
+            solve6(acc, x);
+            if (weighted) {
+                double D[16];
+                delta_from_x(x, D);
+                finish_iteration(st, tr, D, nvalid, nvalid, update_pose, kp);
+                stop = 1;
+            }
+            for (int k = 0; k < 6; ++k) xs[k] = x[k];
+        }
+    }
+    __syncthreads();
+    DBG_STAMP(1);
+    if (stop) return;
+    // |r| under the first solution, valid rows only (solver.cpp:110-122)
+    for (int i = t; i < N; i += kSmallBlock) {
+        double a[6], b, wt;
+        if (rows.get(i, a, b, wt)) {
+            double v = a[0] * xs[0];
+            for (int k = 1; k < 6; ++k) v = v + a[k] * xs[k];
+            const double key = fabs(v - b);
+            const int at = atomicAdd(&nkey, 1);
+            ck[at] = (unsigned long long)__double_as_longlong(key);
+            cr[at] = (unsigned)i;
+        }
+    }
+    __syncthreads();
+    DBG_STAMP(2);
+    const int n = nkey;
+    const long long lo = (long long)(kp.ls_threshold * (double)n);
+    long long hi = (long long)((1 - kp.ls_threshold) * (double)n);
+    if (hi > n - 1) hi = n - 1;       // Q11
+    // exact ranks at the two trim boundaries: a 4096-bin LDS histogram of the float image of |r|
+    // (monotone) locates the boundary bins; only their rows are sorted by (|r| bits, row)
+    for (int b = t; b < kSmallBins; b += kSmallBlock) hist[b] = 0u;
+    __syncthreads();
+    for (int r = t; r < n; r += kSmallBlock) atomicAdd(&hist[small_bin(ck[r])], 1u);
+    __syncthreads();
+    {
+        constexpr int per = kSmallBins / kSmallBlock;
+        unsigned loc_sum = 0;
+        for (int k = 0; k < per; ++k) loc_sum += hist[t * per + k];
+        csum[t] = loc_sum;
+        __syncthreads();
+        for (int off = 1; off < kSmallBlock; off <<= 1) {
+            const unsigned v = t >= off ? csum[t - off] : 0u;
+            __syncthreads();
+            csum[t] += v;
+            __syncthreads();
+        }
+        long long cum = (long long)csum[t] - loc_sum;
+        for (int k = 0; k < per; ++k) {
+            const long long c = hist[t * per + k];
+            if (lo >= cum && lo < cum + c) { bsel[0] = t * per + k; bsel[2] = (int)cum; }
+            if (hi >= cum && hi < cum + c) { bsel[1] = t * per + k; bsel[3] = (int)cum; }
+            cum += c;
+        }
+        if (t == 0) ncand = 0;
+    }
+    __syncthreads();
+    const int blo = bsel[0], bhi = bsel[1];
+    if (t == 0) bsel[4] = (int)hist[blo];           // candidates of the lower boundary bin
+    for (int r = t; r < n; r += kSmallBlock) {
+        const int b = small_bin(ck[r]);
+        if (b == blo || b == bhi) {
+            const int at = atomicAdd(&ncand, 1);
+            qk[at] = ck[r];
+            qr[at] = cr[r];
+        }
+    }
+    __syncthreads();
+    const int nc = ncand;
+    int np = 1;
+    while (np < nc) np <<= 1;
+    for (int i = nc + t; i < np; i += kSmallBlock) { qk[i] = ~0ull; qr[i] = ~0u; }
+    __syncthreads();
+    bitonic(qk, qr, np);
+    DBG_STAMP(3);
+#pragma unroll
+    for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
+    auto add_row = [&](unsigned row) {
+        double a[6], b, wt;
+        rows.get((int)row, a, b, wt);
+        int k = 0;
+        for (int p = 0; p < 6; ++p)
+            for (int c = p; c < 6; ++c) loc[k++] += a[p] * a[c];
+        for (int p = 0; p < 6; ++p) loc[21 + p] += a[p] * b;
+        loc[27] += 1.0;
+    };
+    for (int r = t; r < n; r += kSmallBlock) {     // interior bins: kept without ranking
+        const int b = small_bin(ck[r]);
+        if (b > blo && b < bhi) add_row(cr[r]);
+    }
+    for (int q = t; q < nc; q += kSmallBlock) {    // boundary bins: exact rank = bin base + order
+        const int b = small_bin(qk[q]);
+        int first = 0;                              // first candidate of this bin in sorted order
+        if (b == bhi && bhi != blo) {
+            // candidates of blo sort before those of bhi: count them
+            first = bsel[4];
+        }
+        const long long rank = (long long)(b == blo ? bsel[2] : bsel[3]) + (q - first);
+        if (rank >= lo && rank <= hi) add_row(qr[q]);
+    }
+    block_sum28<kSmallBlock>(loc, red, acc);
+    DBG_STAMP(4);
+    if (t != 0) return;
+    double x[6], D[16];
+    solve6(acc, x);
+    DBG_STAMP(5);
+    delta_from_x(x, D);
+    DBG_STAMP(6);
+    finish_iteration(st, tr, D, (double)n, acc[27], update_pose, kp);
+    DBG_STAMP(7);
+}
+
 }  // namespace
 
 int solve_blocks(int N) { return (N + kBlock - 1) / kBlock; }
@@ -361,6 +531,10 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
         k_rows_pass1<kBlock><<<blocks1, kBlock, 0, s>>>(rows, N, st.partial1);
     }
     const int weighted = kp.solve_method == IMLS_SOLVE_WEIGHTED_LS;
+    if (!rows_are_double && N <= kSmallRows) {
+        k_solve_small<<<1, kSmallBlock, 0, s>>>(rows, N, st.partial1, blocks1, st, tr, kp, weighted, update_pose);
+        return;
+    }
     k_solve_first<<<1, 256, 0, s>>>(st.partial1, blocks1, st, tr, kp, weighted, update_pose);
     if (weighted) return;
     k_resid_hist<kBlock><<<solve_blocks(N), kBlock, 0, s>>>(rows, N, st, kp);
@@ -371,3 +545,9 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
 }
 
 }  // namespace imlsgpu
+
+#ifdef IMLS_DEBUG_WAVE_TRACE
+extern "C" int imls_debug_solve(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(imlsgpu::g_dbg_solve), 64) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -59,8 +59,19 @@ def check_projection(got, want_idx, want_rej, want_x, want_y, want_n):
     return float((dy == 0).all(axis=1).mean())
 
 
+@pytest.fixture(params=["auto", "0", "1"], ids=["auto", "packets", "wave_per_query"])
+def traversal(request, monkeypatch):
+    """Both traversal kernels on the same inputs: packets of 64 queries (k_knn_wave) and one wave
+    per query (k_knn_qwave); the choice is read when the parameters are set."""
+    if request.param != "auto":
+        monkeypatch.setenv("IMLS_QWAVE", request.param)
+    else:
+        monkeypatch.delenv("IMLS_QWAVE", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair"])
-def test_project_matches_golden(ctx, name):
+def test_project_matches_golden(ctx, name, traversal):
     g = golden(name)
     p = gparams()
     ctx.set_params(p)
@@ -74,7 +85,7 @@ def test_project_matches_golden(ctx, name):
 
 
 @pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair"])
-def test_register_frame_matches_golden(ctx, name):
+def test_register_frame_matches_golden(ctx, name, traversal):
     g = golden(name)
     ctx.set_params(gparams())
     ctx.set_target(soa_to_rows(g["tgt"]))
