@@ -228,7 +228,7 @@ int imls_reset_timing(imls_ctx* ctx);
 int imls_index_stats(imls_ctx* ctx, uint64_t out[8]);
 /* Counters accumulated since the last frame start / projection (diagnostics): Σ k_q, NN-1 found,
  * leaves visited (per wave), inner nodes visited (per wave), waves, uncertified queries re-run
- * exactly, 0, 0. */
+ * exactly, lanes whose list was reused without a traversal (Verlet reuse), 0. */
 int imls_traversal_stats(imls_ctx* ctx, uint64_t out[8]);
 
 #ifdef __cplusplus

@@ -122,6 +122,8 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_SEED_HALF")) k.seed_half = std::atoi(w);
     if (const char* w = std::getenv("IMLS_RESEED")) k.reseed = (float)std::atof(w);
     if (const char* w = std::getenv("IMLS_WAVE_TRACE")) k.wave_trace = std::atoi(w);
+    k.verlet = 1;
+    if (const char* w = std::getenv("IMLS_VERLET")) k.verlet = std::atoi(w);
     return k;
 }
 
@@ -154,7 +156,7 @@ int ensure_solve(imls_ctx* c, int N) {
     size_t n = (size_t)std::max(N, 1);
     if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, n * 4 + 256))
         return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
-    if (!grow(c->prevnn, n * (kMaxKL + 1) * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
+    if (!grow(c->prevnn, prevnn_bytes((int)n))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
     const int pb = std::max(project_blocks((int)n), solve_blocks((int)n)) + 1;
     size_t bytes = 0;
     auto add = [&](size_t b) { size_t o = bytes; bytes += (b + 255) / 256 * 256; return o; };

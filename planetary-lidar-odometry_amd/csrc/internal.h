@@ -54,6 +54,7 @@ struct KParams {
     int sparse_lanes;         // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
     int sparse_lanes_seed;    // the same for waves holding freshly seeded lanes
     int qwave;                // traversal: 0 = packets of 64 queries per wave, 1 = one wave per query
+    int verlet;               // reuse a query's list without traversal while its certification holds
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
 };
 
@@ -131,6 +132,12 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
 // kept across ICP iterations (temporal seed); marks: 3 events recorded before k_knn_wave, between
 // it and k_finish, and after k_finish (timing), or null
 constexpr int kMaxKL = 36;
+// per-query reference position + list guarantee (float4), after the [kMaxKL+1][N] list block
+inline float4* xref_of(int* lists, int N) {
+    return reinterpret_cast<float4*>(reinterpret_cast<char*>(lists) + ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256);
+}
+inline size_t prevnn_bytes(int N) { return ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256 + (size_t)N * 16; }
+constexpr int kStatSkipped = 6;   // nbr_stats slot: lanes whose list was reused without traversal
 int project_blocks(int N);
 
 // solve.hip

@@ -277,6 +277,40 @@ constexpr int kDbgWaves = 8192;
 __device__ unsigned g_dbg_wave[kDbgWaves][16];
 #endif
 
+
+// Verlet-list reuse (neighbour lists with a skin, as in molecular dynamics): the list of a query
+// was built at xr.xyz with the guarantee that every map point outside it has fp32 key ≥ xr.w.
+// At the new position x (|x − xr| = D) those points are at exact distance ≥ √xr.w − D, so the
+// re-measured list (lk, ascending) is the exact answer when the distance it relies on — the K-th
+// key within r (or r itself when fewer than K are within r) and the NN-1 key — stays below that
+// bound.  fp32 keys carry ≤ 3.1e-7 relative error and D ≤ 3e-7 relative: the 1e-6 factors and
+// the 1e-5 margin cover both, and k_finish re-certifies in fp64 against the returned bound
+// (a failure there only costs the exact fallback).  Returns true when the traversal can be
+// skipped; w_out = lower bound (exact d²) of every point outside the list.
+template <int KL>
+__device__ __forceinline__ bool verlet_skip(const float (&lk)[KL], float4 xr, const float xf[3], float r2s,
+                                            const KParams& kp, float& w_out) {
+    const float dx = xf[0] - xr.x, dy = xf[1] - xr.y, dz = xf[2] - xr.z;
+    const float D = sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
+    const float g = sqrtf(xr.w) * (1.0f - 1e-6f) - D * (1.0f + 1e-6f) - 1e-6f;
+    if (!(g > 0.f)) return false;
+    const float w = fminf(g * g, r2s);
+    const float r2f = (float)kp.r2 * (1.0f + 1e-6f);
+    int cnt_r = 0;
+    float dK = kInfF, d1 = kInfF;
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+        const bool in = lk[j] <= r2f;
+        cnt_r += in ? 1 : 0;
+        if (in && d1 == kInfF && lk[j] > 1e-15f) d1 = lk[j];
+        if (j == kp.K - 1) dK = lk[j];
+    }
+    if (d1 == kInfF) return false;
+    const float need = fmaxf(cnt_r >= kp.K ? dK : r2f, d1);
+    w_out = w;
+    return need * (1.0f + 1e-5f) < w;
+}
+
 template <int KL>
 __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
@@ -284,7 +318,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                                                          const int* __restrict__ done, KParams kp,
                                                          const double* __restrict__ delta,
                                                          int* __restrict__ lists, float* __restrict__ wlist,
-                                                         int use_prev, unsigned long long* __restrict__ nbr_stats) {
+                                                         float4* __restrict__ xref, int use_prev,
+                                                         unsigned long long* __restrict__ nbr_stats) {
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kStackDepth];
     __shared__ float4 sbox[kWaveBlock / 64][kStackDepth][2];
@@ -310,6 +345,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
 #endif
     int seed_lo = 0, seed_hi = -1;   // leaves already scanned by the seed pass (skipped below)
     bool greedy = active && !use_prev;
+    bool skip = false;               // list certified without a traversal (Verlet-list reuse)
+    float wskip = kInfF;
     if (active && use_prev) {
         // temporal seed only while the query moved little against its neighbourhood: the last
         // pose increment Δ moves it by at most ‖t‖ + ‖R − I‖_F·‖x‖
@@ -342,6 +379,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                 }
             }
         }
+        if (kp.verlet) skip = verlet_skip<KL>(lk, xref[slot], xf, r2s, kp, wskip);
     } else if (active) {
         // seed: the leaf the query's own Morton key falls into (binary search over the leaves'
         // first keys) and its Morton neighbours — Morton-near points are mostly space-near, while
@@ -379,9 +417,12 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
 #endif
     // waves with freshly seeded lanes insert a lot: per-lane leaf scans would serialise that
     const int sparse_thr = __ballot(greedy) ? kp.sparse_lanes_seed : kp.sparse_lanes;
+    if (skip) bnd = -1.0f;           // a certified lane takes no part in the traversal
     int node = 1, sp = 0;
-    unsigned long long em = __ballot(active);   // lanes whose bound admits the current node's box
-    while (true) {
+    unsigned long long em = __ballot(active && !skip);   // lanes whose bound admits the current node's box
+    const unsigned long long skipped = __ballot(skip);
+    if (nbr_stats && lane == 0 && skipped) atomicAdd(&nbr_stats[kStatSkipped], (unsigned long long)__popcll(skipped));
+    while (em) {
         if (node < P) {
             ++n_inner;
             const float4* rec = t.nodes + 3 * (size_t)node;
@@ -492,7 +533,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
     if (active) {
 #pragma unroll
         for (int j = 0; j < KL; ++j) lists[(size_t)j * N + slot] = lp[j];
-        wlist[slot] = lk[KL - 1];
+        wlist[slot] = skip ? wskip : lk[KL - 1];
+        // reference position + guarantee of a fresh list: every map point outside it has fp32
+        // key ≥ the KL-th key (full list) or > the search bound (all points within r listed)
+        if (!skip) xref[slot] = make_float4(xf[0], xf[1], xf[2], lk[KL - 1] < kInfF ? lk[KL - 1] : r2s);
     }
 #ifdef IMLS_DEBUG_WAVE_TRACE   // debug build only (make DEBUG_WAVE_TRACE=1): insert counters
     if (nbr_stats && lane == 0) {
@@ -550,7 +594,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
                                                           const int* __restrict__ done, KParams kp,
                                                           const double* __restrict__ delta,
                                                           int* __restrict__ lists, float* __restrict__ wlist,
-                                                          int use_prev, unsigned long long* __restrict__ nbr_stats) {
+                                                          float4* __restrict__ xref, int use_prev,
+                                                          unsigned long long* __restrict__ nbr_stats) {
     static_assert(KL <= 64, "one list entry per lane");
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kStackDepth];
@@ -582,6 +627,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
     auto worst = [&]() { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), KL - 1)); };
     int seed_lo = 0, seed_hi = -1;
     bool greedy = !use_prev;
+    bool skip = false;
+    float wskip = kInfF;
     if (use_prev) {
         double rf = 0.0;
 #pragma unroll
@@ -608,6 +655,12 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
             const int cp = __builtin_amdgcn_readlane(pos, k);
             const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), k));
             if (cp >= 0 && c <= bnd && c < worst()) insert(c, cp);
+        }
+        if (kp.verlet) {
+            float lkr[KL];   // the list gathered to every lane (wave-uniform test)
+#pragma unroll
+            for (int k = 0; k < KL; ++k) lkr[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), k));
+            skip = verlet_skip<KL>(lkr, xref[slot], xf, r2s, kp, wskip);
         }
     } else {
         // seed: the leaf of the query's own Morton key ± seed_half Morton neighbours
@@ -638,8 +691,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
         }
     }
     unsigned n_inner = 0, n_leaf = 0;
-    int node = 1, sp = 0;
-    while (true) {
+    int node = skip ? 0 : 1, sp = 0;
+    if (nbr_stats && lane == 0 && skip) atomicAdd(&nbr_stats[kStatSkipped], 1ull);
+    while (node) {
         if (node < P) {
             ++n_inner;
             const float4* rec = t.nodes + 3 * (size_t)node;
@@ -687,7 +741,11 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
         if (!node) break;
     }
     if (lane < KL) lists[(size_t)lane * N + slot] = lpos;
-    if (lane == 0) wlist[slot] = worst();
+    if (lane == 0) {
+        const float wk = worst();
+        wlist[slot] = skip ? wskip : wk;
+        if (!skip) xref[slot] = make_float4(xf[0], xf[1], xf[2], wk < kInfF ? wk : r2s);
+    }
     if (nbr_stats && lane == 0) {
         atomicAdd(&nbr_stats[2], (unsigned long long)n_leaf);
         atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
@@ -986,14 +1044,16 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
                  double* partial1, imls_iter_trace* tr, unsigned long long* stats, unsigned* fb_list, unsigned* fb_count,
                  const double* delta, int* lists, int use_prev, hipEvent_t* marks) {
     float* wlist = reinterpret_cast<float*>(lists + (size_t)KL * N);
+    float4* xref = xref_of(lists, N);
     if (marks) (void)hipEventRecord(marks[0], s);
     // sparse query sets (≤ kQwaveAutoN queries, e.g. FPS-sampled frames): one wave per query;
     // dense scans: packets of 64 Morton-coherent queries
     if (kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
-                                                                                          delta, lists, wlist, use_prev, stats);
+                                                                                          delta, lists, wlist, xref, use_prev, stats);
     else
-        k_knn_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, use_prev, stats);
+        k_knn_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, use_prev,
+                                                    stats);
     if (marks) (void)hipEventRecord(marks[1], s);
     k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,
                                                stats, fb_list, fb_count);

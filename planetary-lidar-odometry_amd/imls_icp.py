@@ -190,7 +190,7 @@ class ImlsContext:
     def traversal_stats(self) -> dict:
         out = np.zeros(8, np.uint64)
         self._check(self.lib.imls_traversal_stats(self.ctx, _ptr(out)))
-        keys = ("sum_kq", "nn_found", "leaves_visited", "inner_visited", "waves", "uncertified")
+        keys = ("sum_kq", "nn_found", "leaves_visited", "inner_visited", "waves", "uncertified", "verlet_reused")
         return {k: int(v) for k, v in zip(keys, out)}
 
 

@@ -1,0 +1,107 @@
+"""Verlet-list reuse (k_knn_wave / k_knn_qwave skip the traversal while a query's previous
+neighbour list stays certified) must not change a single correspondence: per-iteration valid
+counts and reject counters are compared exactly with the reuse switched off (IMLS_VERLET=0), and
+the poses to 1e-12 — the correspondences are identical, but a query whose reused bound fails the
+fp64 certificate is finished by the exact fallback kernel, which sums its normal-equation terms
+in a different slab (a different fp64 association).  The full config-B frame is also compared
+with the CPU oracle.
+
+The oracle restates laser_odometry.cpp:478-660 / imls_icp.cpp:496-745 / solver.cpp:74-166
+(oracle/imls_oracle.cpp); it knows nothing about list reuse, so agreement with it is the check
+that the reuse certificate is sound on a realistic 1.26M-point map.
+"""
+import pathlib
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+from planetary_lidar_odometry_amd import _abi, config, imls_icp, synth
+
+pytestmark = pytest.mark.gpu
+GOLDEN = pathlib.Path(__file__).resolve().parent / "golden"
+POSE_TOL = 1e-6
+
+
+def _params(iters=20, shipped_thresholds=True):
+    p = config.bench_params(iters)
+    if shipped_thresholds:
+        p.delta_dist_threshold = 0.001
+        p.delta_angle_threshold = 0.0001745353
+    return p
+
+
+def _frame(ctx, p, verlet, monkeypatch):
+    monkeypatch.setenv("IMLS_VERLET", "1" if verlet else "0")
+    ctx.set_params(p)          # KParams (incl. the reuse switch) are read when params are set
+    r = ctx.register_frame()
+    r["stats"] = ctx.traversal_stats()
+    return r
+
+
+def _same_frame(a, b):
+    assert a["iters"] == b["iters"] and a["status"] == b["status"]
+    assert np.abs(a["pose"] - b["pose"]).max() < 1e-12
+    for ta, tb in zip(a["trace"], b["trace"]):
+        assert ta.n_valid == tb.n_valid
+        assert list(ta.reject) == list(tb.reject)
+        assert np.abs(np.array(ta.delta) - np.array(tb.delta)).max() < 1e-12
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = imls_icp.ImlsContext(_params())
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def config_b():
+    return synth.make_pair("hdl64", map_scans=10)
+
+
+@pytest.mark.parametrize("qwave", ["0", "1"], ids=["packets", "wave_per_query"])
+@pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair"])
+def test_reuse_bit_identical_on_golden_pairs(ctx, name, qwave, monkeypatch):
+    g = dict(np.load(GOLDEN / f"{name}.npz"))
+    monkeypatch.setenv("IMLS_QWAVE", qwave)
+    ctx.set_target(np.ascontiguousarray(g["tgt"].T))
+    ctx.set_source(np.ascontiguousarray(g["src"].T))
+    p = _params(10, shipped_thresholds=False)
+    on = _frame(ctx, p, True, monkeypatch)
+    off = _frame(ctx, p, False, monkeypatch)
+    _same_frame(on, off)
+    assert off["stats"]["verlet_reused"] == 0
+    assert on["stats"]["verlet_reused"] > 0, on["stats"]
+
+
+def test_config_b_reuse_bit_identical(ctx, config_b, monkeypatch):
+    monkeypatch.delenv("IMLS_QWAVE", raising=False)
+    ctx.set_target(config_b.target)
+    ctx.set_source(config_b.source)
+    p = _params(20, shipped_thresholds=False)
+    on = _frame(ctx, p, True, monkeypatch)
+    off = _frame(ctx, p, False, monkeypatch)
+    _same_frame(on, off)
+    q = on["stats"]
+    # most lists are reused once the pose settles (iterations 1..19 offer N lanes each)
+    assert q["verlet_reused"] > 0.3 * 19 * config_b.source.size, q
+
+
+def test_config_b_frame_matches_oracle(ctx, config_b, monkeypatch):
+    """The headline workload end to end (index build + up to 20 iterations, shipped convergence
+    thresholds) against the oracle: iterations, status, per-iteration valid counts and reject
+    counters exact; pose within POSE_TOL."""
+    monkeypatch.delenv("IMLS_QWAVE", raising=False)
+    monkeypatch.setenv("IMLS_VERLET", "1")
+    p = _params(20)
+    ctx.set_params(p)
+    ctx.set_target(config_b.target)
+    ctx.set_source(config_b.source)
+    got = ctx.register_frame()
+    want = oc.register_frame(synth.soa(config_b.source), synth.soa(config_b.target), p)
+    assert got["iters"] == want["iters"] and got["status"] == want["status"]
+    for tg, tw in zip(got["trace"], want["trace"]):
+        assert tg.n_valid == tw.n_valid
+        assert list(tg.reject) == list(tw.reject)
+    assert np.abs(got["pose"] - want["pose"]).max() < POSE_TOL
