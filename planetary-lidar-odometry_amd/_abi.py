@@ -140,7 +140,8 @@ def load_library(path: os.PathLike | None = None) -> C.CDLL:
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = pathlib.Path(path) if path else LIB_PATH
+    # IMLS_LIB_PATH: a diagnostic build of the same library (e.g. make debug → csrc/debug/)
+    p = pathlib.Path(path) if path else pathlib.Path(os.environ.get("IMLS_LIB_PATH", LIB_PATH))
     if not p.exists():
         raise RuntimeError(f"HIP extension missing: {p} (run __graft_entry__.build())")
     lib = _bind(C.CDLL(str(p)))

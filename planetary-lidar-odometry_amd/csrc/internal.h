@@ -132,11 +132,12 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
 // kept across ICP iterations (temporal seed); marks: 3 events recorded before k_knn_wave, between
 // it and k_finish, and after k_finish (timing), or null
 constexpr int kMaxKL = 36;
-// per-query reference position + list guarantee (float4), after the [kMaxKL+1][N] list block
+// per-query reference position + list guarantee (float4 xref[N]) and the key the list's answer
+// relied on (float nref[N]), after the [kMaxKL+1][N] list block
 inline float4* xref_of(int* lists, int N) {
     return reinterpret_cast<float4*>(reinterpret_cast<char*>(lists) + ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256);
 }
-inline size_t prevnn_bytes(int N) { return ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256 + (size_t)N * 16; }
+inline size_t prevnn_bytes(int N) { return ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256 + (size_t)N * 20; }
 constexpr int kStatSkipped = 6;   // nbr_stats slot: lanes whose list was reused without traversal
 int project_blocks(int N);
 

@@ -41,7 +41,8 @@ constexpr float kInfF = __builtin_huge_valf();
 constexpr int kWaveBlock = 256;
 constexpr int kFallbackBlocks = 64;
 constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query up to this many queries
-constexpr int kSeedChunk = 8;        // seed-pass points loaded per batch
+constexpr int kSeedLeaves = 8;       // first-iteration seed pass: at most this many leaves per wave
+constexpr int kSeedChunk = 8;        // per-lane reseed: points loaded per batch
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
 constexpr double kCertSlack = 1.0 + 4e-7;
 
@@ -150,9 +151,10 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
     int nacc = 0;
 #pragma unroll
     for (int j = 0; j < CAP; ++j) {
-        if (j >= first && j < first + cnt) {
+        const bool inl = j >= first && j < first + cnt;
+        const float4 qn = t.mnr[inl ? lpos[j] : p1];   // unconditional: the loads issue together
+        if (inl) {
             ++kq;
-            const float4 qn = t.mnr[lpos[j]];
             bool ok = isfinite(qn.x) && isfinite(qn.y) && isfinite(qn.z);
             if (ok && kp.angle_on) ok = !angle_reject(ns, qn.x, qn.y, qn.z, kp.angle_thr_deg);
             if (ok) { acc |= 1ull << j; ++nacc; }
@@ -167,9 +169,10 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
     double wsum = 0.0, psum = 0.0;
 #pragma unroll
     for (int j = 0; j < CAP; ++j) {
+        const int pj = (acc & (1ull << j)) ? lpos[j] : p1;
+        const float4 qp = t.mpt[pj];
+        const float4 qn = t.mnr[pj];
         if (acc & (1ull << j)) {
-            const float4 qp = t.mpt[lpos[j]];
-            const float4 qn = t.mnr[lpos[j]];
             const double dx = xd[0] - (double)qp.x, dy = xd[1] - (double)qp.y, dz = xd[2] - (double)qp.z;
             double dn = dx * dx;
             dn = dn + dy * dy;
@@ -278,24 +281,32 @@ __device__ unsigned g_dbg_wave[kDbgWaves][16];
 #endif
 
 
-// Verlet-list reuse (neighbour lists with a skin, as in molecular dynamics): the list of a query
-// was built at xr.xyz with the guarantee that every map point outside it has fp32 key ≥ xr.w.
-// At the new position x (|x − xr| = D) those points are at exact distance ≥ √xr.w − D, so the
-// re-measured list (lk, ascending) is the exact answer when the distance it relies on — the K-th
-// key within r (or r itself when fewer than K are within r) and the NN-1 key — stays below that
-// bound.  fp32 keys carry ≤ 3.1e-7 relative error and D ≤ 3e-7 relative: the 1e-6 factors and
-// the 1e-5 margin cover both, and k_finish re-certifies in fp64 against the returned bound
-// (a failure there only costs the exact fallback).  Returns true when the traversal can be
-// skipped; w_out = lower bound (exact d²) of every point outside the list.
-template <int KL>
-__device__ __forceinline__ bool verlet_skip(const float (&lk)[KL], float4 xr, const float xf[3], float r2s,
-                                            const KParams& kp, float& w_out) {
+// Verlet-list reuse (neighbour lists with a skin, as in molecular dynamics): a query's list was
+// built at xr.xyz with the guarantee that every map point outside it has fp32 key ≥ xr.w, and
+// nr = the key its exact answer relied on there (the K-th key within r, or the NN-1 key if
+// larger; ∞ when fewer than K points were within r).  At the new position x, |x − xr| = D:
+//   * every point outside the list is at exact distance ≥ √xr.w − D          (lower bound W'),
+//   * the answer needs distances ≤ √nr + D (those K points are still there)   (upper bound U),
+// so the list — unchanged, not even re-read — still holds the exact answer when U < W'.
+// fp32 keys carry ≤ 3.1e-7 relative error and D ≤ 3e-7: the 1e-6 factors and the 1e-5 margin
+// cover both; k_finish re-certifies in fp64 against W' (a failure there only costs the exact
+// fallback).  Returns true when the traversal can be skipped; w_out = W'.
+__device__ __forceinline__ bool verlet_skip(float4 xr, float nr, const float xf[3], float r2s, float& w_out) {
     const float dx = xf[0] - xr.x, dy = xf[1] - xr.y, dz = xf[2] - xr.z;
-    const float D = sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
-    const float g = sqrtf(xr.w) * (1.0f - 1e-6f) - D * (1.0f + 1e-6f) - 1e-6f;
-    if (!(g > 0.f)) return false;
+    const float D = sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz))) * (1.0f + 1e-6f) + 1e-6f;
+    const float g = sqrtf(xr.w) * (1.0f - 1e-6f) - D;
+    if (!(g > 0.f) || !(nr < kInfF)) return false;
+    const float u = sqrtf(nr) * (1.0f + 1e-6f) + D;
     const float w = fminf(g * g, r2s);
-    const float r2f = (float)kp.r2 * (1.0f + 1e-6f);
+    w_out = w;
+    return u * u * (1.0f + 1e-5f) < w;
+}
+
+// The key a fresh list's exact answer relies on (see verlet_skip): max(K-th key within r, NN-1
+// key), ∞ when fewer than K keys are within r or no NN-1 exists.  lk ascending.
+template <int KL>
+__device__ __forceinline__ float need_key(const float (&lk)[KL], float r2, int K) {
+    const float r2f = r2 * (1.0f + 1e-6f);
     int cnt_r = 0;
     float dK = kInfF, d1 = kInfF;
 #pragma unroll
@@ -303,12 +314,9 @@ __device__ __forceinline__ bool verlet_skip(const float (&lk)[KL], float4 xr, co
         const bool in = lk[j] <= r2f;
         cnt_r += in ? 1 : 0;
         if (in && d1 == kInfF && lk[j] > 1e-15f) d1 = lk[j];
-        if (j == kp.K - 1) dK = lk[j];
+        if (j == K - 1) dK = lk[j];
     }
-    if (d1 == kInfF) return false;
-    const float need = fmaxf(cnt_r >= kp.K ? dK : r2f, d1);
-    w_out = w;
-    return need * (1.0f + 1e-5f) < w;
+    return cnt_r >= K ? fmaxf(dK, d1) : kInfF;
 }
 
 template <int KL>
@@ -318,8 +326,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                                                          const int* __restrict__ done, KParams kp,
                                                          const double* __restrict__ delta,
                                                          int* __restrict__ lists, float* __restrict__ wlist,
-                                                         float4* __restrict__ xref, int use_prev,
-                                                         unsigned long long* __restrict__ nbr_stats) {
+                                                         float4* __restrict__ xref, float* __restrict__ nref,
+                                                         int use_prev, unsigned long long* __restrict__ nbr_stats) {
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kStackDepth];
     __shared__ float4 sbox[kWaveBlock / 64][kStackDepth][2];
@@ -362,42 +370,149 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
         const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
         greedy = disp * disp > kp.reseed * wlist[slot];
     }
-    if (active && !greedy) {
-        // prefill from the previous iteration's list re-measured at the new pose (all lanes insert
-        // in lockstep, so the list is full and the bound tight before the traversal starts; a
-        // later leaf insert must then skip points already listed)
+    if (active && !greedy && kp.verlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip);
+    if (active && !greedy && !skip) {
+        // prefill from the previous iteration's list re-measured at the new pose: all positions,
+        // then all points are loaded before any is consumed (two memory round trips, not 2·KL),
+        // and the nearly sorted keys are ordered by an early-exit odd-even transposition sort
+        // (the list is full and the bound tight before the traversal starts; a later leaf insert
+        // must then skip points already listed)
+#pragma unroll
+        for (int j = 0; j < KL; ++j) lp[j] = lists[(size_t)j * N + slot];
 #pragma unroll
         for (int j = 0; j < KL; ++j) {
-            const int pos = lists[(size_t)j * N + slot];
-            if (pos >= 0) {
-                const float4 q = t.mpt[pos];
-                const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
+            const float4 q = t.mpt[max(lp[j], 0)];
+            const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
+            const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+            const bool keep = lp[j] >= 0 && d32 <= r2s;
+            lk[j] = keep ? d32 : kInfF;
+            lp[j] = keep ? lp[j] : -1;
+        }
+        bool swapped = true;
+        while (swapped) {
+            swapped = false;
+#pragma unroll
+            for (int par = 0; par < 2; ++par) {
+#pragma unroll
+                for (int j = par; j + 1 < KL; j += 2) {
+                    const bool sw = lk[j + 1] < lk[j];
+                    const float tk = lk[j];
+                    const int tp = lp[j];
+                    lk[j] = sw ? lk[j + 1] : lk[j];
+                    lp[j] = sw ? lp[j + 1] : lp[j];
+                    lk[j + 1] = sw ? tk : lk[j + 1];
+                    lp[j + 1] = sw ? tp : lp[j + 1];
+                    swapped |= sw;
+                }
+            }
+        }
+        bnd = fminf(r2s, lk[KL - 1]);
+    }
+    // leaf scan shared by the seed pass and the traversal: the lanes in `want` test every point of
+    // leaf `leaf` against their bound; `listed`: the leaf may hold points already in a lane's
+    // list (prefilled or seeded), which must not be inserted twice
+    int sparse_thr = kp.sparse_lanes;
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    unsigned dbg_ev = 0, dbg_ins = 0;
+    unsigned dbg_sparse = 0, dbg_bcast = 0, dbg_sparse_lanes = 0, dbg_sparse_ins = 0;
+#endif
+    auto scan_leaf = [&](int leaf, unsigned long long want, bool listed) {
+        const int base = leaf * B;
+        const int cnt = min(B, M - base);
+        float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane < cnt) mine = t.mpt[base + lane];
+        // points of this leaf already in the lane's list, as a bit mask: one lockstep pass over
+        // the list instead of a divergent membership test per point
+        unsigned long long inl = 0ull;
+        if (listed) {
+#pragma unroll
+            for (int k = 0; k < KL; ++k) {
+                const unsigned rel = (unsigned)(lp[k] - base);
+                inl |= rel < 64u ? (1ull << rel) : 0ull;
+            }
+        }
+#ifdef IMLS_DEBUG_WAVE_TRACE
+        if (__popcll(want) <= sparse_thr) { ++dbg_sparse; dbg_sparse_lanes += __popcll(want); } else { ++dbg_bcast; }
+#endif
+        if (__popcll(want) <= sparse_thr) {
+            // few lanes want this leaf (spread-out queries in a dense region): per wanting lane,
+            // all leaf points are measured at once (one per lane) and only the ones under that
+            // lane's bound and not yet listed are handed to it, in index order
+            unsigned long long m = want;
+            while (m) {
+                const int q = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
+                m &= m - 1;
+                const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[0]), q));
+                const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[1]), q));
+                const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[2]), q));
+                const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bnd), q));
+                const unsigned long long inq =
+                    ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(inl >> 32), q) << 32) |
+                    (unsigned)__builtin_amdgcn_readlane((int)(unsigned)inl, q);
+                const float ex = mine.x - qx, ey = mine.y - qy, ez = mine.z - qz;
                 const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                if (d32 <= bnd && d32 < lk[KL - 1]) {
-                    insert_top<KL>(lk, lp, d32, pos);
+                unsigned long long pm = __ballot(lane < cnt && d32 <= qb) & ~inq;
+                while (pm) {
+                    const int j = __builtin_amdgcn_readfirstlane(__builtin_ctzll(pm));
+                    pm &= pm - 1;
+                    const float dj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d32), j));
+                    if (lane == q && dj <= bnd && dj < lk[KL - 1]) {
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                        ++dbg_sparse_ins;
+#endif
+                        insert_top<KL>(lk, lp, dj, base + j);
+                        bnd = fminf(r2s, lk[KL - 1]);
+                    }
+                }
+            }
+        } else {
+            const bool wants = (want >> lane) & 1ull;
+            for (int j = 0; j < cnt; ++j) {
+                const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
+                const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.y), j));
+                const float pz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.z), j));
+                const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
+                const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                const bool ins = wants && d32 <= bnd && d32 < lk[KL - 1] && !((inl >> j) & 1ull);
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                const unsigned long long bi = __ballot(ins);
+                dbg_ev += bi ? 1 : 0;
+                dbg_ins += __popcll(bi);
+#endif
+                if (ins) {
+                    insert_top<KL>(lk, lp, d32, base + j);
                     bnd = fminf(r2s, lk[KL - 1]);
                 }
             }
         }
-        if (kp.verlet) skip = verlet_skip<KL>(lk, xref[slot], xf, r2s, kp, wskip);
-    } else if (active) {
-        // seed: the leaf the query's own Morton key falls into (binary search over the leaves'
-        // first keys) and its Morton neighbours — Morton-near points are mostly space-near, while
-        // a greedy box-distance descent goes astray in the heavily overlapping upper-level boxes
+    };
+    // seed, first ICP iteration (every lane): the leaves holding the lanes' own Morton keys
+    // (binary search over the leaves' first keys) — Morton-near points are mostly space-near,
+    // while a greedy box-distance descent goes astray in the heavily overlapping upper-level
+    // boxes.  The wave's 64 queries are Morton-coherent, so their leaves mostly coincide: a
+    // narrow range [min, max] ± seed_half is scanned wave-wide (one coalesced load per leaf,
+    // skipped by the traversal later); otherwise each distinct lane leaf once (≤ kSeedLeaves).
+    const unsigned long long gmask = __ballot(greedy);
+    if (greedy && use_prev) {
+        // a reseeded lane amid prefilled ones: its own leaf ± seed_half, scanned per lane (the
+        // traversal re-scans these leaves harmlessly: listed points are masked, the rest are
+        // not under the bound)
         const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
-        int lo = 0, hi = t.L - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (t.lkeys[mid] <= qk) lo = mid;
-            else hi = mid - 1;
+        int l = 0, h = t.L - 1;
+        while (l < h) {
+            const int mid = (l + h + 1) >> 1;
+            if (t.lkeys[mid] <= qk) l = mid;
+            else h = mid - 1;
         }
-        seed_lo = max(0, lo - kp.seed_half);
-        seed_hi = min(t.L - 1, lo + kp.seed_half);
-        const int pend = min(M, (seed_hi + 1) * B);
-        for (int p0 = seed_lo * B; p0 < pend; p0 += kSeedChunk) {
-            float4 qs[kSeedChunk];   // issue the chunk's loads together, then consume them
+        const int p0s = max(0, l - kp.seed_half) * B;
+        const int pend = min(M, (min(t.L - 1, l + kp.seed_half) + 1) * B);
+        float4 qs[kSeedChunk];
 #pragma unroll
-            for (int k = 0; k < kSeedChunk; ++k) qs[k] = t.mpt[min(p0 + k, pend - 1)];
+        for (int k = 0; k < kSeedChunk; ++k) qs[k] = t.mpt[min(p0s + k, pend - 1)];
+        for (int p0 = p0s; p0 < pend; p0 += kSeedChunk) {
+            float4 nx[kSeedChunk];   // software pipelined: the next chunk is in flight while this one is consumed
+#pragma unroll
+            for (int k = 0; k < kSeedChunk; ++k) nx[k] = t.mpt[min(p0 + kSeedChunk + k, pend - 1)];
 #pragma unroll
             for (int k = 0; k < kSeedChunk; ++k) {
                 const float ex = qs[k].x - xf[0], ey = qs[k].y - xf[1], ez = qs[k].z - xf[2];
@@ -407,16 +522,48 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                     bnd = fminf(r2s, lk[KL - 1]);
                 }
             }
+#pragma unroll
+            for (int k = 0; k < kSeedChunk; ++k) qs[k] = nx[k];
+        }
+    }
+    if (gmask && !use_prev) {
+        sparse_thr = kp.sparse_lanes_seed;   // freshly seeded lanes insert a lot: per-lane scans would serialise that
+        int lo = 0x7fffffff;
+        if (greedy) {
+            const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
+            int l = 0, h = t.L - 1;
+            while (l < h) {
+                const int mid = (l + h + 1) >> 1;
+                if (t.lkeys[mid] <= qk) l = mid;
+                else h = mid - 1;
+            }
+            lo = l;
+        }
+        int lmin = lo, lmax = greedy ? lo : -1;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            lmin = min(lmin, __shfl_xor(lmin, o, 64));
+            lmax = max(lmax, __shfl_xor(lmax, o, 64));
+        }
+        lmin = __builtin_amdgcn_readfirstlane(lmin);
+        lmax = __builtin_amdgcn_readfirstlane(lmax);
+        if (lmax - lmin + 1 + 2 * kp.seed_half <= kSeedLeaves) {
+            seed_lo = max(0, lmin - kp.seed_half);
+            seed_hi = min(t.L - 1, lmax + kp.seed_half);
+            for (int leaf = seed_lo; leaf <= seed_hi; ++leaf) scan_leaf(leaf, gmask, false);
+        } else {
+            unsigned long long m = gmask;
+            for (int n = 0; m && n < kSeedLeaves; ++n) {
+                const int leaf = __builtin_amdgcn_readlane(lo, __builtin_ctzll(m));
+                m &= ~__ballot(lo == leaf);
+                scan_leaf(leaf, gmask, true);
+            }
         }
     }
     unsigned n_inner = 0, n_leaf = 0;
 #ifdef IMLS_DEBUG_WAVE_TRACE
-    unsigned dbg_ev = 0, dbg_ins = 0;
-    unsigned dbg_sparse = 0, dbg_bcast = 0, dbg_sparse_lanes = 0, dbg_sparse_ins = 0;
     const long long dbg_t1 = wall_clock64();
 #endif
-    // waves with freshly seeded lanes insert a lot: per-lane leaf scans would serialise that
-    const int sparse_thr = __ballot(greedy) ? kp.sparse_lanes_seed : kp.sparse_lanes;
     if (skip) bnd = -1.0f;           // a certified lane takes no part in the traversal
     int node = 1, sp = 0;
     unsigned long long em = __ballot(active && !skip);   // lanes whose bound admits the current node's box
@@ -450,74 +597,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
         } else {
             ++n_leaf;
             const int leaf = node - P;
-            const int base = leaf * B;
-            const int cnt = min(B, M - base);
-            const float lb = (leaf >= seed_lo && leaf <= seed_hi) ? -1.0f : r2s;
-            float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (lane < cnt) mine = t.mpt[base + lane];
-            // points of this leaf already in the lane's (prefilled) list, as a bit mask: one
-            // lockstep pass over the list instead of a divergent membership test per point
-            unsigned long long inl = 0ull;
-            if (use_prev) {
-#pragma unroll
-                for (int k = 0; k < KL; ++k) {
-                    const unsigned rel = (unsigned)(lp[k] - base);
-                    inl |= rel < 64u ? (1ull << rel) : 0ull;
-                }
-            }
-#ifdef IMLS_DEBUG_WAVE_TRACE
-            if (__popcll(em) <= sparse_thr) { ++dbg_sparse; dbg_sparse_lanes += __popcll(em); } else { ++dbg_bcast; }
-#endif
-            if (__popcll(em) <= sparse_thr) {
-                // few lanes want this leaf (spread-out queries in a dense region): per wanting
-                // lane, all leaf points are measured at once (one per lane) and only the ones
-                // under that lane's bound and not yet listed are handed to it, in index order
-                unsigned long long m = em;
-                while (m) {
-                    const int q = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
-                    m &= m - 1;
-                    const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[0]), q));
-                    const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[1]), q));
-                    const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[2]), q));
-                    const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fminf(lb, bnd)), q));   // lb: q's seed leaves
-                    const unsigned long long inq =
-                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(inl >> 32), q) << 32) |
-                        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)inl, q);
-                    const float ex = mine.x - qx, ey = mine.y - qy, ez = mine.z - qz;
-                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                    unsigned long long pm = __ballot(lane < cnt && d32 <= qb) & ~inq;
-                    while (pm) {
-                        const int j = __builtin_amdgcn_readfirstlane(__builtin_ctzll(pm));
-                        pm &= pm - 1;
-                        const float dj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d32), j));
-                        if (lane == q && dj <= bnd && dj < lk[KL - 1]) {
-#ifdef IMLS_DEBUG_WAVE_TRACE
-                            ++dbg_sparse_ins;
-#endif
-                            insert_top<KL>(lk, lp, dj, base + j);
-                            bnd = fminf(r2s, lk[KL - 1]);
-                        }
-                    }
-                }
-            } else {
-                for (int j = 0; j < cnt; ++j) {
-                    const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
-                    const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.y), j));
-                    const float pz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.z), j));
-                    const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
-                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                    const bool ins = d32 <= fminf(lb, bnd) && d32 < lk[KL - 1] && !((inl >> j) & 1ull);
-#ifdef IMLS_DEBUG_WAVE_TRACE
-                    const unsigned long long bi = __ballot(ins);
-                    dbg_ev += bi ? 1 : 0;
-                    dbg_ins += __popcll(bi);
-#endif
-                    if (ins) {
-                        insert_top<KL>(lk, lp, d32, base + j);
-                        bnd = fminf(r2s, lk[KL - 1]);
-                    }
-                }
-            }
+            if (leaf < seed_lo || leaf > seed_hi) scan_leaf(leaf, em, use_prev || gmask);
         }
         // pop: the stacked node's box is in LDS — re-check it against the shrunken lane bounds
         node = 0;
@@ -530,13 +610,15 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
         }
         if (!node) break;
     }
-    if (active) {
+    if (active && skip) wlist[slot] = wskip;   // a reused list stays in place
+    if (active && !skip) {
 #pragma unroll
         for (int j = 0; j < KL; ++j) lists[(size_t)j * N + slot] = lp[j];
-        wlist[slot] = skip ? wskip : lk[KL - 1];
+        wlist[slot] = lk[KL - 1];
         // reference position + guarantee of a fresh list: every map point outside it has fp32
         // key ≥ the KL-th key (full list) or > the search bound (all points within r listed)
-        if (!skip) xref[slot] = make_float4(xf[0], xf[1], xf[2], lk[KL - 1] < kInfF ? lk[KL - 1] : r2s);
+        xref[slot] = make_float4(xf[0], xf[1], xf[2], lk[KL - 1] < kInfF ? lk[KL - 1] : r2s);
+        nref[slot] = need_key<KL>(lk, (float)kp.r2, kp.K);
     }
 #ifdef IMLS_DEBUG_WAVE_TRACE   // debug build only (make DEBUG_WAVE_TRACE=1): insert counters
     if (nbr_stats && lane == 0) {
@@ -594,8 +676,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
                                                           const int* __restrict__ done, KParams kp,
                                                           const double* __restrict__ delta,
                                                           int* __restrict__ lists, float* __restrict__ wlist,
-                                                          float4* __restrict__ xref, int use_prev,
-                                                          unsigned long long* __restrict__ nbr_stats) {
+                                                          float4* __restrict__ xref, float* __restrict__ nref,
+                                                          int use_prev, unsigned long long* __restrict__ nbr_stats) {
     static_assert(KL <= 64, "one list entry per lane");
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kStackDepth];
@@ -642,7 +724,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
         const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
         greedy = disp * disp > kp.reseed * wlist[slot];
     }
-    if (!greedy) {
+    if (!greedy && kp.verlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip);
+    if (skip) {
+        // the list stays in place
+    } else if (!greedy) {
         // prefill: previous list re-measured at the new pose
         const int pos = lane < KL ? lists[(size_t)lane * N + slot] : -1;
         float d = kInfF;
@@ -655,12 +740,6 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
             const int cp = __builtin_amdgcn_readlane(pos, k);
             const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), k));
             if (cp >= 0 && c <= bnd && c < worst()) insert(c, cp);
-        }
-        if (kp.verlet) {
-            float lkr[KL];   // the list gathered to every lane (wave-uniform test)
-#pragma unroll
-            for (int k = 0; k < KL; ++k) lkr[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), k));
-            skip = verlet_skip<KL>(lkr, xref[slot], xf, r2s, kp, wskip);
         }
     } else {
         // seed: the leaf of the query's own Morton key ± seed_half Morton neighbours
@@ -740,11 +819,20 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
         }
         if (!node) break;
     }
-    if (lane < KL) lists[(size_t)lane * N + slot] = lpos;
-    if (lane == 0) {
-        const float wk = worst();
-        wlist[slot] = skip ? wskip : wk;
-        if (!skip) xref[slot] = make_float4(xf[0], xf[1], xf[2], wk < kInfF ? wk : r2s);
+    if (skip) {
+        if (lane == 0) wlist[slot] = wskip;
+    } else {
+        if (lane < KL) lists[(size_t)lane * N + slot] = lpos;
+        float lkr[KL];   // the list gathered to every lane for the reuse key
+#pragma unroll
+        for (int k = 0; k < KL; ++k) lkr[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), k));
+        const float nk = need_key<KL>(lkr, (float)kp.r2, kp.K);
+        if (lane == 0) {
+            const float wk = worst();
+            wlist[slot] = wk;
+            xref[slot] = make_float4(xf[0], xf[1], xf[2], wk < kInfF ? wk : r2s);
+            nref[slot] = nk;
+        }
     }
     if (nbr_stats && lane == 0) {
         atomicAdd(&nbr_stats[2], (unsigned long long)n_leaf);
@@ -788,18 +876,14 @@ __global__ __launch_bounds__(kWaveBlock) void k_finish(TreeView t, const float4*
         const float W = wlist[slot];
         double ed[KL];
         int eo[KL], ep[KL];
+        // all positions, then all points, before any is consumed (two memory round trips)
+#pragma unroll
+        for (int j = 0; j < KL; ++j) ep[j] = lists[(size_t)j * N + slot];
 #pragma unroll
         for (int j = 0; j < KL; ++j) {
-            const int pos = lists[(size_t)j * N + slot];
-            ep[j] = pos;
-            if (pos >= 0) {
-                const float4 q = t.mpt[pos];
-                ed[j] = exact_d2(xd, q.x, q.y, q.z);
-                eo[j] = (int)__float_as_uint(q.w);
-            } else {
-                ed[j] = kInfD;
-                eo[j] = 0x7fffffff;
-            }
+            const float4 q = t.mpt[max(ep[j], 0)];
+            ed[j] = ep[j] >= 0 ? exact_d2(xd, q.x, q.y, q.z) : kInfD;
+            eo[j] = ep[j] >= 0 ? (int)__float_as_uint(q.w) : 0x7fffffff;
         }
         // odd-even transposition sort by (d², index); the fp32 order is already nearly exact
         bool swapped = true;
@@ -1045,15 +1129,16 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
                  const double* delta, int* lists, int use_prev, hipEvent_t* marks) {
     float* wlist = reinterpret_cast<float*>(lists + (size_t)KL * N);
     float4* xref = xref_of(lists, N);
+    float* nref = reinterpret_cast<float*>(xref + N);
     if (marks) (void)hipEventRecord(marks[0], s);
     // sparse query sets (≤ kQwaveAutoN queries, e.g. FPS-sampled frames): one wave per query;
     // dense scans: packets of 64 Morton-coherent queries
     if (kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
-                                                                                          delta, lists, wlist, xref, use_prev, stats);
+                                                                                          delta, lists, wlist, xref, nref, use_prev, stats);
     else
-        k_knn_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, use_prev,
-                                                    stats);
+        k_knn_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref,
+                                                    use_prev, stats);
     if (marks) (void)hipEventRecord(marks[1], s);
     k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,
                                                stats, fb_list, fb_count);
