@@ -122,6 +122,8 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_SEED_HALF")) k.seed_half = std::atoi(w);
     if (const char* w = std::getenv("IMLS_RESEED")) k.reseed = (float)std::atof(w);
     if (const char* w = std::getenv("IMLS_WAVE_TRACE")) k.wave_trace = std::atoi(w);
+    k.wide = 3;
+    if (const char* w = std::getenv("IMLS_WIDE")) k.wide = std::max(1, std::min(3, std::atoi(w)));
     k.verlet = 1;
     if (const char* w = std::getenv("IMLS_VERLET")) k.verlet = std::atoi(w);
     return k;

@@ -54,6 +54,7 @@ struct KParams {
     int sparse_lanes;         // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
     int sparse_lanes_seed;    // the same for waves holding freshly seeded lanes
     int qwave;                // traversal: 0 = packets of 64 queries per wave, 1 = one wave per query
+    int wide;                 // packet traversal: binary levels descended per step (1..3)
     int verlet;               // reuse a query's list without traversal while its certification holds
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
 };

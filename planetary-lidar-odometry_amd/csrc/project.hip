@@ -41,6 +41,8 @@ constexpr float kInfF = __builtin_huge_valf();
 constexpr int kWaveBlock = 256;
 constexpr int kFallbackBlocks = 64;
 constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query up to this many queries
+constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
+constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
 constexpr int kSeedLeaves = 8;       // first-iteration seed pass: at most this many leaves per wave
 constexpr int kSeedChunk = 8;        // per-lane reseed: points loaded per batch
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
@@ -329,8 +331,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                                                          float4* __restrict__ xref, float* __restrict__ nref,
                                                          int use_prev, unsigned long long* __restrict__ nbr_stats) {
     if (done && *done) return;
-    __shared__ int snode[kWaveBlock / 64][kStackDepth];
-    __shared__ float4 sbox[kWaveBlock / 64][kStackDepth][2];
+    __shared__ int snode[kWaveBlock / 64][kWaveStack];
+    __shared__ float4 sbox[kWaveBlock / 64][kWaveStack][2];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int slot = blockIdx.x * kWaveBlock + tid;
@@ -571,29 +573,54 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
     if (nbr_stats && lane == 0 && skipped) atomicAdd(&nbr_stats[kStatSkipped], (unsigned long long)__popcll(skipped));
     while (em) {
         if (node < P) {
+            // one step descends `sw` binary levels at once: the 2^sw descendants' boxes sit in
+            // the 2^(sw−1) consecutive records of the intermediate level (one scalar burst of
+            // ≤ 192 B), so a root-to-leaf walk costs ⌈levels/3⌉ dependent loads instead of levels
             ++n_inner;
-            const float4* rec = t.nodes + 3 * (size_t)node;
-            const float4 a = rec[0], b = rec[1], c = rec[2];
-            const float dl = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
-            const float dr = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
+            const int lev = 31 - __builtin_clz(node);
+            const int sw = min(kp.wide, t.levels - lev);
+            const int nk = 1 << sw, nrec = nk >> 1;
+            const float4* rec = t.nodes + 3 * ((size_t)node << (sw - 1));
+            float4 R[3 * (kWideMax / 2)];
+#pragma unroll
+            for (int k = 0; k < 3 * (kWideMax / 2); ++k) R[k] = rec[min(k, 3 * nrec - 1)];
             const float bs = bnd * kBoxSlack;
-            const bool nl = dl <= bs, nr = dr <= bs;
-            const unsigned long long ml = __ballot(nl), mr = __ballot(nr);
-            if (ml && mr) {
-                const unsigned long long pl = __ballot((nl || nr) && dl <= dr);
-                const bool lf = 2 * __popcll(pl) >= __popcll(ml | mr);
-                if (lane == 0) {
-                    snode[wv][sp] = lf ? 2 * node + 1 : 2 * node;
-                    sbox[wv][sp][0] = lf ? make_float4(b.z, b.w, c.x, c.y) : make_float4(a.x, a.y, a.z, a.w);
-                    sbox[wv][sp][1] = lf ? make_float4(c.z, c.w, 0.f, 0.f) : make_float4(b.x, b.y, 0.f, 0.f);
+            unsigned long long m[kWideMax];
+            int best = -1;
+            float bd = kInfF;
+#pragma unroll
+            for (int k = 0; k < kWideMax; ++k) {
+                const float4 a = R[3 * (k >> 1)], b = R[3 * (k >> 1) + 1], c = R[3 * (k >> 1) + 2];
+                const float d = (k & 1) ? box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w) : box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+                const bool w = k < nk && d <= bs;
+                m[k] = __ballot(w);
+                if (w && d < bd) { bd = d; best = k; }
+            }
+            // descend into the child most lanes find nearest; stack the other wanted ones so that
+            // they pop in Morton (index) order
+            int cstar = -1, vbest = 0;
+#pragma unroll
+            for (int k = 0; k < kWideMax; ++k) {
+                const int v = __popcll(__ballot(best == k));
+                if (m[k] && (cstar < 0 || v > vbest)) { cstar = k; vbest = v; }
+            }
+            if (cstar >= 0) {
+#pragma unroll
+                for (int k = kWideMax - 1; k >= 0; --k) {
+                    if (m[k] && k != cstar) {
+                        if (lane == 0) {
+                            const float4 a = R[3 * (k >> 1)], b = R[3 * (k >> 1) + 1], c = R[3 * (k >> 1) + 2];
+                            snode[wv][sp] = (node << sw) + k;
+                            sbox[wv][sp][0] = (k & 1) ? make_float4(b.z, b.w, c.x, c.y) : make_float4(a.x, a.y, a.z, a.w);
+                            sbox[wv][sp][1] = (k & 1) ? make_float4(c.z, c.w, 0.f, 0.f) : make_float4(b.x, b.y, 0.f, 0.f);
+                        }
+                        ++sp;
+                    }
                 }
-                ++sp;
-                node = lf ? 2 * node : 2 * node + 1;
-                em = lf ? ml : mr;
+                em = m[cstar];
+                node = (node << sw) + cstar;
                 continue;
             }
-            if (ml) { node = 2 * node; em = ml; continue; }
-            if (mr) { node = 2 * node + 1; em = mr; continue; }
         } else {
             ++n_leaf;
             const int leaf = node - P;
