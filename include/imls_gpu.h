@@ -101,8 +101,9 @@ typedef struct imls_params {
     double r_proj;                    /* IMLS.use_projected_distance.r_proj */
     double angle_diff_threshold;      /* IMLS.normal_angle_constraint.angle_diff_threshold (deg) */
     int32_t search_number;            /* IMLS."IMLS function".search_number (K, ≤ 32) */
-    int32_t use_tensor_voting;        /* IMLS.use_tensor_voting.enabled (not on the GPU path) */
-    int32_t tensor_k;
+    int32_t use_tensor_voting;        /* IMLS.use_tensor_voting.enabled (with get_normals=false:
+                                         VoteForAny normals; needs imls_set_target_tensors) */
+    int32_t tensor_k;                 /* IMLS.use_tensor_voting.k (≤ 64 on the GPU path) */
     int32_t recompute_normal_count_mode; /* SURVEY Q1 switch: 0 = reference (libnabo knn() return
                                             value is a statistic → recompute path rejects), 1 = count */
     double tensor_sigma;
@@ -181,6 +182,22 @@ int imls_set_source(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n,
  * (x[], y[], z[], nx[], ny[], nz[]) — inputs stay in HBM, no PCIe in the hot loop. */
 int imls_set_target_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
 int imls_set_source_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
+
+/* Tensor voting input (use_tensor_voting): the target's per-point input tensors T — what
+ * VoteForAny's tv_input.encode(m_targetPointCloudDP, AWARE_TENSOR) produces (imls_icp.cpp:179,
+ * 535; the DP cloud of setTargetPointCloudDP, 105-144).  n records of 6 floats (xx, xy, xz, yy,
+ * yz, zz) at `stride_floats`, in the order of the last imls_set_target's points (n must equal
+ * that call's n; records of points its NaN filter dropped are ignored).  Invalidated by the next
+ * imls_set_target.  The _device form takes SoA float32[6][n] in device memory. */
+int imls_set_target_tensors(imls_ctx* ctx, const float* tensors, size_t n, size_t stride_floats);
+int imls_set_target_tensors_device(imls_ctx* ctx, const float* d_ten6, size_t n);
+/* The reference's own tensor encoding of per-point PCA features (CustomTensorVoting::
+ * myCustomFunctionWithEigen, scan_registration.cpp:358-381), host float arithmetic:
+ * λ = |evals|, λ1 = max, λ3 = min, λ2 = Σλ − (λ1 + λ3); T = ((λ1−λ2)/k)·e1e1ᵀ +
+ * (λ3/k)·(e1e1ᵀ + e2e2ᵀ), or I when not λ1 ≥ λ2 ≥ λ3.  evals: [n][3] (λ1, λ2, λ3 as
+ * scan_registration.cpp:1204 stores them); evecs: [n][9], the 3×3 eigenvector matrix column-major
+ * (1205-1207: e1 = largest, e2, e3 = normal); out: [n][6] as imls_set_target_tensors reads. */
+void imls_tv_encode_pca(const float* evals, const float* evecs, size_t n, int32_t k, float* out);
 
 /* ---- matching -------------------------------------------------------------------------- */
 /* Replaces IMLSICPMatcher::ProjSourcePtToSurface (imls_icp.cpp:496-745) applied to the source

@@ -244,3 +244,67 @@ def register_frame(src6, tgt6, p: dict):
     else:
         it = p["iterations"]
     return pose, it, status, trace
+
+
+def tv_normals(tgt6: np.ndarray, ten6: np.ndarray, q3: np.ndarray, p: dict):
+    """VoteForAny (imls_icp.cpp:171-296) for the query points q3 (3, Q): the voted normal
+    ("tangents" — the eigenvector of the smallest |λ| of the summed tensor's lower triangle,
+    flipped to +z) and the non-zero flag (Eigen isZero(1e-12)).  ten6: (6, M) input tensors
+    (xx, xy, xz, yy, yz, zz) in input order.  libpointmatcher decompose semantics: unpinned."""
+    keep = np.isfinite(tgt6[:3]).all(axis=0)
+    tgt, ten = tgt6[:, keep], ten6[:, keep].astype(np.float64)
+    knn = ExactKnn(tgt[:3])
+    P = tgt[:3].T.astype(np.float64)
+    sigma, thr, k = p["tensor_sigma"], p["tensor_distance_threshold"], p["tensor_k"]
+    Q = q3.shape[1]
+    nrm = np.zeros((Q, 3))
+    found = np.zeros(Q, dtype=np.int32)
+    acc_all = np.zeros((Q, 3, 3))
+    I3 = np.eye(3)
+    for q in range(Q):
+        x = q3[:, q].astype(np.float64)
+        dk, ik = knn.query(x, k, np.inf, allow_self=False)
+        acc = np.zeros((3, 3))
+        for j in ik[ik >= 0]:
+            r = x - P[j]
+            nr = math.sqrt((r[0] * r[0] + r[1] * r[1]) + r[2] * r[2])
+            dist = nr / sigma
+            if dist <= 0.0 or dist >= thr:
+                continue
+            u = r / nr
+            w = math.exp(-(nr * nr) / sigma)
+            t = ten[:, j]
+            T = np.array([[t[0], t[1], t[2]], [t[1], t[3], t[4]], [t[2], t[4], t[5]]])
+            R = I3 - 2.0 * np.outer(u, u)
+            Rp = (I3 - 0.5 * np.outer(u, u)) @ R
+            acc += w * (R @ T @ Rp)
+        acc_all[q] = acc
+        if np.all(np.abs(acc) <= 1e-12):
+            continue
+        ev, U = np.linalg.eigh(acc, UPLO="L")      # Eigen SelfAdjointEigenSolver reads the lower triangle
+        m = int(np.argmin(np.abs(ev)))
+        n = U[:, m]
+        if n[2] < 0:
+            n = -n
+        nrm[q] = n
+        found[q] = 1
+    return nrm, found, acc_all
+
+
+def tv_encode_pca(evals: np.ndarray, evecs: np.ndarray, k: int) -> np.ndarray:
+    """CustomTensorVoting::myCustomFunctionWithEigen (scan_registration.cpp:358-381) in float32:
+    (n, 3) eigenvalues + (n, 9) column-major eigenvectors → (n, 6) tensors (xx xy xz yy yz zz)."""
+    a = np.abs(evals.astype(np.float32))
+    l1, l3 = a.max(axis=1), a.min(axis=1)
+    l2 = ((a[:, 0] + a[:, 1]) + a[:, 2]) - (l1 + l3)
+    kf = np.float32(k)
+    e1, e2 = evecs[:, 0:3].astype(np.float32), evecs[:, 3:6].astype(np.float32)
+    s1, s3 = (l1 - l2) / kf, l3 / kf
+    out = np.zeros((len(a), 6), np.float32)
+    for m, (r, c) in enumerate(((0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2))):
+        S = e1[:, r] * e1[:, c]
+        Pm = S + e2[:, r] * e2[:, c]
+        out[:, m] = s1 * S + s3 * Pm
+    ok = (l1 >= l2) & (l2 >= l3)
+    out[~ok] = np.array([1, 0, 0, 1, 0, 1], np.float32)
+    return out

@@ -641,6 +641,7 @@ struct Matcher {
     const imls_params* P;
     Cloud tgt;
     KdTree tree;
+    std::vector<double> ten;   // tensor-voting input tensors [M][6] (xx xy xz yy yz zz), filtered order
 
     // angle test shared by imls_icp.cpp:442-451, 681-692 and laser_odometry.cpp:373-384; NaN
     // angles pass (Q8).
@@ -675,6 +676,74 @@ struct Matcher {
         sym_eig(3, C, ev, U);
         double nn = std::sqrt(U[0] * U[0] + U[1] * U[1] + U[2] * U[2]);
         for (int k = 0; k < 3; ++k) nrm[k] = U[k] / nn;
+        if (nrm[2] < 0) { nrm[0] = -nrm[0]; nrm[1] = -nrm[1]; nrm[2] = -nrm[2]; }
+        return true;
+    }
+
+    // Tensor voting (IMLSICPMatcher::VoteForAny, imls_icp.cpp:171-296, used at 514-546 and
+    // 634-643) for ONE output point x (a transformed source point, in_cloudDP column).
+    //   * candidates: libnabo knn(x, k) over the target — K = tensor_k, no radius, no
+    //     ALLOW_SELF_MATCH (197), sorted (d², index); unfound slots skipped (205-208);
+    //   * vote of input j: r = x − p_j, dist = ‖r‖/σ; skipped unless 0 < dist < threshold
+    //     (212-217); w = exp(−‖r‖²/σ) (220: σ, not σ²); R = I − 2 r̂r̂ᵀ, R' = (I − ½ r̂r̂ᵀ)R,
+    //     S = w·R·T_j·R' (222-224), summed into the output tensor (226);
+    //   * non-zero test (233): Eigen isZero(1e-12) — every |coeff| ≤ 1e-12 counts as zero;
+    //   * decompose (245; libpointmatcher TensorVoting::decompose, UNPINNED — not in the
+    //     container): SelfAdjointEigenSolver on the (non-symmetric) sum reads its LOWER triangle;
+    //     eigenvalues ordered by |λ| descending, "tangents" = the eigenvector of the smallest |λ|
+    //     (the vector the reference uses as the normal, 272-278 / 541-545), flipped to +z (274).
+    // T_j = the target's input tensor as given (encode(AWARE_TENSOR), 179: see
+    // oracle_tv_encode_pca for the reference's own encoding of PCA features).  Returns false when
+    // the tensor is zero (the lookup at 637 then fails → "no normal").
+    bool tv_normal(const double x[3], double nrm[3], double acc_out[9] = nullptr) const {
+        KdTree::Heap h;
+        tree.knn(x, P->tensor_k, kInf, false, h);
+        double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        const double sigma = P->tensor_sigma;
+        for (int k = 0; k < h.n; ++k) {
+            const int32_t j = h.i[k];
+            const double r[3] = {x[0] - (double)tgt.x[j], x[1] - (double)tgt.y[j], x[2] - (double)tgt.z[j]};
+            const double nr = std::sqrt((r[0] * r[0] + r[1] * r[1]) + r[2] * r[2]);
+            const double dist = nr / sigma;
+            if (dist <= 0. || dist >= P->tensor_distance_threshold) continue;
+            const double u[3] = {r[0] / nr, r[1] / nr, r[2] / nr};
+            const double w = std::exp(-(nr * nr) / sigma);
+            const double* t6 = &ten[(size_t)j * 6];
+            const double T[9] = {t6[0], t6[1], t6[2], t6[1], t6[3], t6[4], t6[2], t6[4], t6[5]};
+            double R[9], Rp[9], RT[9];
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) R[a * 3 + b] = (a == b ? 1.0 : 0.0) - 2 * u[a] * u[b];
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) {
+                    double s = 0.0;
+                    for (int c = 0; c < 3; ++c) s += ((a == c ? 1.0 : 0.0) - 0.5 * u[a] * u[c]) * R[c * 3 + b];
+                    Rp[a * 3 + b] = s;
+                }
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) {
+                    double s = 0.0;
+                    for (int c = 0; c < 3; ++c) s += R[a * 3 + c] * T[c * 3 + b];
+                    RT[a * 3 + b] = s;
+                }
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) {
+                    double s = 0.0;
+                    for (int c = 0; c < 3; ++c) s += RT[a * 3 + c] * Rp[c * 3 + b];
+                    acc[a * 3 + b] += w * s;
+                }
+        }
+        if (acc_out) std::memcpy(acc_out, acc, sizeof(acc));
+        bool zero = true;
+        for (double v : acc) zero = zero && std::abs(v) <= 1e-12;
+        if (zero) return false;
+        double A[9];
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) A[a * 3 + b] = a >= b ? acc[a * 3 + b] : acc[b * 3 + a];
+        double ev[3], U[9];
+        sym_eig(3, A, ev, U);
+        int m = 0;
+        for (int c = 1; c < 3; ++c) if (std::abs(ev[c]) < std::abs(ev[m])) m = c;
+        for (int k = 0; k < 3; ++k) nrm[k] = U[m * 3 + k];
         if (nrm[2] < 0) { nrm[0] = -nrm[0]; nrm[1] = -nrm[1]; nrm[2] = -nrm[2]; }
         return true;
     }
@@ -773,7 +842,9 @@ struct Matcher {
         if (min_dist > P->h * P->h) return IMLS_REJ_TOO_FAR;
         double nn[3];
         if (P->get_normals) { nn[0] = tgt.nx[best]; nn[1] = tgt.ny[best]; nn[2] = tgt.nz[best]; }
-        else if (P->use_tensor_voting) return IMLS_REJ_NO_NORMAL;   // TV not restated (out of scope)
+        else if (P->use_tensor_voting) {   // imls_icp.cpp:634-643: the query's own voted normal
+            if (ten.empty() || !tv_normal(x, nn)) return IMLS_REJ_NO_NORMAL;
+        }
         else { double pt[3] = {tgt.x[best], tgt.y[best], tgt.z[best]}; recompute_normal(pt, nn); }
         if (!finite3(nn[0], nn[1], nn[2])) return IMLS_REJ_INVALID_NORMAL;
         if (P->normal_angle_constraint && angle_reject(ns, nn)) return IMLS_REJ_NORMAL_CONSTRAINT;
@@ -878,6 +949,17 @@ bool solve_dispatch(int method, const double* s, const double* d, const double* 
 
 }  // namespace
 
+// Tensor-voting input tensors [6][n] (SoA, input order) → [M][6] in the filtered order.
+std::vector<double> load_tensors(const float* tgt6, size_t n, const float* ten6) {
+    std::vector<double> t;
+    if (!ten6) return t;
+    for (size_t i = 0; i < n; ++i) {
+        if (!(std::isfinite(tgt6[i]) && std::isfinite(tgt6[n + i]) && std::isfinite(tgt6[2 * n + i]))) continue;
+        for (int k = 0; k < 6; ++k) t.push_back(ten6[k * n + i]);
+    }
+    return t;
+}
+
 // ==========================================================================================
 // C ABI
 // ==========================================================================================
@@ -904,9 +986,16 @@ int oracle_knn(const float* tgt6, size_t M, const float* q3, size_t Q, int K, do
 int oracle_project(const float* src6, size_t N, const float* tgt6, size_t M, const double pose[16],
                    const imls_params* p, float* x_out, float* y_out, float* n_out, uint32_t* src_index_out,
                    size_t* n_valid, uint64_t reject[IMLS_NUM_REJ]) {
+    return oracle_project_tv(src6, N, tgt6, M, nullptr, pose, p, x_out, y_out, n_out, src_index_out, n_valid, reject);
+}
+
+int oracle_project_tv(const float* src6, size_t N, const float* tgt6, size_t M, const float* ten6, const double pose[16],
+                      const imls_params* p, float* x_out, float* y_out, float* n_out, uint32_t* src_index_out,
+                      size_t* n_valid, uint64_t reject[IMLS_NUM_REJ]) {
     if (!p || p->search_number <= 0 || p->search_number > 64) return IMLS_ERR_ARG;
+    if (p->use_tensor_voting && (p->tensor_k <= 0 || p->tensor_k > 64)) return IMLS_ERR_ARG;
     Cloud src = load_filtered(src6, N);
-    Matcher m{p, load_filtered(tgt6, M), {}};
+    Matcher m{p, load_filtered(tgt6, M), {}, load_tensors(tgt6, M, ten6)};
     m.tree.build(m.tgt);
     Corr c;
     uint64_t rej[6];
@@ -933,10 +1022,19 @@ int oracle_solve(int32_t method, const double* s, const double* d, const double*
 int oracle_register_frame(const float* src6, size_t N, const float* tgt6, size_t M, const imls_params* p,
                           double pose_out[16], int* iters_run, int* status, imls_iter_trace* trace,
                           int corr_iter, float* corr, size_t* corr_n, double* seconds_index, double* seconds_total) {
+    return oracle_register_frame_tv(src6, N, tgt6, M, nullptr, p, pose_out, iters_run, status, trace, corr_iter, corr,
+                                    corr_n, seconds_index, seconds_total);
+}
+
+int oracle_register_frame_tv(const float* src6, size_t N, const float* tgt6, size_t M, const float* ten6,
+                             const imls_params* p, double pose_out[16], int* iters_run, int* status,
+                             imls_iter_trace* trace, int corr_iter, float* corr, size_t* corr_n,
+                             double* seconds_index, double* seconds_total) {
     if (!p || p->search_number <= 0 || p->search_number > 64) return IMLS_ERR_ARG;
+    if (p->use_tensor_voting && (p->tensor_k <= 0 || p->tensor_k > 64)) return IMLS_ERR_ARG;
     auto t0 = std::chrono::steady_clock::now();
     Cloud src = load_filtered(src6, N);
-    Matcher m{p, load_filtered(tgt6, M), {}};
+    Matcher m{p, load_filtered(tgt6, M), {}, load_tensors(tgt6, M, ten6)};
     m.tree.build(m.tgt);
     auto t1 = std::chrono::steady_clock::now();
     int32_t rs[34];
@@ -990,6 +1088,20 @@ int oracle_register_frame(const float* src6, size_t N, const float* tgt6, size_t
     std::memcpy(pose_out, pose.m, sizeof(pose.m));
     if (seconds_index) *seconds_index = std::chrono::duration<double>(t1 - t0).count();
     if (seconds_total) *seconds_total = std::chrono::duration<double>(t2 - t0).count();
+    return IMLS_OK;
+}
+
+int oracle_tv_normals(const float* tgt6, size_t M, const float* ten6, const float* q3, size_t Q, const imls_params* p,
+                      double* nrm, int32_t* found, double* tensors) {
+    if (!p || !ten6 || p->tensor_k <= 0 || p->tensor_k > 64) return IMLS_ERR_ARG;
+    Matcher m{p, load_filtered(tgt6, M), {}, load_tensors(tgt6, M, ten6)};
+    m.tree.build(m.tgt);
+    for (size_t q = 0; q < Q; ++q) {
+        const double x[3] = {q3[q], q3[Q + q], q3[2 * Q + q]};
+        double n[3] = {0, 0, 0};
+        found[q] = m.tv_normal(x, n, tensors ? tensors + 9 * q : nullptr) ? 1 : 0;
+        for (int k = 0; k < 3; ++k) nrm[3 * q + k] = n[k];
+    }
     return IMLS_OK;
 }
 

@@ -53,6 +53,23 @@ int oracle_register_frame(const float* src6, size_t N, const float* tgt6, size_t
                           imls_iter_trace* trace, int corr_iter, float* corr, size_t* corr_n,
                           double* seconds_index, double* seconds_total);
 
+/* Tensor voting (VoteForAny, imls_icp.cpp:171-296): per query point, the voted normal ("tangents",
+ * flipped to +z) and whether its tensor is non-zero.  ten6: the target's input tensors, SoA
+ * float32[6][M] (xx, xy, xz, yy, yz, zz), input order.  tensors (nullable): the summed tensors,
+ * row-major [Q][9].  libpointmatcher decompose semantics are UNPINNED (see imls_oracle.cpp). */
+int oracle_tv_normals(const float* tgt6, size_t M, const float* ten6, const float* q3, size_t Q,
+                      const imls_params* p, double* nrm, int32_t* found, double* tensors);
+/* oracle_project / oracle_register_frame with the target's tensors (use_tensor_voting). */
+int oracle_project_tv(const float* src6, size_t N, const float* tgt6, size_t M, const float* ten6,
+                      const double pose[16], const imls_params* p, float* x_out, float* y_out,
+                      float* n_out, uint32_t* src_index_out, size_t* n_valid,
+                      uint64_t reject[IMLS_NUM_REJ]);
+int oracle_register_frame_tv(const float* src6, size_t N, const float* tgt6, size_t M,
+                             const float* ten6, const imls_params* p, double pose_out[16],
+                             int* iters_run, int* status, imls_iter_trace* trace, int corr_iter,
+                             float* corr, size_t* corr_n, double* seconds_index,
+                             double* seconds_total);
+
 /* glibc rand() restated (common.cpp:49 consumes it).  Fills 34-word state for srand(seed). */
 void oracle_rand_seed(int32_t* state, uint32_t seed);
 int32_t oracle_rand_next(int32_t* state);

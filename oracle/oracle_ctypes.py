@@ -40,6 +40,10 @@ def lib():
         L.oracle_solve.argtypes = [C.c_int32, VP, VP, VP, VP, SZ, P(abi.ImlsParams), VP, VP, P(C.c_int)]
         L.oracle_register_frame.argtypes = [VP, SZ, VP, SZ, P(abi.ImlsParams), VP, P(C.c_int), P(C.c_int), VP,
                                             C.c_int, VP, P(SZ), P(C.c_double), P(C.c_double)]
+        L.oracle_project_tv.argtypes = [VP, SZ, VP, SZ, VP, VP, P(abi.ImlsParams), VP, VP, VP, VP, P(SZ), VP]
+        L.oracle_register_frame_tv.argtypes = [VP, SZ, VP, SZ, VP, P(abi.ImlsParams), VP, P(C.c_int), P(C.c_int), VP,
+                                               C.c_int, VP, P(SZ), P(C.c_double), P(C.c_double)]
+        L.oracle_tv_normals.argtypes = [VP, SZ, VP, VP, SZ, P(abi.ImlsParams), VP, VP, VP]
         L.oracle_rand_seed.argtypes = [VP, C.c_uint32]
         L.oracle_rand_next.argtypes = [VP]
         L.oracle_rand_next.restype = C.c_int32
@@ -70,14 +74,23 @@ def knn(tgt6, q3, K, r, allow_self):
     return d2, idx
 
 
-def project(src6, tgt6, pose, params):
+def _ten6(t, M):
+    if t is None:
+        return None
+    t = np.ascontiguousarray(t, dtype=np.float32)
+    assert t.shape == (6, M)
+    return t
+
+
+def project(src6, tgt6, pose, params, tensors=None):
     src6, tgt6 = _soa6(src6), _soa6(tgt6)
+    ten = _ten6(tensors, tgt6.shape[1])
     N = src6.shape[1]
     pose = np.ascontiguousarray(pose, dtype=np.float64).reshape(16)
     x = np.zeros((N, 3), np.float32); y = np.zeros((N, 3), np.float32); n = np.zeros((N, 3), np.float32)
     idx = np.zeros(N, np.uint32); rej = np.zeros(6, np.uint64); nv = C.c_size_t()
-    rc = lib().oracle_project(_ptr(src6), N, _ptr(tgt6), tgt6.shape[1], _ptr(pose), C.byref(params),
-                              _ptr(x), _ptr(y), _ptr(n), _ptr(idx), C.byref(nv), _ptr(rej))
+    rc = lib().oracle_project_tv(_ptr(src6), N, _ptr(tgt6), tgt6.shape[1], None if ten is None else _ptr(ten),
+                                 _ptr(pose), C.byref(params), _ptr(x), _ptr(y), _ptr(n), _ptr(idx), C.byref(nv), _ptr(rej))
     assert rc == 0
     k = nv.value
     return x[:k], y[:k], n[:k], idx[:k], rej
@@ -93,8 +106,22 @@ def solve(method, s, d, n, params, weights=None, rand_state=None):
     return bool(ok.value), D.reshape(4, 4)
 
 
-def register_frame(src6, tgt6, params, corr_iter=-1):
+def tv_normals(tgt6, tensors, q3, params):
+    """VoteForAny per query: (normals (Q,3) double, found (Q,) int32, summed tensors (Q,3,3))."""
+    tgt6 = _soa6(tgt6)
+    ten = _ten6(tensors, tgt6.shape[1])
+    q3 = np.ascontiguousarray(q3, dtype=np.float32)
+    Q = q3.shape[1]
+    nrm = np.zeros((Q, 3)); found = np.zeros(Q, np.int32); acc = np.zeros((Q, 9))
+    rc = lib().oracle_tv_normals(_ptr(tgt6), tgt6.shape[1], _ptr(ten), _ptr(q3), Q, C.byref(params), _ptr(nrm),
+                                 _ptr(found), _ptr(acc))
+    assert rc == 0
+    return nrm, found, acc.reshape(Q, 3, 3)
+
+
+def register_frame(src6, tgt6, params, corr_iter=-1, tensors=None):
     src6, tgt6 = _soa6(src6), _soa6(tgt6)
+    ten = _ten6(tensors, tgt6.shape[1])
     abi = _abi()
     it = params.iterations
     trace = (abi.ImlsIterTrace * max(it, 1))()
@@ -102,7 +129,8 @@ def register_frame(src6, tgt6, params, corr_iter=-1):
     N = src6.shape[1]
     corr = np.zeros((N, 9), np.float32) if corr_iter >= 0 else None
     cn = C.c_size_t(); ti = C.c_double(); tt = C.c_double()
-    rc = lib().oracle_register_frame(_ptr(src6), N, _ptr(tgt6), tgt6.shape[1], C.byref(params), _ptr(pose),
+    rc = lib().oracle_register_frame_tv(_ptr(src6), N, _ptr(tgt6), tgt6.shape[1], None if ten is None else _ptr(ten),
+                                        C.byref(params), _ptr(pose),
                                      C.byref(iters), C.byref(status), trace, corr_iter,
                                      None if corr is None else _ptr(corr), C.byref(cn), C.byref(ti), C.byref(tt))
     assert rc == 0

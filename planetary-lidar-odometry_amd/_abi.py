@@ -104,6 +104,9 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_set_source": (C.c_int, [VP, VP, VP, SZ, SZ, P(SZ), VP]),
         "imls_set_target_device": (C.c_int, [VP, VP, SZ, P(SZ)]),
         "imls_set_source_device": (C.c_int, [VP, VP, SZ, P(SZ)]),
+        "imls_set_target_tensors": (C.c_int, [VP, VP, SZ, SZ]),
+        "imls_set_target_tensors_device": (C.c_int, [VP, VP, SZ]),
+        "imls_tv_encode_pca": (None, [VP, VP, SZ, C.c_int32, VP]),
         "imls_project": (C.c_int, [VP, VP, VP, VP, VP, VP, P(SZ), VP]),
         "imls_solve": (C.c_int, [VP, VP, P(C.c_int)]),
         "imls_solve_correspondences": (C.c_int, [VP, C.c_int32, VP, VP, VP, VP, SZ, VP, P(C.c_int)]),
@@ -126,7 +129,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
 ABI_SYMBOLS = (
     "imls_abi_version", "imls_default_params", "imls_create", "imls_destroy", "imls_set_params",
     "imls_last_error", "imls_set_stream", "imls_synchronize", "imls_set_target", "imls_set_source",
-    "imls_set_target_device", "imls_set_source_device", "imls_project", "imls_solve",
+    "imls_set_target_device", "imls_set_source_device", "imls_set_target_tensors",
+    "imls_set_target_tensors_device", "imls_tv_encode_pca", "imls_project", "imls_solve",
     "imls_solve_correspondences", "imls_register_frame", "imls_register_frame_async",
     "imls_register_frame_result", "imls_enable_timing", "imls_kernel_timing", "imls_reset_timing",
     "imls_index_stats", "imls_traversal_stats",

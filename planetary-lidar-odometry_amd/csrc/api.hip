@@ -36,6 +36,11 @@ struct imls_ctx {
     int rnr_k = -1;
     double rnr_r = -1.0;
     DevBuf prevnn;                        // per-query neighbour lists carried between ICP iterations
+    DevBuf tkept;                         // target: filtered index → input index (tensor upload)
+    DevBuf mten, upload_ten;              // tensor voting: input tensors (Morton order) + upload staging
+    DevBuf tvn;                           // tensor voting: per-source voted normal + found flag (double4)
+    size_t n_target_in = 0;               // input size of the last set_target (tensor arrays match it)
+    bool has_tensors = false;
     int lane_mode = 0;
     int temporal_seed = 1;
     int N = 0;
@@ -126,6 +131,12 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_WIDE")) k.wide = std::max(1, std::min(3, std::atoi(w)));
     k.verlet = 1;
     if (const char* w = std::getenv("IMLS_VERLET")) k.verlet = std::atoi(w);
+    // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
+    // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)
+    k.tv = (p.use_tensor_voting && !p.get_normals && p.matching_method == IMLS_MATCH_IMLS) ? 1 : 0;
+    k.tv_k = p.tensor_k;
+    k.tv_sigma = p.tensor_sigma;
+    k.tv_thr = p.tensor_distance_threshold;
     return k;
 }
 
@@ -134,7 +145,10 @@ int check_params(imls_ctx* c, const imls_params* p) {
     if (p->search_number < 1 || p->search_number > 32) return fail(c, IMLS_ERR_UNSUPPORTED, "search_number must be in [1, 32]");
     if (p->matching_method != IMLS_MATCH_IMLS && p->matching_method != IMLS_MATCH_PLANE_ICP)
         return fail(c, IMLS_ERR_ARG, "matching_method must be IMLS or plane_ICP");
-    if (p->use_tensor_voting && !p->get_normals) return fail(c, IMLS_ERR_UNSUPPORTED, "tensor voting normals are not on the GPU path");
+    if (p->use_tensor_voting && !p->get_normals) {
+        if (p->tensor_k < 1 || p->tensor_k > kTvMaxK) return fail(c, IMLS_ERR_UNSUPPORTED, "tensor_voting.k must be in [1, 64]");
+        if (!(p->tensor_sigma > 0)) return fail(c, IMLS_ERR_ARG, "tensor_voting.sigma must be > 0");
+    }
     if (!p->get_normals && p->recompute_normal_count_mode && (p->search_number_normal < 1 || p->search_number_normal > 32))
         return fail(c, IMLS_ERR_UNSUPPORTED, "search_number_normal must be in [1, 32]");
     if (p->solve_method != IMLS_SOLVE_LS && p->solve_method != IMLS_SOLVE_WEIGHTED_LS && p->solve_method != IMLS_SOLVE_RANSAC)
@@ -159,6 +173,7 @@ int ensure_solve(imls_ctx* c, int N) {
     if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, n * 4 + 256))
         return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
     if (!grow(c->prevnn, prevnn_bytes((int)n))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
+    if (!grow(c->tvn, n * sizeof(double4))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tvn)");
     const int pb = std::max(project_blocks((int)n), solve_blocks((int)n)) + 1;
     size_t bytes = 0;
     auto add = [&](size_t b) { size_t o = bytes; bytes += (b + 255) / 256 * 256; return o; };
@@ -278,6 +293,8 @@ TreeView tree_view(imls_ctx* c) {
     t.L = c->B > 0 ? (c->M + c->B - 1) / c->B : 0;
     t.lkeys = (const unsigned long long*)c->lkeys.p;
     t.qparams = c->lkeys.p ? (const float*)((const unsigned long long*)c->lkeys.p + t.L) : nullptr;
+    t.mten = c->has_tensors ? (const float4*)c->mten.p : nullptr;
+    t.tvn = (const double4*)c->tvn.p;
     return t;
 }
 
@@ -350,12 +367,15 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
 }
 
 int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
+    if (!grow(c->tkept, n * 4 + 16)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (kept)");
+    c->has_tensors = false;
     int slot;
     timed_begin(c, 1, slot);
     int rc = build_target_index(c->stream, d_soa6, n, c->B, c->lkeys, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch,
-                                c->treescratch, c->permbuf, &c->M, &c->Pl, &c->levels, c->err);
+                                c->treescratch, c->permbuf, &c->M, &c->Pl, &c->levels, c->err, (unsigned*)c->tkept.p);
     timed_end(c, 1, slot);
     if (rc) return rc;
+    c->n_target_in = n;
     c->has_target = c->M > 0;
     c->rnr_valid = false;
     c->has_corr = false;
@@ -373,6 +393,22 @@ int do_set_source(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept, ui
     c->has_corr = false;
     if (n_kept) *n_kept = (size_t)c->N;
     return ensure_solve(c, c->N);
+}
+
+int do_set_tensors(imls_ctx* c, const float* d_ten6, size_t n) {
+    if (!c->has_target) return fail(c, IMLS_ERR_STATE, "set_target first");
+    if (n != c->n_target_in) return fail(c, IMLS_ERR_ARG, "tensor count must equal the last set_target's point count");
+    if (!grow(c->mten, (size_t)std::max(c->M, 1) * 32)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tensors)");
+    launch_tensor_gather(c->stream, d_ten6, n, (const unsigned*)c->tkept.p, (const float4*)c->mpt.p, c->M, (float4*)c->mten.p);
+    if (hipGetLastError() != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "tensor gather launch failed");
+    c->has_tensors = true;
+    return IMLS_OK;
+}
+
+// tensor voting needs the target's tensors
+int check_tv_ready(imls_ctx* c) {
+    if (c->kp.tv && !c->has_tensors) return fail(c, IMLS_ERR_STATE, "use_tensor_voting: imls_set_target_tensors first");
+    return IMLS_OK;
 }
 
 int check_device(imls_ctx* c) {
@@ -465,7 +501,7 @@ void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
+    DevBuf* bufs[] = {&c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
                       &c->upload_t, &c->spt, &c->snr, &c->sscratch,
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
@@ -512,6 +548,51 @@ int imls_set_target_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n
     return do_set_target(c, d_soa6, n, n_kept);
 }
 
+int imls_set_target_tensors(imls_ctx* c, const float* tens, size_t n, size_t stride) {
+    if (!c || !tens || n == 0 || stride < 6) return fail(c, IMLS_ERR_ARG, "bad tensor pointer/size/stride");
+    if (int rc = check_device(c)) return rc;
+    std::vector<float> h(6 * n);
+    for (size_t i = 0; i < n; ++i)
+        for (int k = 0; k < 6; ++k) h[(size_t)k * n + i] = tens[i * stride + k];
+    if (!grow(c->upload_ten, h.size() * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (upload)");
+    if (hipMemcpyAsync(c->upload_ten.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "tensor upload failed");
+    int rc = do_set_tensors(c, (const float*)c->upload_ten.p, n);
+    if (rc) return rc;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? IMLS_OK : fail(c, IMLS_ERR_DEVICE, "tensor upload failed");
+}
+
+int imls_set_target_tensors_device(imls_ctx* c, const float* d_ten6, size_t n) {
+    if (!c || !d_ten6) return IMLS_ERR_ARG;
+    if (int rc = check_device(c)) return rc;
+    return do_set_tensors(c, d_ten6, n);
+}
+
+void imls_tv_encode_pca(const float* evals, const float* evecs, size_t n, int32_t k, float* out) {
+    // CustomTensorVoting::myCustomFunctionWithEigen (scan_registration.cpp:358-381), float arithmetic
+    const float kf = (float)k;
+    for (size_t i = 0; i < n; ++i) {
+        const float a0 = std::fabs(evals[3 * i]), a1 = std::fabs(evals[3 * i + 1]), a2 = std::fabs(evals[3 * i + 2]);
+        const float l1 = std::max(a0, std::max(a1, a2));
+        const float l3 = std::min(a0, std::min(a1, a2));
+        const float l2 = ((a0 + a1) + a2) - (l1 + l3);
+        const float* e = evecs + 9 * i;           // columns: e1 = e[0..2] (stick tail), e2 = e[3..5] (plate tail)
+        float T[6];
+        if (l1 >= l2 && l2 >= l3) {
+            const float s1 = (l1 - l2) / kf, s3 = l3 / kf;
+            const int rr[6] = {0, 0, 0, 1, 1, 2}, cc[6] = {0, 1, 2, 1, 2, 2};
+            for (int m = 0; m < 6; ++m) {
+                const float S = e[rr[m]] * e[cc[m]];
+                const float Pm = S + e[3 + rr[m]] * e[3 + cc[m]];
+                T[m] = s1 * S + s3 * Pm;
+            }
+        } else {
+            T[0] = 1.f; T[1] = 0.f; T[2] = 0.f; T[3] = 1.f; T[4] = 0.f; T[5] = 1.f;   // unit ball (377-380)
+        }
+        for (int m = 0; m < 6; ++m) out[6 * i + m] = T[m];
+    }
+}
+
 int imls_set_source(imls_ctx* c, const float* xyz, const float* nrm, size_t n, size_t stride, size_t* n_kept,
                     uint32_t* kept_index) {
     if (!c) return IMLS_ERR_ARG;
@@ -532,6 +613,7 @@ int imls_project(imls_ctx* c, const double pose[16], float* x_out, float* y_out,
     if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
     if (int rc = check_device(c)) return rc;
     if (int rc = ensure_solve(c, c->N)) return rc;
+    if (int rc = check_tv_ready(c)) return rc;
     if (int rc = ensure_map_normals(c)) return rc;
     if (!grow(c->pose_tmp, 32 * 8) || !grow(c->stats, 128)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");
     double* dpose = (double*)c->pose_tmp.p;
@@ -641,6 +723,7 @@ int imls_register_frame_async(imls_ctx* c) {
     if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
     if (int rc = check_device(c)) return rc;
     if (int rc = ensure_solve(c, c->N)) return rc;
+    if (int rc = check_tv_ready(c)) return rc;
     const int iters = c->P.iterations;
     if (int rc = ensure_trace(c, iters)) return rc;
     if (!grow(c->stats, 128)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");

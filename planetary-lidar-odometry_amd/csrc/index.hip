@@ -257,10 +257,10 @@ int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf
 
 int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket, DevBuf& lkeys, DevBuf& tpt, DevBuf& tnr,
                        DevBuf& mpt, DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* M_out,
-                       int* P_out, int* levels_out, std::string& err) {
+                       int* P_out, int* levels_out, std::string& err, unsigned* kept) {
     if (n_in == 0 || n_in > (size_t)0x7fffffff) { err = "target size out of range"; return IMLS_ERR_ARG; }
     int M = 0;
-    int rc = filter_compact(s, d_soa6, n_in, tpt, tnr, scratch, &M, nullptr, err);
+    int rc = filter_compact(s, d_soa6, n_in, tpt, tnr, scratch, &M, kept, err);
     if (rc) return rc;
     *M_out = M;
     if (M == 0) { *P_out = 0; *levels_out = 0; return IMLS_OK; }

@@ -57,7 +57,11 @@ struct KParams {
     int wide;                 // packet traversal: binary levels descended per step (1..3)
     int verlet;               // reuse a query's list without traversal while its certification holds
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
+    int tv;                   // tensor-voting normals (use_tensor_voting && !get_normals, IMLS matcher)
+    int tv_k;                 // use_tensor_voting.k (≤ kTvMaxK)
+    double tv_sigma, tv_thr;  // use_tensor_voting.sigma, .distance_threshold
 };
+constexpr int kTvMaxK = 64;    // tensor-voting kNN size handled on device
 
 struct TreeView {
     const float4* mpt;        // map points in Morton order, w = original index (bits)
@@ -70,6 +74,9 @@ struct TreeView {
     const unsigned long long* lkeys;   // [L] Morton key of each leaf's first point (seed search)
     const float* qparams;              // [4] Morton quantisation: bbox lo xyz, scale
     int L;                             // leaves holding points
+    const float4* mten;                // TV: input tensors in Morton order, 2 float4 per point
+                                       //     (xx, xy, xz, yy | yz, zz, 0, 0), or null
+    const double4* tvn;                // TV: per source index, the voted normal + found flag (w)
 };
 
 // 48-bit Morton code with isotropic quantisation (one scale for all axes keeps buckets compact);
@@ -113,10 +120,11 @@ struct SolveState {
 };
 
 // index.hip
+// kept (nullable, n_in entries): filtered index → input index
 int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket, DevBuf& lkeys,
                        DevBuf& tpt, DevBuf& tnr, DevBuf& mpt, DevBuf& nodes, DevBuf& scratch,
                        DevBuf& treescratch, DevBuf& permbuf, int* M_out, int* P_out, int* levels_out,
-                       std::string& err);
+                       std::string& err, unsigned* kept = nullptr);
 // also computes qperm: the source in Morton order (query order of the wave kernel)
 int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, DevBuf& snr,
                 DevBuf& scratch, DevBuf& qperm, int* N_out, std::vector<uint32_t>* kept, std::string& err);
@@ -151,6 +159,13 @@ int solve_blocks(int N);
 
 // normals.hip — map normals recomputed from the map (get_normals=false, count mode), Morton order
 int launch_map_normals(hipStream_t s, const TreeView& t, int K, double r_normal, float4* out);
+
+// tv.hip — tensor voting (VoteForAny, imls_icp.cpp:171-296): the voted normal of every source point
+// at the current pose → tvn[N]; input tensors gathered to Morton order once per target
+void launch_tv_vote(hipStream_t s, const TreeView& t, const float4* spt, int N, const double* pose, const int* done,
+                    const KParams& kp, double4* tvn);
+void launch_tensor_gather(hipStream_t s, const float* ten6_in, size_t n_in, const unsigned* kept, const float4* mpt, int M,
+                          float4* mten);
 
 // ransac.hip — RANSAC (+ final LS / weighted LS / DRPM) and the solve-method dispatcher
 constexpr int kHypMax = 4096;          // hypotheses per chunk (chunks grow 16, 64, 256, 1024, 4096)

@@ -32,6 +32,7 @@
 #include <cfloat>
 
 #include "internal.h"
+#include "geom.h"
 
 namespace imlsgpu {
 namespace {
@@ -50,22 +51,6 @@ constexpr double kCertSlack = 1.0 + 4e-7;
 
 __device__ __forceinline__ bool lessp(double da, int ia, double db, int ib) {
     return da < db || (da == db && ia < ib);
-}
-
-__device__ __forceinline__ float box_d2(const float q[3], float lx, float ly, float lz, float hx, float hy, float hz) {
-    const float vx = fmaxf(fmaxf(lx - q[0], q[0] - hx), 0.f);
-    const float vy = fmaxf(fmaxf(ly - q[1], q[1] - hy), 0.f);
-    const float vz = fmaxf(fmaxf(lz - q[2], q[2] - hz), 0.f);
-    return __builtin_fmaf(vx, vx, __builtin_fmaf(vy, vy, vz * vz));
-}
-
-// exact libnabo metric on float storage
-__device__ __forceinline__ double exact_d2(const double xd[3], float px, float py, float pz) {
-    const double dx = xd[0] - (double)px, dy = xd[1] - (double)py, dz = xd[2] - (double)pz;
-    double d2 = dx * dx;
-    d2 = d2 + dy * dy;
-    d2 = d2 + dz * dz;
-    return d2;
 }
 
 // imls_icp.cpp:442-451 / 681-692: acos(ns·n/(|ns||n|))·180/π > threshold; NaN passes (Q8).
@@ -104,35 +89,6 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// x = float(rPose·[p;1]) and the (optionally rotated) source normal (laser_odometry.cpp:527-549)
-__device__ __forceinline__ void transform_query(const double* __restrict__ pose, float4 p, float4 nsv, int rot_normal,
-                                                float xf[3], double ns[3]) {
-    double T[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = pose[k];
-    const double pd[3] = {p.x, p.y, p.z};
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        double v = T[r * 4 + 0] * pd[0];
-        v = v + T[r * 4 + 1] * pd[1];
-        v = v + T[r * 4 + 2] * pd[2];
-        v = v + T[r * 4 + 3] * 1.0;
-        xf[r] = (float)v;
-    }
-    if (rot_normal) {
-        const double nd[3] = {nsv.x, nsv.y, nsv.z};
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            double v = T[r * 4 + 0] * nd[0];
-            v = v + T[r * 4 + 1] * nd[1];
-            v = v + T[r * 4 + 2] * nd[2];
-            ns[r] = (double)(float)v;
-        }
-    } else {
-        ns[0] = nsv.x; ns[1] = nsv.y; ns[2] = nsv.z;
-    }
-}
-
 // Gates + ImplicitMLSFunction + projection for one query given its exact neighbour list
 // L = (ld[j], lpos[j]) for j ∈ [first, first+cnt) sorted by (d², index) and its NN-1 (d1, p1);
 // positions are Morton positions (mpt/mnr: the neighbours of a query share cache lines).
@@ -140,12 +96,20 @@ __device__ __forceinline__ void transform_query(const double* __restrict__ pose,
 template <int CAP>
 __device__ int finish_query(const float xf[3], const double ns[3], const double (&ld)[CAP], const int (&lpos)[CAP],
                             int first, int cnt, double d1, int p1, const TreeView& t, const KParams& kp, float yf[3],
-                            float nf[3], int& kq) {
+                            float nf[3], int& kq, int qi) {
     if (p1 < 0) return IMLS_REJ_TOO_FAR;                      // InvalidIndex → counted as too far (Q18)
     if (d1 > kp.h2) return IMLS_REJ_TOO_FAR;                  // imls_icp.cpp:620
-    if (!kp.get_normals) return IMLS_REJ_INVALID_NORMAL;      // recompute branch under libnabo semantics (Q1)
-    const float4 n4 = t.mnr[p1];
-    const double nn[3] = {n4.x, n4.y, n4.z};
+    double nn[3];
+    if (kp.tv) {
+        // imls_icp.cpp:634-643: the query's own voted normal (tv.hip); a zero tensor has none
+        const double4 v = t.tvn[qi];
+        if (v.w == 0.0) return IMLS_REJ_NO_NORMAL;
+        nn[0] = v.x; nn[1] = v.y; nn[2] = v.z;
+    } else {
+        if (!kp.get_normals) return IMLS_REJ_INVALID_NORMAL;  // recompute branch under libnabo semantics (Q1)
+        const float4 n4 = t.mnr[p1];
+        nn[0] = n4.x; nn[1] = n4.y; nn[2] = n4.z;
+    }
     if (!(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) return IMLS_REJ_INVALID_NORMAL;
     if (kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg)) return IMLS_REJ_NORMAL_CONSTRAINT;
     const double xd[3] = {xf[0], xf[1], xf[2]};
@@ -157,7 +121,8 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
         const float4 qn = t.mnr[inl ? lpos[j] : p1];   // unconditional: the loads issue together
         if (inl) {
             ++kq;
-            bool ok = isfinite(qn.x) && isfinite(qn.y) && isfinite(qn.z);
+            // get_normals=false without count mode (TV's IMLS neighbours): every normal is ∞ (Q1)
+            bool ok = kp.get_normals && isfinite(qn.x) && isfinite(qn.y) && isfinite(qn.z);
             if (ok && kp.angle_on) ok = !angle_reject(ns, qn.x, qn.y, qn.z, kp.angle_thr_deg);
             if (ok) { acc |= 1ull << j; ++nacc; }
         }
@@ -958,7 +923,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_finish(TreeView t, const float4*
             cat = -3;                                         // deferred to k_project_lane
         } else {
             cat = kp.matcher ? finish_plane(xf, ns, p1, t, kp, yf, nf)
-                             : finish_query<KL>(xf, ns, ed, ep, 0, min(K, cnt_r), d1, p1, t, kp, yf, nf, kq);
+                             : finish_query<KL>(xf, ns, ed, ep, 0, min(K, cnt_r), d1, p1, t, kp, yf, nf, kq, i);
             store_result(i, cat, xf, yf, nf, cs, cd, cn);
         }
     }
@@ -1120,7 +1085,7 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(TreeView t, const f
             for (int j = 0; j < KCAP; ++j) lpos[j] = (li[j] >= 0 && li[j] != 0x7fffffff) ? (int)t.ipos[li[j]] : 0;
             const int p1 = nn_found ? (int)t.ipos[i1] : -1;
             cat = kp.matcher ? finish_plane(xf, ns, p1, t, kp, yf, nf)
-                             : finish_query<KCAP>(xf, ns, ld, lpos, KCAP - K, cnt, d1, p1, t, kp, yf, nf, kq);
+                             : finish_query<KCAP>(xf, ns, ld, lpos, KCAP - K, cnt, d1, p1, t, kp, yf, nf, kq, i);
             store_result(i, cat, xf, yf, nf, cs, cd, cn);
         }
         if (cat >= 0) atomicAdd(&rej_s[cat], 1u);
@@ -1183,6 +1148,8 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
     const int wblocks = (N + kWaveBlock - 1) / kWaveBlock;
     double* p_fb = partial1 + (size_t)wblocks * kNormEq;
     const int K = kp.K;
+    // tensor voting: every source point's voted normal at this pose first (imls_icp.cpp:514-546)
+    if (kp.tv) launch_tv_vote(s, t, spt, N, pose, done, kp, const_cast<double4*>(t.tvn));
     if (lane_mode || kp.proj) {
         // reference mode: every query through the exact per-lane kernel (grid-stride over the
         // fallback slabs); the wave slabs are zeroed

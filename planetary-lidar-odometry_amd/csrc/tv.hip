@@ -1,0 +1,266 @@
+// tv.hip — tensor-voting normals on device: IMLSICPMatcher::VoteForAny (imls_icp.cpp:171-296) as
+// ProjSourcePtToSurface uses it (get_normals=false, use_tensor_voting=true: 514-546, 634-643).
+//
+// Every ICP iteration the reference votes from the target's input tensors into every transformed
+// source point x (in_cloudDP): the voters are x's libnabo knn(k) over the target (no radius, no
+// self match, 197), a voter p counts when 0 < ‖x−p‖/σ < distance_threshold (212-217) and adds
+// S = w·R·T_p·R' with w = exp(−‖r‖²/σ), R = I − 2r̂r̂ᵀ, R' = (I − ½r̂r̂ᵀ)R (220-226).  The query's
+// normal is the "tangent" of the summed tensor (the eigenvector of its smallest |λ|, lower
+// triangle, flipped to +z; 245, 272-278, 543); a zero tensor (Eigen isZero, |coeff| ≤ 1e-12) has
+// none and the query is rejected as "no normal" (637-643).
+//
+// Voters are the k nearest, but only those within ρ = threshold·σ of x vote, and every point
+// nearer than a voting one is itself within ρ: so the exact voter set is "the ≤ k best (d², index)
+// of the ball of radius ρ" — a small fixed-radius search, not a k-nearest search.  One wave per
+// query: the tree walk is wave-uniform (scalar node loads), a leaf is one coalesced load with one
+// point per lane, ball members (fp32 screen with slack, exact fp64 libnabo metric, self match
+// excluded by d² > DBL_EPSILON) are appended to an LDS buffer by ballot; a full buffer is sorted
+// and cut to the best k (the k-th entry then bounds the search).  Finally the buffer is sorted by
+// (d², index), lane j < k computes voter j's S in fp64, lane 0 sums them in list order (the
+// reference's order) and runs the shared 3×3 Jacobi eigensolver.
+#include <cfloat>
+
+#include "geom.h"
+#include "solve_common.h"
+
+namespace imlsgpu {
+namespace {
+
+constexpr int kTvBlock = 256;              // 4 waves per block, one query per wave
+constexpr int kTvWaves = kTvBlock / 64;
+constexpr int kTvCap = 256;                // ball members buffered per query before a cut to the best k
+constexpr int kTvStack = 32;               // tree depth ≤ 23 (kStackDepth − 1), one push per level
+constexpr float kTvSlack = 1.0f + 2e-6f;   // fp32 screen vs exact distance: ≤ 3.1e-7 relative
+static_assert(kTvCap >= kTvMaxK + 64, "a cut must leave room for one more leaf");
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave sorts n (a power of two) LDS entries ascending by (key, index).
+__device__ void wave_bitonic(unsigned long long* k, unsigned* ix, unsigned* ps, int n, int lane) {
+    for (int size = 2; size <= n; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int a = lane; a < n; a += 64) {
+                const int b = a ^ stride;
+                if (b > a) {
+                    const bool up = (a & size) == 0;
+                    const bool gt = k[a] > k[b] || (k[a] == k[b] && ix[a] > ix[b]);
+                    if (gt == up) {
+                        const unsigned long long tk = k[a]; k[a] = k[b]; k[b] = tk;
+                        const unsigned ti = ix[a]; ix[a] = ix[b]; ix[b] = ti;
+                        const unsigned tp = ps[a]; ps[a] = ps[b]; ps[b] = tp;
+                    }
+                }
+            }
+            wave_sync();
+        }
+}
+
+__global__ __launch_bounds__(kTvBlock) void k_tv_vote(TreeView t, const float4* __restrict__ spt, int N,
+                                                      const double* __restrict__ pose, const int* __restrict__ done,
+                                                      KParams kp, double4* __restrict__ tvn) {
+    if (done && *done) return;
+    __shared__ unsigned long long ck[kTvWaves][kTvCap];   // exact d² bits (positive doubles order as integers)
+    __shared__ unsigned ci[kTvWaves][kTvCap];             // filtered target index (the tie order)
+    __shared__ unsigned cp[kTvWaves][kTvCap];             // Morton position
+    __shared__ int snode[kTvWaves][kTvStack];
+    __shared__ float sdist[kTvWaves][kTvStack];
+    __shared__ double sv[kTvWaves][kTvMaxK][9];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * kTvWaves + wv);
+    if (q >= N) return;
+    float xf[3];
+    {
+        double ns_unused[3];
+        transform_query(pose, spt[q], make_float4(0.f, 0.f, 0.f, 0.f), 0, xf, ns_unused);
+    }
+    const double xd[3] = {xf[0], xf[1], xf[2]};
+    const double sigma = kp.tv_sigma, thr = kp.tv_thr;
+    const double rho = thr * sigma;
+    const float r2s = (float)(rho * rho) * kTvSlack + 1e-30f;
+    const int K = kp.tv_k;
+    unsigned long long* wk = ck[wv];
+    unsigned* wi = ci[wv];
+    unsigned* wp = cp[wv];
+    int cnt = 0;
+    unsigned long long bk = ~0ull;     // after a cut: the k-th (d², index) — later members must beat it
+    unsigned bi = ~0u;
+    float bnd = r2s;
+    auto sort_buffer = [&]() {
+        int n = 1;
+        while (n < cnt) n <<= 1;
+        for (int a = cnt + lane; a < n; a += 64) { wk[a] = ~0ull; wi[a] = ~0u; wp[a] = 0u; }
+        wave_sync();
+        wave_bitonic(wk, wi, wp, n, lane);
+    };
+    const int P = t.P, B = t.B, M = t.M;
+    int node = 1, sp = 0;
+    while (node) {
+        if (node < P) {
+            const float4* rec = t.nodes + 3 * (size_t)node;
+            const float4 a = rec[0], b = rec[1], c = rec[2];
+            const float dl = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+            const float dr = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
+            const float bs = bnd * kTvSlack;
+            const bool nl = dl <= bs, nr = dr <= bs;
+            if (nl && nr) {
+                const bool lf = dl <= dr;
+                snode[wv][sp] = lf ? 2 * node + 1 : 2 * node;
+                sdist[wv][sp] = lf ? dr : dl;
+                ++sp;
+                node = __builtin_amdgcn_readfirstlane(lf ? 2 * node : 2 * node + 1);
+                continue;
+            }
+            if (nl) { node = 2 * node; continue; }
+            if (nr) { node = 2 * node + 1; continue; }
+        } else {
+            const int base = (node - P) * B, cl = min(B, M - base);
+            bool pass = false;
+            unsigned long long key = 0ull;
+            unsigned oi = 0u;
+            if (lane < cl) {
+                const float4 p4 = t.mpt[base + lane];
+                const float ex = p4.x - xf[0], ey = p4.y - xf[1], ez = p4.z - xf[2];
+                const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                if (d32 <= bnd) {
+                    const double d2 = exact_d2(xd, p4.x, p4.y, p4.z);
+                    key = (unsigned long long)__double_as_longlong(d2);
+                    oi = __float_as_uint(p4.w);
+                    pass = d2 > DBL_EPSILON && (key < bk || (key == bk && oi < bi));   // no self match (197)
+                }
+            }
+            unsigned long long m = __ballot(pass);
+            if (cnt + __popcll(m) > kTvCap) {
+                // cut to the best k; its k-th entry bounds everything after
+                sort_buffer();
+                cnt = min(cnt, K);
+                if (cnt == K) {
+                    bk = wk[K - 1];
+                    bi = wi[K - 1];
+                    bnd = fminf(r2s, (float)__longlong_as_double((long long)bk) * kTvSlack + 1e-30f);
+                }
+                pass = pass && (key < bk || (key == bk && oi < bi));
+                m = __ballot(pass);
+            }
+            if (pass) {
+                const int at = cnt + __popcll(m & ((1ull << lane) - 1ull));
+                wk[at] = key;
+                wi[at] = oi;
+                wp[at] = (unsigned)(base + lane);
+            }
+            cnt += __popcll(m);
+        }
+        node = 0;
+        while (sp > 0) {
+            --sp;
+            if (sdist[wv][sp] <= bnd * kTvSlack) { node = snode[wv][sp]; break; }
+        }
+        node = __builtin_amdgcn_readfirstlane(node);
+    }
+    if (cnt > 0) sort_buffer();
+    const int kk = min(cnt, K);
+    // voter j = list entry j (lane j): S = w·(R·T)·R' in fp64, the oracle's evaluation order
+    if (lane < kk) {
+        double S[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        const int pos = (int)wp[lane];
+        const float4 p4 = t.mpt[pos];
+        const double r[3] = {xd[0] - (double)p4.x, xd[1] - (double)p4.y, xd[2] - (double)p4.z};
+        double nn2 = r[0] * r[0];
+        nn2 = nn2 + r[1] * r[1];
+        nn2 = nn2 + r[2] * r[2];
+        const double nr = sqrt(nn2);
+        const double dist = nr / sigma;
+        if (!(dist <= 0. || dist >= thr)) {
+            const double u[3] = {r[0] / nr, r[1] / nr, r[2] / nr};
+            const double w = exp(-(nr * nr) / sigma);
+            const float4 t0 = t.mten[2 * (size_t)pos], t1 = t.mten[2 * (size_t)pos + 1];
+            const double T[9] = {t0.x, t0.y, t0.z, t0.y, t0.w, t1.x, t0.z, t1.x, t1.y};
+            double R[9], Rp[9], RT[9];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) R[a * 3 + b] = (a == b ? 1.0 : 0.0) - 2 * u[a] * u[b];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    double s = 0.0;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) s += ((a == c ? 1.0 : 0.0) - 0.5 * u[a] * u[c]) * R[c * 3 + b];
+                    Rp[a * 3 + b] = s;
+                }
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    double s = 0.0;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) s += R[a * 3 + c] * T[c * 3 + b];
+                    RT[a * 3 + b] = s;
+                }
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    double s = 0.0;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) s += RT[a * 3 + c] * Rp[c * 3 + b];
+                    S[a * 3 + b] = w * s;
+                }
+        }
+#pragma unroll
+        for (int e = 0; e < 9; ++e) sv[wv][lane][e] = S[e];
+    }
+    wave_sync();
+    if (lane != 0) return;
+    double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < kk; ++j)
+#pragma unroll
+        for (int e = 0; e < 9; ++e) acc[e] += sv[wv][j][e];
+    bool zero = true;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) zero = zero && fabs(acc[e]) <= 1e-12;
+    if (zero) { tvn[q] = make_double4(0.0, 0.0, 0.0, 0.0); return; }
+    double A[9], ev[3], U[9];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) A[a * 3 + b] = a >= b ? acc[a * 3 + b] : acc[b * 3 + a];
+    sym_eig<3>(A, ev, U);
+    int mi = 0;
+    if (fabs(ev[1]) < fabs(ev[mi])) mi = 1;
+    if (fabs(ev[2]) < fabs(ev[mi])) mi = 2;
+    double n0 = U[mi * 3], n1 = U[mi * 3 + 1], n2 = U[mi * 3 + 2];
+    if (n2 < 0) { n0 = -n0; n1 = -n1; n2 = -n2; }
+    tvn[q] = make_double4(n0, n1, n2, 1.0);
+}
+
+// Input tensors [6][n_in] (input order) → Morton order, 2 float4 per point.
+__global__ void k_tensor_gather(const float* __restrict__ ten6, size_t n_in, const unsigned* __restrict__ kept,
+                                const float4* __restrict__ mpt, int M, float4* __restrict__ mten) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= M) return;
+    const size_t in = kept[__float_as_uint(mpt[m].w)];
+    mten[2 * (size_t)m] = make_float4(ten6[in], ten6[n_in + in], ten6[2 * n_in + in], ten6[3 * n_in + in]);
+    mten[2 * (size_t)m + 1] = make_float4(ten6[4 * n_in + in], ten6[5 * n_in + in], 0.f, 0.f);
+}
+
+}  // namespace
+
+void launch_tv_vote(hipStream_t s, const TreeView& t, const float4* spt, int N, const double* pose, const int* done,
+                    const KParams& kp, double4* tvn) {
+    if (N <= 0 || t.M <= 0) return;
+    k_tv_vote<<<(N + kTvWaves - 1) / kTvWaves, kTvBlock, 0, s>>>(t, spt, N, pose, done, kp, tvn);
+}
+
+void launch_tensor_gather(hipStream_t s, const float* ten6_in, size_t n_in, const unsigned* kept, const float4* mpt, int M,
+                          float4* mten) {
+    if (M <= 0) return;
+    k_tensor_gather<<<(M + 255) / 256, 256, 0, s>>>(ten6_in, n_in, kept, mpt, M, mten);
+}
+
+}  // namespace imlsgpu

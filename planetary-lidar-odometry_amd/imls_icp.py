@@ -106,6 +106,17 @@ class ImlsContext:
         self.n_target = n.value
         return n.value
 
+    def set_target_tensors(self, tensors):
+        """Tensor-voting input tensors of the last set_target's points: (n, 6) float32
+        (xx, xy, xz, yy, yz, zz) — VoteForAny's encode(AWARE_TENSOR) input (imls_icp.cpp:179)."""
+        t = np.ascontiguousarray(tensors, dtype=np.float32)
+        if t.ndim != 2 or t.shape[1] != 6:
+            raise ValueError("tensors must be (n, 6)")
+        self._check(self.lib.imls_set_target_tensors(self.ctx, _ptr(t), t.shape[0], 6))
+
+    def set_target_tensors_device(self, ten6_ptr: int, n: int):
+        self._check(self.lib.imls_set_target_tensors_device(self.ctx, C.c_void_p(ten6_ptr), n))
+
     def set_source(self, cloud):
         a = _as_xyzn(cloud)
         n = C.c_size_t()
@@ -258,6 +269,16 @@ class IMLSICPMatcher:
         out["x"], out["y"], out["z"] = y[:, 0], y[:, 1], y[:, 2]
         out["normal_x"], out["normal_y"], out["normal_z"] = n[:, 0], n[:, 1], n[:, 2]
         return keep, out, dict(zip(_abi.REJECT_NAMES, map(int, rej)))
+
+
+def tv_encode_pca(evals, evecs, k: int = 50) -> np.ndarray:
+    """The reference's tensor encoding of PCA features (scan_registration.cpp:358-381) via the
+    library's host helper: evals (n, 3), evecs (n, 9) column-major 3×3 → tensors (n, 6)."""
+    ev = np.ascontiguousarray(evals, dtype=np.float32)
+    ec = np.ascontiguousarray(evecs, dtype=np.float32)
+    out = np.zeros((ev.shape[0], 6), np.float32)
+    _abi.load_library().imls_tv_encode_pca(_ptr(ev), _ptr(ec), ev.shape[0], int(k), _ptr(out))
+    return out
 
 
 def _triples(v) -> np.ndarray:

@@ -198,33 +198,42 @@ def _cast(scene: Scene, o: np.ndarray, d: np.ndarray, max_range: float):
             t_best[idx] = tt[idx]
             n_best[idx] = nn
     else:
-        # heightfield: march then bisect (rays going down only hit reliably; rays up miss)
+        # heightfield: march then bisect (rays going down only hit reliably; rays up miss).  Only
+        # the boulders within reach of this sensor position and only the still-marching rays are
+        # evaluated per step (a full scan takes seconds, not minutes).
+        bsub = scene.boulders
+        if len(bsub):
+            reach = max_range + 6.0 * bsub[:, 3] + 2.0     # exp(−d²/2σ²) < 1e-10 beyond
+            bsub = bsub[np.hypot(bsub[:, 0] - o[0], bsub[:, 1] - o[1]) < reach]
+        sub = Scene(scene.kind, scene.boxes, scene.poles, scene.terrain, bsub)
         t = np.full(R, np.inf)
-        tprev = np.zeros(R)
-        fprev = o[2] - _terrain_height(scene, o[0] + 0 * d[:, 0], o[1] + 0 * d[:, 1])
+        fprev = o[2] - _terrain_height(sub, o[0] + 0 * d[:, 0], o[1] + 0 * d[:, 1])
         step = 0.25
-        active = np.ones(R, bool)
+        act = np.nonzero(fprev > 0)[0]
+        fprev = fprev[act]
         tk = 0.0
-        while tk < max_range and active.any():
+        while tk < max_range and act.size:
             tk += step
-            p = o[None, :] + tk * d
-            f = p[:, 2] - _terrain_height(scene, p[:, 0], p[:, 1])
-            cross = active & (f <= 0) & (fprev > 0)
+            p = o[None, :] + tk * d[act]
+            f = p[:, 2] - _terrain_height(sub, p[:, 0], p[:, 1])
+            cross = f <= 0
             if cross.any():
-                lo, hi = np.full(R, tk - step), np.full(R, tk)
+                ci = act[cross]
+                dc = d[ci]
+                lo, hi = np.full(ci.size, tk - step), np.full(ci.size, tk)
                 for _ in range(30):
                     mid = 0.5 * (lo + hi)
-                    pm = o[None, :] + mid[:, None] * d
-                    fm = pm[:, 2] - _terrain_height(scene, pm[:, 0], pm[:, 1])
+                    pm = o[None, :] + mid[:, None] * dc
+                    fm = pm[:, 2] - _terrain_height(sub, pm[:, 0], pm[:, 1])
                     lo = np.where(fm > 0, mid, lo)
                     hi = np.where(fm > 0, hi, mid)
-                t = np.where(cross, 0.5 * (lo + hi), t)
-                active &= ~cross
+                t[ci] = 0.5 * (lo + hi)
+                act, f = act[~cross], f[~cross]
             fprev = f
             step = min(1.0, 0.25 + tk * 0.01)
         hit = np.isfinite(t)
         p = o[None, :] + np.where(hit, t, 0)[:, None] * d
-        gx, gy = _terrain_grad(scene, p[:, 0], p[:, 1])
+        gx, gy = _terrain_grad(sub, p[:, 0], p[:, 1])
         nn = np.stack([-gx, -gy, np.ones(R)], 1)
         nn /= np.linalg.norm(nn, axis=1, keepdims=True)
         t_best = t
@@ -373,3 +382,36 @@ def fps_subsample(cloud: np.ndarray, n: int, seed: int = 0) -> np.ndarray:
         idx.append(j)
         d = np.minimum(d, np.linalg.norm(p - p[j], axis=1))
     return cloud[np.sort(np.asarray(idx))]
+
+
+def pca_features(cloud: np.ndarray, k: int = 15):
+    """Per-point PCA features as scan_registration.cpp:158-229 produces them (covariance of the
+    neighbourhood / (count − 1), SelfAdjointEigenSolver, eigenvalues re-ordered λ1 ≥ λ2 ≥ λ3 with
+    the eigenvector columns swapped to match, 220-226), laid out like 1202-1207: evals (n, 3) and
+    evecs (n, 9) = the 3×3 eigenvector matrix column-major (e1 = largest, e2, e3 = normal).
+    The neighbourhood here is the k nearest points (the reference takes ring windows of 3 scan
+    lines) — synthetic input for config E, not a restatement of the ring search."""
+    from scipy.spatial import cKDTree
+    p = np.stack([cloud["x"], cloud["y"], cloud["z"]], 1).astype(np.float32)
+    _, nb = cKDTree(p.astype(np.float64)).query(p.astype(np.float64), k=min(k, len(p)))
+    g = p[nb]                                                    # (n, k, 3) float32
+    c = g - g.mean(axis=1, keepdims=True)
+    cov = np.einsum("nki,nkj->nij", c, c) / np.float32(g.shape[1] - 1)
+    w, v = np.linalg.eigh(cov.astype(np.float64))               # ascending
+    w, v = w[:, ::-1].astype(np.float32), v[:, :, ::-1].astype(np.float32)
+    evecs = np.transpose(v, (0, 2, 1)).reshape(-1, 9)            # column-major: e1 | e2 | e3
+    return np.ascontiguousarray(w), np.ascontiguousarray(evecs)
+
+
+def make_planetary_pair(map_scans: int = 1, scene_seed: int = 3, start: int = 30, tensor_k: int = 50,
+                        pca_k: int = 15):
+    """BASELINE config E: sparse VLP-16 scans over the procedural planetary heightfield; the
+    target additionally carries tensor-voting input tensors — the reference's own encoding of
+    per-point PCA features (CustomTensorVoting, scan_registration.cpp:358-381, restated by
+    imls_icp.tv_encode_pca) — that VoteForAny reads through encode(AWARE_TENSOR)."""
+    from . import imls_icp
+    pr = make_pair("vlp16", map_scans=map_scans, scene_seed=scene_seed, scene_kind="planetary", start=start)
+    evals, evecs = pca_features(pr.target, pca_k)
+    pr.meta["tensors"] = imls_icp.tv_encode_pca(evals, evecs, tensor_k)
+    pr.meta["pca"] = (evals, evecs)
+    return pr

@@ -1,0 +1,136 @@
+"""GPU parity of tensor-voting normals (BASELINE config E): IMLS matcher with
+get_normals=false and use_tensor_voting=true — every ICP iteration the query's normal is the
+VoteForAny tangent of the target's input tensors (imls_icp.cpp:171-296, 514-546, 634-643), the
+IMLS neighbours keep the recompute-normal branch (count mode; dead mode rejects them all, Q1).
+
+Fixture tests/golden/tv_pair.npz (make_golden.py): a VLP-16 planetary pair, the target's tensors
+from the reference's own PCA encoding (scan_registration.cpp:358-381), the C++ oracle's outputs
+(pinned to the numpy restatement).  libpointmatcher's decompose semantics are unpinned (not in
+the container); both sides use the documented restatement (imls_oracle.cpp, tv_normal).
+
+Tolerances: found flags, validity masks, reject counters, x exact; TV normals (n) ≤ 1e-6 — the
+device sums the votes in the same order with the same Jacobi sweeps, but its exp() may differ
+from glibc's by 1 ulp; y ≤ 1e-5 m; poses ≤ 1e-6."""
+import pathlib
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+from planetary_lidar_odometry_amd import _abi, config, imls_icp
+
+pytestmark = pytest.mark.gpu
+GOLDEN = pathlib.Path(__file__).resolve().parent / "golden"
+N_TOL = 1e-6
+Y_TOL = 1e-5
+POSE_TOL = 1e-6
+
+
+def rows(soa6):
+    return np.ascontiguousarray(np.asarray(soa6, np.float32).T)
+
+
+def tv_params(count_mode=1, iters=10, k=50, sigma=0.2, thr=0.6):
+    p = config.bench_params(iters)
+    p.delta_dist_threshold = 0.001
+    p.delta_angle_threshold = 0.0001745353
+    p.get_normals = 0
+    p.recompute_normal_count_mode = count_mode
+    p.use_tensor_voting = 1
+    p.tensor_k, p.tensor_sigma, p.tensor_distance_threshold = k, sigma, thr
+    return p
+
+
+@pytest.fixture(scope="module")
+def g():
+    return dict(np.load(GOLDEN / "tv_pair.npz"))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = imls_icp.ImlsContext(tv_params())
+    yield c
+    c.close()
+
+
+def load(ctx, g, p):
+    ctx.set_params(p)
+    ctx.set_target(rows(g["tgt"]))
+    ctx.set_target_tensors(rows(g["ten"]))
+    ctx.set_source(rows(g["src"]))
+
+
+def test_tv_projection_matches_golden(ctx, g):
+    load(ctx, g, tv_params())
+    for k in (0, 1):
+        x, y, n, idx, rej = ctx.project(g[f"pose{k}"])
+        assert np.array_equal(rej, g[f"rej{k}"]), (rej, g[f"rej{k}"])
+        assert np.array_equal(idx, g[f"idx{k}"])
+        assert np.array_equal(x, g[f"x{k}"])
+        assert np.abs(n.astype(np.float64) - g[f"n{k}"]).max() <= N_TOL
+        assert np.abs(y.astype(np.float64) - g[f"y{k}"]).max() <= Y_TOL
+
+
+@pytest.mark.parametrize("k,sigma,thr", [(50, 0.2, 0.6), (8, 0.5, 0.6), (64, 0.4, 1.0), (20, 1.0, 0.3)])
+def test_tv_projection_vs_oracle_params(ctx, g, k, sigma, thr):
+    """Other voting radii / k: the k-cut (more ball members than k) and a full candidate buffer."""
+    p = tv_params(k=k, sigma=sigma, thr=thr)
+    load(ctx, g, p)
+    pose = g["pose1"]
+    x, y, n, idx, rej = ctx.project(pose)
+    wx, wy, wn, widx, wrej = oc.project(g["src"], g["tgt"], pose, p, tensors=g["ten"])
+    assert np.array_equal(rej, wrej) and np.array_equal(idx, widx)
+    assert np.array_equal(x, wx)
+    assert np.abs(n.astype(np.float64) - wn).max() <= N_TOL
+    assert np.abs(y.astype(np.float64) - wy).max() <= Y_TOL
+
+
+def test_tv_register_frame(ctx, g):
+    load(ctx, g, tv_params())
+    r = ctx.register_frame()
+    assert r["iters"] == int(g["frame_iters"]) and r["status"] == int(g["frame_status"])
+    assert np.abs(r["pose"] - g["frame_pose"]).max() <= POSE_TOL
+    nv = np.array([t.n_valid for t in r["trace"]])
+    assert np.array_equal(nv, g["frame_nvalid"])
+    assert np.array_equal(np.array([list(t.reject) for t in r["trace"]]), g["frame_rej"])
+
+
+def test_tv_dead_mode_rejects_all_imls(ctx, g):
+    """Reference semantics (Q1): the IMLS neighbours' recomputed normals are ∞ → every query
+    that has a voted normal fails the IMLS function; the frame stops with too few pairs."""
+    p = tv_params(count_mode=0)
+    load(ctx, g, p)
+    x, y, n, idx, rej = ctx.project(g["pose1"])
+    wx, wy, wn, widx, wrej = oc.project(g["src"], g["tgt"], g["pose1"], p, tensors=g["ten"])
+    assert len(idx) == 0 and np.array_equal(rej, wrej)
+    assert rej[4] > 0
+    r = ctx.register_frame()
+    assert r["status"] == _abi.IMLS_FRAME_TOO_FEW and r["iters"] == 0
+
+
+def test_tv_needs_tensors(ctx, g):
+    ctx.set_params(tv_params())
+    ctx.set_target(rows(g["tgt"]))          # invalidates the tensors
+    ctx.set_source(rows(g["src"]))
+    with pytest.raises(_abi.ImlsError) as e:
+        ctx.project(np.eye(4))
+    assert e.value.status == _abi.IMLS_ERR_STATE
+    with pytest.raises(_abi.ImlsError) as e:
+        ctx.set_target_tensors(rows(g["ten"])[:-1])
+    assert e.value.status == _abi.IMLS_ERR_ARG
+
+
+def test_tv_nan_target_points_are_skipped(ctx, g):
+    """Tensor records follow set_target's INPUT order; records of NaN-filtered points are dropped."""
+    tgt = np.array(g["tgt"], copy=True)
+    tgt[0, 5] = np.nan
+    tgt[2, 100] = np.inf
+    p = tv_params()
+    ctx.set_params(p)
+    ctx.set_target(rows(tgt))
+    ctx.set_target_tensors(rows(g["ten"]))
+    ctx.set_source(rows(g["src"]))
+    x, y, n, idx, rej = ctx.project(g["pose1"])
+    wx, wy, wn, widx, wrej = oc.project(g["src"], tgt, g["pose1"], p, tensors=g["ten"])
+    assert np.array_equal(rej, wrej) and np.array_equal(idx, widx)
+    assert np.abs(n.astype(np.float64) - wn).max() <= N_TOL

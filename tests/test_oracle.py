@@ -309,3 +309,73 @@ def test_plane_icp_kat():
     x, y, n, idx, rej = oc.project(src, tgt, np.eye(4), p)
     assert list(idx) == [0, 1] and rej[0] == 1 and rej.sum() == 1
     assert np.allclose(y[:, 2], 0.0, atol=1e-7) and np.allclose(y[:, :2], x[:, :2], atol=1e-7)
+
+
+# ---- tensor voting (libpointmatcher decompose semantics unpinned) ----------
+def tv_params(count_mode=1, k=50, sigma=0.2, thr=0.6):
+    p = gparams()
+    p.get_normals = 0
+    p.recompute_normal_count_mode = count_mode
+    p.use_tensor_voting = 1
+    p.tensor_k, p.tensor_sigma, p.tensor_distance_threshold = k, sigma, thr
+    return p
+
+
+def test_tv_oracle_reproduces_golden():
+    g = golden("tv_pair")
+    p = tv_params()
+    for k in (0, 1):
+        nrm, found, _ = oc.tv_normals(g["tgt"], g["ten"], g[f"tvq{k}"], p)
+        assert np.array_equal(found, g[f"tvf{k}"]) and np.array_equal(nrm, g[f"tvn{k}"])
+        x, y, n, idx, rej = oc.project(g["src"], g["tgt"], g[f"pose{k}"], p, tensors=g["ten"])
+        assert np.array_equal(idx, g[f"idx{k}"]) and np.array_equal(rej, g[f"rej{k}"])
+        assert np.array_equal(x, g[f"x{k}"]) and np.array_equal(y, g[f"y{k}"]) and np.array_equal(n, g[f"n{k}"])
+    fr = oc.register_frame(g["src"], g["tgt"], p, tensors=g["ten"])
+    assert fr["iters"] == int(g["frame_iters"]) and fr["status"] == int(g["frame_status"])
+    assert np.abs(fr["pose"] - g["frame_pose"]).max() < 1e-12
+
+
+@pytest.mark.parametrize("k,sigma,thr", [(8, 0.5, 0.6), (64, 0.4, 1.0), (20, 1.0, 0.3)])
+def test_tv_restatements_agree(k, sigma, thr):
+    """C++ oracle vs the independent numpy restatement (cKDTree candidates, numpy products,
+    LAPACK eigh on the lower triangle), incl. the k-cut of large voting balls."""
+    g = golden("tv_pair")
+    p = tv_params(k=k, sigma=sigma, thr=thr)
+    q = g["tvq1"][:, ::10]
+    nrm, found, acc = oc.tv_normals(g["tgt"], g["ten"], q, p)
+    nrm2, found2, acc2 = imls_np.tv_normals(g["tgt"], g["ten"], q, dict(tensor_k=k, tensor_sigma=sigma,
+                                                                          tensor_distance_threshold=thr))
+    assert np.array_equal(found, found2) and found.sum() > 10
+    assert np.abs(acc - acc2).max() <= 1e-15 * max(1.0, np.abs(acc).max()) * 10
+    assert np.abs(nrm - nrm2).max() <= 1e-10
+
+
+def test_tv_kat_plane_normal():
+    """Known answer: voters on the plane z = 0 whose tensors span the plane (the PCA encoding of
+    a flat patch: e1, e2 in-plane) vote into a point of the plane: every r̂ is in-plane, so R and
+    R' fix ẑ, the summed tensor has a zero z row/column and its smallest-|λ| eigenvector is ẑ."""
+    rng = np.random.default_rng(3)
+    M = 400
+    tgt = np.zeros((6, M), np.float32)
+    tgt[0], tgt[1] = rng.uniform(-0.3, 0.3, M), rng.uniform(-0.3, 0.3, M)
+    ev = np.tile(np.array([[0.02, 0.01, 1e-5]], np.float32), (M, 1))
+    evecs = np.tile(np.array([[1, 0, 0, 0, 1, 0, 0, 0, 1]], np.float32), (M, 1))
+    ten = imls_np.tv_encode_pca(ev, evecs, 50).T
+    q = np.array([[0.01], [0.02], [0.0]], np.float32)
+    p = tv_params(sigma=0.2, thr=0.6)
+    nrm, found, _ = oc.tv_normals(tgt, ten, q, p)
+    assert found[0] == 1 and abs(nrm[0, 2] - 1.0) < 1e-12
+    far = np.array([[5.0], [5.0], [5.0]], np.float32)       # no voter within thr·σ → zero tensor
+    _, found, _ = oc.tv_normals(tgt, ten, far, p)
+    assert found[0] == 0
+
+
+def test_tv_encode_pca_host_helper_matches_restatement():
+    """imls_tv_encode_pca (product host helper, scan_registration.cpp:358-381) is pure host float
+    arithmetic: bit-identical to the numpy restatement; the unit-ball branch for non-ordered λ."""
+    from planetary_lidar_odometry_amd import imls_icp
+    g = golden("tv_pair")
+    ev, ec = g["evals"], g["evecs"]
+    assert np.array_equal(imls_icp.tv_encode_pca(ev, ec, 50), imls_np.tv_encode_pca(ev, ec, 50))
+    bad = np.array([[np.nan, 1.0, 0.5]], np.float32)
+    assert np.array_equal(imls_icp.tv_encode_pca(bad, ec[:1], 50)[0], np.array([1, 0, 0, 1, 0, 1], np.float32))
