@@ -131,6 +131,8 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_WIDE")) k.wide = std::max(1, std::min(3, std::atoi(w)));
     k.verlet = 1;
     if (const char* w = std::getenv("IMLS_VERLET")) k.verlet = std::atoi(w);
+    k.lockstep = 1;
+    if (const char* w = std::getenv("IMLS_LOCKSTEP")) k.lockstep = std::atoi(w);
     // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
     // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)
     k.tv = (p.use_tensor_voting && !p.get_normals && p.matching_method == IMLS_MATCH_IMLS) ? 1 : 0;

@@ -286,7 +286,7 @@ __device__ __forceinline__ float need_key(const float (&lk)[KL], float r2, int K
     return cnt_r >= K ? fmaxf(dK, d1) : kInfF;
 }
 
-template <int KL>
+template <int KL, bool LOCKSTEP>
 __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
                                                          const double* __restrict__ pose,
@@ -298,6 +298,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float4 sbox[kWaveBlock / 64][kWaveStack][2];
+    __shared__ float4 sleaf[kWaveBlock / 64][64];   // the current leaf's points (lockstep insertion)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int slot = blockIdx.x * kWaveBlock + tid;
@@ -401,7 +402,60 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
 #ifdef IMLS_DEBUG_WAVE_TRACE
         if (__popcll(want) <= sparse_thr) { ++dbg_sparse; dbg_sparse_lanes += __popcll(want); } else { ++dbg_bcast; }
 #endif
-        if (__popcll(want) <= sparse_thr) {
+        if (LOCKSTEP && __popcll(want) <= sparse_thr) {
+            // few lanes want this leaf (spread-out queries in a dense region): per wanting lane,
+            // all leaf points are measured at once (one per lane) and the ones under that lane's
+            // bound and not yet listed become its candidate mask; then the lanes insert their own
+            // candidates in lockstep, each its lowest pending point per step (index order) read
+            // back from LDS — max(per-lane candidates) insertion steps instead of one per
+            // candidate of every lane.  (The broadcast path keeps inline insertion: there the
+            // candidates of different lanes mostly coincide in time.)
+            unsigned long long cm = 0ull;
+            {
+                unsigned long long m = want;
+                while (m) {
+                    const int q = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
+                    m &= m - 1;
+                    const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[0]), q));
+                    const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[1]), q));
+                    const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[2]), q));
+                    const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bnd), q));
+                    const unsigned long long inq =
+                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(inl >> 32), q) << 32) |
+                        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)inl, q);
+                    const float ex = mine.x - qx, ey = mine.y - qy, ez = mine.z - qz;
+                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                    const unsigned long long pm = __ballot(lane < cnt && d32 <= qb) & ~inq;
+                    if (lane == q) cm = pm;
+                }
+            }
+            if (__ballot(cm != 0ull)) {
+                sleaf[wv][lane] = mine;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                while (__ballot(cm != 0ull)) {
+                    if (cm) {
+                        const int j = (int)__builtin_ctzll(cm);
+                        cm &= cm - 1;
+                        const float4 p = sleaf[wv][j];
+                        const float ex = p.x - xf[0], ey = p.y - xf[1], ez = p.z - xf[2];
+                        const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                        if (d32 <= bnd && d32 < lk[KL - 1]) {
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                            ++dbg_ins;
+#endif
+                            insert_top<KL>(lk, lp, d32, base + j);
+                            bnd = fminf(r2s, lk[KL - 1]);
+                        }
+                    }
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                    ++dbg_ev;
+#endif
+                }
+                __builtin_amdgcn_wave_barrier();   // sleaf is rewritten by the next leaf
+            }
+        } else if (__popcll(want) <= sparse_thr) {
             // few lanes want this leaf (spread-out queries in a dense region): per wanting lane,
             // all leaf points are measured at once (one per lane) and only the ones under that
             // lane's bound and not yet listed are handed to it, in index order
@@ -1128,9 +1182,12 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
     if (kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
                                                                                           delta, lists, wlist, xref, nref, use_prev, stats);
+    else if (kp.lockstep)
+        k_knn_wave<KL, true><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
+                                                          nref, use_prev, stats);
     else
-        k_knn_wave<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref,
-                                                    use_prev, stats);
+        k_knn_wave<KL, false><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
+                                                           nref, use_prev, stats);
     if (marks) (void)hipEventRecord(marks[1], s);
     k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,
                                                stats, fb_list, fb_count);
