@@ -180,7 +180,7 @@ int ensure_solve(imls_ctx* c, int N) {
     size_t bytes = 0;
     auto add = [&](size_t b) { size_t o = bytes; bytes += (b + 255) / 256 * 256; return o; };
     size_t o_pose = add(16 * 8), o_delta = add(16 * 8), o_x0 = add(8 * 8), o_done = add(16), o_status = add(16),
-           o_iters = add(16), o_hist = add(kHistBins * 4), o_cc = add(16), o_cl = add((size_t)kCandCap * 8),
+           o_iters = add(16), o_hist = add(kHistBins * 4), o_coarse = add(kHistBins / 256 * 4), o_cc = add(16), o_cl = add((size_t)kCandCap * 8),
            o_clr = add((size_t)kCandCap * 4), o_ch = add((size_t)kCandCap * 8), o_chr = add((size_t)kCandCap * 4),
            o_sel = add(16 * 4), o_p1 = add((size_t)pb * kNormEq * 8), o_p2 = add((size_t)pb * kNormEq * 8),
            o_keys = add(n * 8), o_trace1 = add(sizeof(imls_iter_trace));
@@ -194,6 +194,7 @@ int ensure_solve(imls_ctx* c, int N) {
     s.status = (int*)(b + o_status);
     s.iters = (int*)(b + o_iters);
     s.hist = (unsigned*)(b + o_hist);
+    s.coarse = (unsigned*)(b + o_coarse);
     s.cand_count = (unsigned*)(b + o_cc);
     s.cand_lo = (unsigned long long*)(b + o_cl);
     s.cand_lo_row = (unsigned*)(b + o_clr);
@@ -205,6 +206,10 @@ int ensure_solve(imls_ctx* c, int N) {
     s.keys = (double*)(b + o_keys);
     s.trace = (imls_iter_trace*)(b + o_trace1);
     s.partial_cap = pb;
+    // the residual histogram is re-zeroed after each use (k_collect); it starts zero
+    if (hipMemsetAsync(s.hist, 0, kHistBins * 4, c->stream) != hipSuccess ||
+        hipMemsetAsync(s.coarse, 0, kHistBins / 256 * 4, c->stream) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "hipMemset (solver)");
     c->st_N = (int)n;
     return IMLS_OK;
 }

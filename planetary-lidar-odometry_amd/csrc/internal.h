@@ -22,7 +22,7 @@ namespace imlsgpu {
 constexpr int kBlock = 256;            // threads per block for streaming kernels
 constexpr int kProjBlock = 128;        // threads per block for the projection kernel
 constexpr int kStackDepth = 24;        // traversal stack entries per lane (tree depth ≤ 24)
-constexpr int kHistBins = 65536;       // residual histogram bins (top 16 bits of float |r|)
+constexpr int kHistBins = 65536;       // residual histogram bins (top 16 bits of float |r|: 1/128 octave)
 constexpr int kCandCap = 8192;         // exact-select candidates handled in LDS per boundary bin
 constexpr int kNormEq = 28;            // 21 (JᵀJ upper) + 6 (Jᵀb) + 1 (row count)
 
@@ -107,6 +107,7 @@ struct SolveState {
     int* status;              // [1]  imls_frame_status
     int* iters;               // [1]  iterations run
     unsigned* hist;           // [kHistBins]
+    unsigned* coarse;         // [kHistBins / 256] the same histogram, 256 bins per entry
     unsigned* cand_count;     // [2]
     unsigned long long* cand_lo;   // [kCandCap*?] (key bits) pairs with row index
     unsigned* cand_lo_row;
@@ -156,6 +157,8 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
                         const float4* cd, const float4* cn, const double* rows_d, const double* weights,
                         SolveState& st, imls_iter_trace* tr, int update_pose, int rows_are_double,
                         const int* count = nullptr, const double* wsum = nullptr);
+// N above which the float-row LS takes the grid chain (below: one block, k_solve_small)
+constexpr int kSmallRows = 4096;
 int solve_blocks(int N);
 
 // normals.hip — map normals recomputed from the map (get_normals=false, count mode), Morton order

@@ -8,12 +8,14 @@
 // the 6×6 system — the same column pivoting and the same rank test (|R_kk| > 6·ε·max|R_ii|) as
 // ColPivHouseholderQR, since JᵀJ's Schur-complement diagonal equals QR's updated column norms².
 //
-// Trim selection is exact in the total order (|r|, row): |r| (fp64) is histogrammed on the top 12
+// Trim selection is exact in the total order (|r|, row): |r| (fp64) is histogrammed on the top 16
 // bits of its float image (monotone), the two boundary bins are collected and sorted by
 // (|r| bits, row) in LDS, everything strictly between them is reduced directly.
 //
-// Launch chain per LS solve: k_solve_first (1 block) → k_resid_hist → k_collect → k_solve_final
-// (1 block).  Every kernel returns at once when the frame's `done` flag is set.
+// Launch chain per LS solve: k_solve_first (1 block) → k_resid_hist → k_find_bins (1 block) →
+// k_collect (also re-zeroes the histogram) → k_solve_final (1 block).  Every kernel returns at
+// once when the frame's `done` flag is set.  (A "last block finishes the reduction" fusion was
+// measured slower on MI355X: each block's agent-scope release fence writes back its XCD's L2.)
 #include <cfloat>
 
 #include "solve_common.h"
@@ -21,7 +23,6 @@
 namespace imlsgpu {
 namespace {
 
-constexpr int kFinalBlock = 1024;
 constexpr int kCollectBlocks = 128;
 
 // ---------------------------------------------------------------------------------------------
@@ -48,147 +49,124 @@ __global__ __launch_bounds__(256) void k_solve_first(const double* __restrict__ 
     if (*st.done) return;
     __shared__ double acc[kNormEq];
     __shared__ double red[(256 / 64) * kNormEq];
-    const int t = threadIdx.x;
-    double loc[kNormEq];
-#pragma unroll
-    for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
-    for (int b = t; b < blocks; b += 256)
-#pragma unroll
-        for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
-    for (int i = t; i < kHistBins / 4; i += 256) reinterpret_cast<uint4*>(st.hist)[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (t < 2) st.cand_count[t] = 0u;
-    block_sum28<256>(loc, red, acc);
-    __syncthreads();
-    if (t != 0) return;
-    const double nvalid = acc[27];
-    if (update_pose && nvalid < (double)kp.correspond_number) {
-        // laser_odometry.cpp:570-576: not enough correspondences → break, keep rPose
-        *st.status = IMLS_FRAME_TOO_FEW;
-        *st.done = 1;
-        if (tr) tr->n_valid = (unsigned long long)nvalid;
-        return;
-    }
-    double x[6];
-    solve6(acc, x);
-    if (weighted) {
-        double D[16];
-        delta_from_x(x, D);
-        finish_iteration(st, tr, D, nvalid, nvalid, update_pose, kp);
-        return;
-    }
-    for (int k = 0; k < 6; ++k) st.x0[k] = x[k];
-    const long long N = (long long)nvalid;
-    long long lo = (long long)(kp.ls_threshold * (double)N);
-    long long hi = (long long)((1 - kp.ls_threshold) * (double)N);
-    if (hi > N - 1) hi = N - 1;       // Q11
-    st.sel[4] = (int)lo;
-    st.sel[5] = (int)hi;
-    st.sel[6] = (int)N;
+    solve_first_block<256>(partial, blocks, st, tr, kp, weighted, update_pose, red, acc);
 }
 
 // 65536 bins on the top 16 bits of the float image of |r| (sign bit 0: 8 exponent + 7 mantissa
-// bits, 1/128-octave bins): monotone in |r|, so ranks map to bins; boundary bins stay small.
+// bits, 1/128-octave bins): monotone in |r|, so ranks map to bins; boundary bins stay small
+// (fewer, wider bins were measured slower: more contention on the histogram atomics and larger
+// boundary sorts).
 __device__ __forceinline__ int key_bin(double key) {
     return (int)(__float_as_uint((float)key) >> 15);
 }
 
+// Block-exclusive prefix sum of one value per thread (NT threads); *all = the block total.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_resid_hist(Rows rows, int N, SolveState st, KParams kp) {
+__device__ unsigned block_exscan(unsigned v, unsigned* wsum, unsigned* all) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
+    }
+    __syncthreads();
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    unsigned before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        before += w < wv ? wsum[w] : 0u;
+        tot += wsum[w];
+    }
+    *all = tot;
+    return before + inc - v;
+}
+
+// Locate the bins holding ranks `lower` and `upper` (st.sel[4..5]) → st.sel[0..3]: a scan of the
+// 256 coarse bins (256 fine bins each) finds the coarse bin of each rank, a scan of that coarse
+// bin's fine bins the fine one.  One block of kCoarse threads; k_collect re-zeroes both levels.
+constexpr int kCoarse = kHistBins / 256;
+__global__ __launch_bounds__(kCoarse) void k_find_bins(SolveState st) {
     if (*st.done) return;
-    const int i = blockIdx.x * NT + threadIdx.x;
-    if (i < N) {
+    __shared__ unsigned wsum[kCoarse / 64];
+    __shared__ int cb[2];
+    __shared__ unsigned cbase[2];
+    const int t = threadIdx.x;
+    const unsigned c = st.coarse[t];
+    unsigned all = 0;
+    const unsigned ex = block_exscan<kCoarse>(c, wsum, &all);
+    const long long rank[2] = {st.sel[4], st.sel[5]};
+#pragma unroll
+    for (int w = 0; w < 2; ++w)
+        if (rank[w] >= (long long)ex && rank[w] < (long long)ex + c) { cb[w] = t; cbase[w] = ex; }
+    if (t == 0) {
+        if (rank[0] >= (long long)all) { st.sel[0] = -1; st.sel[2] = 0; cb[0] = -1; }   // N = 0
+        if (rank[1] >= (long long)all) { st.sel[1] = -1; st.sel[3] = 0; cb[1] = -1; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+        const int cw = cb[w];                                  // block-uniform
+        if (cw < 0) continue;
+        const unsigned f = st.hist[cw * 256 + t];
+        unsigned fall = 0;
+        const unsigned fex = block_exscan<kCoarse>(f, wsum, &fall) + cbase[w];
+        if (rank[w] >= (long long)fex && rank[w] < (long long)fex + f) {
+            st.sel[w] = cw * 256 + t;
+            st.sel[2 + w] = (int)fex;
+        }
+    }
+}
+
+// |r| under the first solution (solver.cpp:110) and its histogram.  Each block privatises the
+// histogram window that holds realistic residuals (kResidWin bins from kResidWinLo, 2^-64 ≤ |r|
+// < 2^64) in LDS and flushes its non-zero bins once: a global bin then takes at most one atomic
+// per block instead of one per row (the hot bins near the residual mode serialised ~thousands).
+constexpr int kResidBlock = 1024;
+constexpr int kResidBlocks = 96;
+constexpr int kResidWin = 16384;                          // 128 octaves of 1/128-octave bins
+constexpr int kResidWinLo = (0x1F800000 >> 15);           // key_bin(2^-64)
+__global__ __launch_bounds__(kResidBlock) void k_resid_hist(Rows rows, int N, SolveState st, KParams kp) {
+    if (*st.done) return;
+    __shared__ unsigned h[kResidWin];
+    for (int k = threadIdx.x; k < kResidWin / 4; k += kResidBlock) reinterpret_cast<uint4*>(h)[k] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    for (int i = blockIdx.x * kResidBlock + threadIdx.x; i < N; i += gridDim.x * kResidBlock) {
         double a[6], b, wt;
         double key = -1.0;
         if (rows.get(i, a, b, wt)) {
             double v = a[0] * st.x0[0];
             for (int k = 1; k < 6; ++k) v = v + a[k] * st.x0[k];
             key = fabs(v - b);
-            atomicAdd(&st.hist[min(key_bin(key), kHistBins - 1)], 1u);
+            const int bin = min(key_bin(key), kHistBins - 1);
+            const unsigned w = (unsigned)(bin - kResidWinLo);
+            if (w < (unsigned)kResidWin) {
+                atomicAdd(&h[w], 1u);
+            } else {
+                atomicAdd(&st.hist[bin], 1u);
+                atomicAdd(&st.coarse[bin >> 8], 1u);
+            }
         }
         st.keys[i] = key;
     }
-}
-
-// One block: locate the bins holding ranks `lower` and `upper` (st.sel[4..5]) → st.sel[0..3].
-constexpr int kFindBlock = 1024;
-__global__ __launch_bounds__(kFindBlock) void k_find_bins(SolveState st) {
-    if (*st.done) return;
-    constexpr int kPer = kHistBins / kFindBlock;
-    __shared__ unsigned csum[kFindBlock];
-    unsigned loc[kPer];
-    unsigned tot = 0;
-    const uint4* h4 = reinterpret_cast<const uint4*>(st.hist) + threadIdx.x * (kPer / 4);
+    __syncthreads();
+    // flush, coalesced (one atomic instruction per wave and 64 bins: device-scope atomics are
+    // costly on MI355X); the window's coarse sums go through LDS and out as ONE more instruction
+    static_assert(kResidWinLo % 256 == 0 && kResidWin % kResidBlock == 0 && kResidWin / 256 == 64, "window layout");
+    __shared__ unsigned csh[kResidWin / 256];
+    if (threadIdx.x < kResidWin / 256) csh[threadIdx.x] = 0u;
+    __syncthreads();
+    for (int k = threadIdx.x; k < kResidWin; k += kResidBlock) {
+        const unsigned v = h[k];
+        if (v) atomicAdd(&st.hist[kResidWinLo + k], v);
+        unsigned csum = v;
 #pragma unroll
-    for (int k = 0; k < kPer / 4; ++k) {
-        const uint4 v = h4[k];
-        loc[4 * k] = v.x; loc[4 * k + 1] = v.y; loc[4 * k + 2] = v.z; loc[4 * k + 3] = v.w;
-        tot += v.x + v.y + v.z + v.w;
-    }
-    csum[threadIdx.x] = tot;
-    __syncthreads();
-    for (int off = 1; off < kFindBlock; off <<= 1) {         // inclusive Hillis-Steele scan
-        const unsigned v = threadIdx.x >= off ? csum[threadIdx.x - off] : 0u;
-        __syncthreads();
-        csum[threadIdx.x] += v;
-        __syncthreads();
-    }
-    const long long lo = st.sel[4], hi = st.sel[5];
-    long long cum = (long long)csum[threadIdx.x] - tot;       // exclusive prefix of this chunk
-    if (threadIdx.x == 0 && lo >= (long long)csum[kFindBlock - 1]) { st.sel[0] = -1; st.sel[2] = 0; }   // N = 0
-    if (threadIdx.x == 0 && hi >= (long long)csum[kFindBlock - 1]) { st.sel[1] = -1; st.sel[3] = 0; }
-    if (lo < cum + (long long)tot || hi < cum + (long long)tot) {
-        for (int k = 0; k < kPer; ++k) {
-            const long long c = loc[k];
-            if (lo >= cum && lo < cum + c) { st.sel[0] = threadIdx.x * kPer + k; st.sel[2] = (int)cum; }
-            if (hi >= cum && hi < cum + c) { st.sel[1] = threadIdx.x * kPer + k; st.sel[3] = (int)cum; }
-            cum += c;
-        }
-    }
-}
-
-// Reduce rows strictly between the boundary bins; collect the boundary rows.
-template <int NT>
-__global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
-    if (*st.done) return;
-    __shared__ double red[(NT / 64) * kNormEq];
-    const int blo = st.sel[0], bhi = st.sel[1];
-    double acc[kNormEq];
-    for (int k = 0; k < kNormEq; ++k) acc[k] = 0.0;
-    for (int i = blockIdx.x * NT + threadIdx.x; i < N; i += gridDim.x * NT) {
-        const double key = st.keys[i];
-        if (key < 0) continue;
-        const int bin = min(key_bin(key), kHistBins - 1);
-        if (bin > blo && bin < bhi) {
-            double a[6], b, wt;
-            rows.get(i, a, b, wt);
-            int k = 0;
-            for (int r = 0; r < 6; ++r)
-                for (int c = r; c < 6; ++c) acc[k++] += a[r] * a[c];
-            for (int r = 0; r < 6; ++r) acc[21 + r] += a[r] * b;
-            acc[27] += 1.0;
-        } else if (bin == blo || bin == bhi) {
-            const int which = (bin == blo) ? 0 : 1;
-            const unsigned pos = atomicAdd(&st.cand_count[which], 1u);
-            if (pos < (unsigned)kCandCap) {
-                unsigned long long* ck = which ? st.cand_hi : st.cand_lo;
-                unsigned* cr = which ? st.cand_hi_row : st.cand_lo_row;
-                ck[pos] = (unsigned long long)__double_as_longlong(key);
-                cr[pos] = (unsigned)i;
-            }
-        }
-    }
-    // block reduction of the 28 partial sums
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int k = 0; k < kNormEq; ++k) {
-        const double v = wave_sum(acc[k]);
-        if (lane == 0) red[wv * kNormEq + k] = v;
+        for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o, 64);
+        if ((threadIdx.x & 63) == 0 && csum) atomicAdd(&csh[k >> 8], csum);
     }
     __syncthreads();
-    if (threadIdx.x < kNormEq) {
-        double s = 0.0;
-        for (int w = 0; w < NT / 64; ++w) s += red[w * kNormEq + threadIdx.x];
-        partial2[(size_t)blockIdx.x * kNormEq + threadIdx.x] = s;
-    }
+    if (threadIdx.x < kResidWin / 256 && csh[threadIdx.x]) atomicAdd(&st.coarse[(kResidWinLo >> 8) + threadIdx.x], csh[threadIdx.x]);
 }
 
 // bitonic sort of n (power of two ≤ kCandCap) (key, row) pairs in LDS, ascending
@@ -267,17 +245,14 @@ __device__ __forceinline__ bool pair_le(unsigned long long ka, unsigned ra, unsi
     return ka < kb || (ka == kb && ra <= rb);
 }
 
-__global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, SolveState st, imls_iter_trace* tr,
-                                                            const double* __restrict__ partial2, int nparts, KParams kp,
-                                                            int update_pose) {
-    if (*st.done) return;
-    __shared__ unsigned long long ck[kCandCap];
-    __shared__ unsigned cr[kCandCap];
-    __shared__ double red[(kFinalBlock / 64) * kNormEq];
-    __shared__ double out[kNormEq];
-    __shared__ unsigned long long shc;
-    __shared__ unsigned long long selk[2];
-    __shared__ unsigned selr[2];
+// The trimmed second solve (solver.cpp:124-166) by one block of NT threads, after k_collect:
+// boundary candidates sorted by (|r| bits, row), exact ranks kept, interior partials added,
+// solve6, Δ, pose update.  LDS: ck/cr [kCandCap], red [(NT/64)·28], out [28], shc, selk/selr [2].
+template <int NT>
+__device__ void final_block(const Rows& rows, int N, SolveState st, imls_iter_trace* tr,
+                            const double* __restrict__ partial2, int nparts, const KParams& kp, int update_pose,
+                            unsigned long long* ck, unsigned* cr, double* red, double* out, unsigned long long& shc,
+                            unsigned long long* selk, unsigned* selr) {
     const int blo = st.sel[0], bhi = st.sel[1];
     const long long clo = st.sel[2], chi = st.sel[3], lo = st.sel[4], hi = st.sel[5];
     const unsigned n_lo = st.cand_count[0], n_hi = st.cand_count[1];
@@ -302,14 +277,14 @@ __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, S
             while (np < (int)n) np <<= 1;
             const unsigned long long* gk = which ? st.cand_hi : st.cand_lo;
             const unsigned* gr = which ? st.cand_hi_row : st.cand_lo_row;
-            for (int i = threadIdx.x; i < np; i += kFinalBlock) {
+            for (int i = threadIdx.x; i < np; i += NT) {
                 ck[i] = i < (int)n ? gk[i] : ~0ull;
                 cr[i] = i < (int)n ? gr[i] : ~0u;
             }
             __syncthreads();
             bitonic(ck, cr, np);
             const long long base = which ? chi : clo;
-            for (int i = threadIdx.x; i < (int)n; i += kFinalBlock) {
+            for (int i = threadIdx.x; i < (int)n; i += NT) {
                 const long long rank = base + i;
                 if (rank >= lo && rank <= hi) add_row(cr[i]);
             }
@@ -320,7 +295,7 @@ __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, S
         rank_select(st.keys, N, lo, &selk[0], &selr[0], &shc);
         rank_select(st.keys, N, hi, &selk[1], &selr[1], &shc);
         __syncthreads();
-        for (int i = threadIdx.x; i < N; i += kFinalBlock) {
+        for (int i = threadIdx.x; i < N; i += NT) {
             const double key = st.keys[i];
             if (key < 0) continue;
             const int bin = min(key_bin(key), kHistBins - 1);
@@ -330,10 +305,10 @@ __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, S
         }
     }
     // the interior partials from k_collect, then one block reduction
-    for (int q = threadIdx.x; q < nparts; q += kFinalBlock)
+    for (int q = threadIdx.x; q < nparts; q += NT)
 #pragma unroll
         for (int k = 0; k < kNormEq; ++k) accA[k] += partial2[(size_t)q * kNormEq + k];
-    block_sum28<kFinalBlock>(accA, red, out);
+    block_sum28<NT>(accA, red, out);
     if (threadIdx.x != 0) return;
     double x[6], D[16];
     solve6(out, x);
@@ -341,12 +316,75 @@ __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, S
     finish_iteration(st, tr, D, (double)st.sel[6], out[27], update_pose, kp);
 }
 
+// Reduce rows strictly between the boundary bins; collect the boundary rows.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
+    if (*st.done) return;
+    __shared__ double red[(NT / 64) * kNormEq];
+    // the histogram was read by k_find_bins: zero it for the next solve
+    for (int b = blockIdx.x * NT + threadIdx.x; b < kHistBins / 4; b += gridDim.x * NT)
+        reinterpret_cast<uint4*>(st.hist)[b] = make_uint4(0u, 0u, 0u, 0u);
+    if (blockIdx.x == 0) for (int b = threadIdx.x; b < kHistBins / 256; b += NT) st.coarse[b] = 0u;
+    const int blo = st.sel[0], bhi = st.sel[1];
+    double acc[kNormEq];
+    for (int k = 0; k < kNormEq; ++k) acc[k] = 0.0;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < N; i += gridDim.x * NT) {
+        const double key = st.keys[i];
+        if (key < 0) continue;
+        const int bin = min(key_bin(key), kHistBins - 1);
+        if (bin > blo && bin < bhi) {
+            double a[6], b, wt;
+            rows.get(i, a, b, wt);
+            int k = 0;
+            for (int r = 0; r < 6; ++r)
+                for (int c = r; c < 6; ++c) acc[k++] += a[r] * a[c];
+            for (int r = 0; r < 6; ++r) acc[21 + r] += a[r] * b;
+            acc[27] += 1.0;
+        } else if (bin == blo || bin == bhi) {
+            const int which = (bin == blo) ? 0 : 1;
+            const unsigned pos = atomicAdd(&st.cand_count[which], 1u);
+            if (pos < (unsigned)kCandCap) {
+                unsigned long long* ck = which ? st.cand_hi : st.cand_lo;
+                unsigned* cr = which ? st.cand_hi_row : st.cand_lo_row;
+                ck[pos] = (unsigned long long)__double_as_longlong(key);
+                cr[pos] = (unsigned)i;
+            }
+        }
+    }
+    // block reduction of the 28 partial sums
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k = 0; k < kNormEq; ++k) {
+        const double v = wave_sum(acc[k]);
+        if (lane == 0) red[wv * kNormEq + k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNormEq) {
+        double s = 0.0;
+        for (int w = 0; w < NT / 64; ++w) s += red[w * kNormEq + threadIdx.x];
+        partial2[(size_t)blockIdx.x * kNormEq + threadIdx.x] = s;
+    }
+}
+
+constexpr int kFinalBlock = 1024;
+__global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, SolveState st, imls_iter_trace* tr,
+                                                            const double* __restrict__ partial2, int nparts, KParams kp,
+                                                            int update_pose) {
+    if (*st.done) return;
+    __shared__ unsigned long long ck[kCandCap];
+    __shared__ unsigned cr[kCandCap];
+    __shared__ double red[(kFinalBlock / 64) * kNormEq];
+    __shared__ double out[kNormEq];
+    __shared__ unsigned long long shc;
+    __shared__ unsigned long long selk[2];
+    __shared__ unsigned selr[2];
+    final_block<kFinalBlock>(rows, N, st, tr, partial2, nparts, kp, update_pose, ck, cr, red, out, shc, selk, selr);
+}
+
 // Small systems (≤ kSmallRows rows, e.g. the ≤2000-query frames of the config-C stream): the whole
 // LS solve in ONE block — reduce the pass-1 slabs, first solve, |r| keys of the valid rows into
 // LDS, bitonic sort by (|r| bits, row), ranks [lo, hi] re-reduced, second solve, pose update —
 // instead of five launches whose fixed latency dominates at this size.  Same arithmetic and the
 // same exact (|r|, row) order as the chain.
-constexpr int kSmallRows = 4096;      // rows the single-block solve holds in LDS (keys, rows, boundary candidates)
 constexpr int kSmallBlock = 256;     // 4 waves: cheap barriers for the sort and reductions
 constexpr int kSmallBins = 4096;     // LDS histogram: top 12 bits of the float image of |r| (1/16 octave)
 __device__ __forceinline__ int small_bin(unsigned long long keybits) {
@@ -537,9 +575,9 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
     }
     k_solve_first<<<1, 256, 0, s>>>(st.partial1, blocks1, st, tr, kp, weighted, update_pose);
     if (weighted) return;
-    k_resid_hist<kBlock><<<solve_blocks(N), kBlock, 0, s>>>(rows, N, st, kp);
+    k_resid_hist<<<std::min(kResidBlocks, (N + kResidBlock - 1) / kResidBlock), kResidBlock, 0, s>>>(rows, N, st, kp);
     const int cb = std::max(1, std::min(kCollectBlocks, (N + kBlock * 4 - 1) / (kBlock * 4)));
-    k_find_bins<<<1, kFindBlock, 0, s>>>(st);
+    k_find_bins<<<1, kCoarse, 0, s>>>(st);
     k_collect<kBlock><<<cb, kBlock, 0, s>>>(rows, N, st, st.partial2);
     k_solve_final<<<1, kFinalBlock, 0, s>>>(rows, N, st, tr, st.partial2, cb, kp, update_pose);
 }

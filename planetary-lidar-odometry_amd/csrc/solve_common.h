@@ -263,6 +263,48 @@ __device__ inline void finish_iteration(SolveState st, imls_iter_trace* tr, cons
 }
 
 
+// The first LS solve (or the only one, weighted LS) over `blocks` pass-1 slabs, by one block of
+// NT threads: reduce, too-few gate (laser_odometry.cpp:570-576), solve6, and for LS the trim
+// ranks (solver.cpp:118-134, Q11) for the selection that follows.  red: LDS [(NT/64)·28],
+// acc: LDS [28].  Run by k_solve_first.
+template <int NT>
+__device__ void solve_first_block(const double* __restrict__ partial, int blocks, SolveState st, imls_iter_trace* tr,
+                                  const KParams& kp, int weighted, int update_pose, double* red, double* acc) {
+    const int t = threadIdx.x;
+    double loc[kNormEq];
+#pragma unroll
+    for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
+    for (int b = t; b < blocks; b += NT)
+#pragma unroll
+        for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
+    if (t < 2) st.cand_count[t] = 0u;
+    block_sum28<NT>(loc, red, acc);
+    if (t != 0) return;
+    const double nvalid = acc[27];
+    if (update_pose && nvalid < (double)kp.correspond_number) {
+        *st.status = IMLS_FRAME_TOO_FEW;
+        *st.done = 1;
+        if (tr) tr->n_valid = (unsigned long long)nvalid;
+        return;
+    }
+    double x[6];
+    solve6(acc, x);
+    if (weighted) {
+        double D[16];
+        delta_from_x(x, D);
+        finish_iteration(st, tr, D, nvalid, nvalid, update_pose, kp);
+        return;
+    }
+    for (int k = 0; k < 6; ++k) st.x0[k] = x[k];
+    const long long N = (long long)nvalid;
+    long long lo = (long long)(kp.ls_threshold * (double)N);
+    long long hi = (long long)((1 - kp.ls_threshold) * (double)N);
+    if (hi > N - 1) hi = N - 1;       // Q11
+    st.sel[4] = (int)lo;
+    st.sel[5] = (int)hi;
+    st.sel[6] = (int)N;
+}
+
 // Cyclic Jacobi on a symmetric N×N (ascending eigenvalues, eigenvectors as columns:
 // U[c·N + r]); identical sweep order to the oracle's sym_eig (Eigen SelfAdjointEigenSolver order).
 template <int N>
