@@ -294,8 +294,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float
                                                          const double* __restrict__ delta,
                                                          int* __restrict__ lists, float* __restrict__ wlist,
                                                          float4* __restrict__ xref, float* __restrict__ nref,
-                                                         int use_prev, unsigned long long* __restrict__ nbr_stats) {
+                                                         int use_prev, unsigned long long* __restrict__ nbr_stats,
+                                                         unsigned* __restrict__ fb_count) {
     if (done && *done) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = 0u;   // k_finish's deferred-query counter
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float4 sbox[kWaveBlock / 64][kWaveStack][2];
     __shared__ float4 sleaf[kWaveBlock / 64][64];   // the current leaf's points (lockstep insertion)
@@ -723,9 +725,11 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
                                                           const double* __restrict__ delta,
                                                           int* __restrict__ lists, float* __restrict__ wlist,
                                                           float4* __restrict__ xref, float* __restrict__ nref,
-                                                          int use_prev, unsigned long long* __restrict__ nbr_stats) {
+                                                          int use_prev, unsigned long long* __restrict__ nbr_stats,
+                                                          unsigned* __restrict__ fb_count) {
     static_assert(KL <= 64, "one list entry per lane");
     if (done && *done) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = 0u;   // k_finish's deferred-query counter
     __shared__ int snode[kWaveBlock / 64][kStackDepth];
     __shared__ float sdist[kWaveBlock / 64][kStackDepth];
     const int lane = threadIdx.x & 63;
@@ -1181,13 +1185,14 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
     // dense scans: packets of 64 Morton-coherent queries
     if (kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
-                                                                                          delta, lists, wlist, xref, nref, use_prev, stats);
+                                                                                          delta, lists, wlist, xref, nref, use_prev, stats,
+                                                                                          fb_count);
     else if (kp.lockstep)
         k_knn_wave<KL, true><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
-                                                          nref, use_prev, stats);
+                                                          nref, use_prev, stats, fb_count);
     else
         k_knn_wave<KL, false><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
-                                                           nref, use_prev, stats);
+                                                           nref, use_prev, stats, fb_count);
     if (marks) (void)hipEventRecord(marks[1], s);
     k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,
                                                stats, fb_list, fb_count);
@@ -1217,7 +1222,7 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
         else launch_lane<32>(s, kFallbackBlocks, t, spt, snr, nullptr, nullptr, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
         return;
     }
-    (void)hipMemsetAsync(fb_count, 0, sizeof(unsigned), s);
+    // (fb_count is re-zeroed by the traversal kernel's first thread)
     if (K <= 8) launch_wave<12>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else if (K <= 20) launch_wave<24>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);

@@ -365,7 +365,7 @@ __global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st,
     }
 }
 
-constexpr int kFinalBlock = 1024;
+constexpr int kFinalBlock = 256;
 __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, SolveState st, imls_iter_trace* tr,
                                                             const double* __restrict__ partial2, int nparts, KParams kp,
                                                             int update_pose) {
