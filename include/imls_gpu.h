@@ -232,11 +232,59 @@ int imls_register_frame_async(imls_ctx* ctx);
 int imls_register_frame_result(imls_ctx* ctx, double pose_out[16], int* iters_run, int* status,
                                imls_iter_trace* trace);
 
+/* ---- upstream producer: ring-neighbourhood PCA normals (scan_registration) ------------- */
+/* scan_registration.compute_normal_method.pca + presample_method.geometric_features
+ * (config.json; read at scan_registration.cpp:1140-1145, 1451, 1133).  imls_default_pca_params()
+ * fills the shipped values. */
+typedef struct imls_pca_params {
+    int32_t window_size;            /* pca.window_size = 3 */
+    int32_t iter_step;              /* pca.iter_step = 1 */
+    float knn_distance_threshold;   /* pca.knn_distance_threshold = 10 (vs the SQUARED NN distance,
+                                       which is what pcl::KdTreeFLANN::nearestKSearch returns) */
+    int32_t neighbor_scan;          /* pca.neighbor_scan: 0 = "kdtree", 1 = "index" */
+    float distance_threshold;       /* pca.plane_constraint.distance_threshold = 0.02 */
+    float valid_points_threshold;   /* pca.plane_constraint.valid_points_threshold = 0.8 */
+    int32_t use_all_points;         /* model.use_all_points = true */
+    float planarity_threshold;      /* presample_method.geometric_features.planarity_threshold = 0.05 */
+} imls_pca_params;
+void imls_default_pca_params(imls_pca_params* p);
+
+/* Output flags of imls_ring_normals_pca. */
+enum {
+    IMLS_PCA_PLANE_INVALID = 1,     /* failed checkPlaneValidity: eigenvalues (-1,-1,-1), normal = the
+                                       largest-eigenvalue axis (scan_registration.cpp:215-218, 1182-1196) */
+    IMLS_PCA_CANDIDATE = 2          /* presample candidate: planarity > threshold and not invalid
+                                       (computeGeometricFeatures 321-326; erase 1481-1489) */
+};
+
+/* Replaces the point-cloud / "pca" branch of scan_registration.cpp's normal estimation
+ * (1136-1229: computeNormalPCA 158-229 with findNearestPoint 117-136 and checkPlaneValidity
+ * 138-156) followed by the geometric-features presample (computeGeometricFeatures 279-327, the
+ * invalid-index erase 1481-1489).
+ *   xyz: the ring-concatenated cloud `laserCloud` (1064-1069), point i at xyz + i*stride_floats;
+ *   ring_sizes[n_rings]: points per scan line, in ring order (laserCloudScans[i].size()).
+ * Outputs (capacity = the number of input points; each nullable) are the rows of
+ * filteredLaserCloud / eigenvalues_matrix / eigenvectors_matrix in the reference's push order:
+ *   index_out[r]  = filteredIndices (= scanStartInd[i] + j, which is 5 past the PCA centre j:
+ *                   the reference's own offset, SURVEY Appendix B "Q-SR1"; the point's xyz,
+ *                   intensity and curvature come from that index, 1210-1220);
+ *   normal_out[3r] (flipped to +z), evals_out[3r] = (λ1, λ2, λ3) descending or (-1,-1,-1),
+ *   evecs_out[9r] = the 3×3 eigenvector matrix column-major as 1205-1207 stores it,
+ *   features_out[8r] = sum, omnivariance, eigenentropy, anisotropy, linearity, planarity,
+ *                   surface variation, sphericity (279-319), flags_out[r] (IMLS_PCA_*).
+ * counters[2] (nullable): pca_failure (1179), plane-check failures (1186; counted whether or
+ * not use_all_points keeps them).  Requires n_rings ≤ 4096 and ring sizes ≤ 1<<20. */
+int imls_ring_normals_pca(imls_ctx* ctx, const imls_pca_params* p, const float* xyz, size_t stride_floats,
+                          const int32_t* ring_sizes, int32_t n_rings, uint32_t* index_out, float* normal_out,
+                          float* evals_out, float* evecs_out, float* features_out, uint8_t* flags_out,
+                          size_t* n_out, uint64_t counters[2]);
+
 /* ---- instrumentation ------------------------------------------------------------------- */
 /* When enabled, HIP events bracket every launch of the projection kernel (on the stream it is
  * launched on); imls_kernel_timing returns the accumulated milliseconds and launch count since
  * the last reset.  kernel: 0 = projection (all its kernels), 1 = index build (all its kernels),
- * 2 = solve chain, 3 = k_knn_wave (packet traversal) alone, 4 = k_finish (exact stage) alone. */
+ * 2 = solve chain, 3 = k_knn_wave (packet traversal) alone, 4 = k_finish (exact stage) alone,
+ * 5 = k_ring_pca (imls_ring_normals_pca's kernel). */
 int imls_enable_timing(imls_ctx* ctx, int enable);
 int imls_kernel_timing(imls_ctx* ctx, int kernel, double* total_ms, uint64_t* launches);
 int imls_reset_timing(imls_ctx* ctx);

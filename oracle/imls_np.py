@@ -308,3 +308,74 @@ def tv_encode_pca(evals: np.ndarray, evecs: np.ndarray, k: int) -> np.ndarray:
     ok = (l1 >= l2) & (l2 >= l3)
     out[~ok] = np.array([1, 0, 0, 1, 0, 1], np.float32)
     return out
+
+
+def ring_pca_np(xyz, ring_sizes, window_size=3, iter_step=1, knn_distance_threshold=10.0, neighbor_scan="kdtree",
+                distance_threshold=0.02, valid_points_threshold=0.8, use_all_points=True, planarity_threshold=0.05):
+    """Independent restatement of scan_registration.cpp's "pca" normals (1136-1229; computeNormalPCA
+    158-229, findNearestPoint 117-136, checkPlaneValidity 138-156) + computeGeometricFeatures
+    (279-327): NN-1 by scipy cKDTree on each line (re-ranked with the float L2 the reference's
+    FLANN tree uses), covariance and plane check in float32 numpy, eigen-decomposition by
+    numpy.linalg.eigh in float64.  Returns (index, normal, evals, flags, pca_failure, invalid)."""
+    xyz = np.asarray(xyz, np.float32)[:, :3]
+    sizes = [int(v) for v in ring_sizes]
+    start = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    rings = [xyz[start[i]:start[i + 1]] for i in range(len(sizes))]
+    trees = [cKDTree(r.astype(np.float64)) if len(r) else None for r in rings]
+    num = 3 * (int(2 * window_size / iter_step) + 1)
+    out_i, out_n, out_l, out_f = [], [], [], []
+    fail = invalid = 0
+
+    def nearest(q, a):
+        if neighbor_scan == "index":
+            return True, None
+        if trees[a] is None:
+            return False, None
+        k = min(8, len(rings[a]))
+        _, cand = trees[a].query(q.astype(np.float64), k=k)
+        cand = np.sort(np.atleast_1d(cand))
+        d = rings[a][cand] - q                      # float32, ((0 + d0²) + d1²) + d2²
+        d2 = ((np.float32(0) + d[:, 0] * d[:, 0]) + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+        b = int(np.argmin(d2))                     # first minimum = lowest index among ties
+        return bool(d2[b] < np.float32(knn_distance_threshold)), int(cand[b])
+
+    for i in range(1, len(sizes) - 1):
+        if sizes[i] == 0 or sizes[i] - 11 < 6 or sizes[i - 1] - 11 < 6 or sizes[i + 1] - 11 < 6:
+            continue
+        for j in range(5, sizes[i] - 5):
+            pts = [rings[i][j + k] for k in range(-window_size, window_size + 1, iter_step) if 0 <= j + k < sizes[i]]
+            for a in (i - 1, i + 1):
+                ok, nb = nearest(rings[i][j], a)
+                if not ok:
+                    continue
+                nb = j if nb is None else nb
+                pts += [rings[a][nb + k] for k in range(-window_size, window_size + 1, iter_step)
+                        if 0 <= nb + k < sizes[a]]
+            if len(pts) < num:
+                fail += 1
+                continue
+            P = np.array(pts, np.float32)
+            c = P.mean(axis=0, dtype=np.float64)
+            C = (P - c).T.astype(np.float64) @ (P - c) / (len(P) - 1)
+            w, V = np.linalg.eigh(C)
+            dist = np.abs((P - c) @ V[:, 0])
+            good = np.count_nonzero(dist < distance_threshold) >= valid_points_threshold * len(P)
+            if not good:
+                invalid += 1
+                if not use_all_points:
+                    continue
+                lam = np.array([-1.0, -1.0, -1.0])
+                nrm = V[:, 2]
+            else:
+                lam = w[::-1]
+                nrm = V[:, 0]
+            nrm = nrm / np.linalg.norm(nrm)
+            if nrm[2] < 0:
+                nrm = -nrm
+            l1, l2, l3 = lam
+            plan = (l2 - l3) / l1
+            out_i.append(start[i] + 5 + j)
+            out_n.append(nrm); out_l.append(lam)
+            out_f.append((1 if not good else 0) | (2 if (good and plan > planarity_threshold) else 0))
+    return (np.array(out_i, np.int64), np.array(out_n).reshape(-1, 3), np.array(out_l).reshape(-1, 3),
+            np.array(out_f, np.uint8), fail, invalid)

@@ -50,6 +50,8 @@ def lib():
         L.oracle_colpiv_qr_solve.argtypes = [VP, C.c_int, C.c_int, VP, VP]
         L.oracle_delta_from_x.argtypes = [VP, VP]
         L.oracle_sym_eig6.argtypes = [VP, VP, VP]
+        L.oracle_ring_pca.argtypes = [VP, SZ, VP, C.c_int32, P(abi.ImlsPcaParams), VP, VP, VP, VP, VP, VP, VP,
+                                      P(SZ), VP]
         _lib = L
     return _lib
 
@@ -158,3 +160,20 @@ def delta_from_x(x):
     x = np.ascontiguousarray(x, dtype=np.float64); D = np.zeros(16)
     lib().oracle_delta_from_x(_ptr(x), _ptr(D))
     return D.reshape(4, 4)
+
+
+def ring_pca(xyz, ring_sizes, pca_params):
+    """scan_registration.cpp pca normals + geometric-features presample (scanreg_oracle.cpp).
+    Returns the same dict as ImlsContext.ring_normals_pca plus `margin` (plane-check margin)."""
+    a = np.ascontiguousarray(xyz, dtype=np.float32)
+    rs = np.ascontiguousarray(ring_sizes, dtype=np.int32)
+    n = max(a.shape[0], 1)
+    idx = np.zeros(n, np.uint32); nrm = np.zeros((n, 3), np.float32); ev = np.zeros((n, 3), np.float32)
+    evec = np.zeros((n, 9), np.float32); feat = np.zeros((n, 8), np.float32); fl = np.zeros(n, np.uint8)
+    mg = np.zeros(n, np.float32); cnt = np.zeros(2, np.uint64); nout = C.c_size_t()
+    rc = lib().oracle_ring_pca(_ptr(a), a.shape[1], _ptr(rs), len(rs), C.byref(pca_params), _ptr(idx), _ptr(nrm),
+                               _ptr(ev), _ptr(evec), _ptr(feat), _ptr(fl), _ptr(mg), C.byref(nout), _ptr(cnt))
+    assert rc == 0
+    k = nout.value
+    return dict(index=idx[:k], normal=nrm[:k], evals=ev[:k], evecs=evec[:k], features=feat[:k], flags=fl[:k],
+                margin=mg[:k], pca_failure=int(cnt[0]), plane_invalid=int(cnt[1]))

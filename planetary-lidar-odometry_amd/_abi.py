@@ -89,6 +89,27 @@ def default_params() -> ImlsParams:
     return p
 
 
+class ImlsPcaParams(C.Structure):
+    """imls_pca_params (include/imls_gpu.h): scan_registration.compute_normal_method.pca +
+    presample_method.geometric_features (config.json, read at scan_registration.cpp:1140-1145, 1451)."""
+    _fields_ = [("window_size", C.c_int32), ("iter_step", C.c_int32), ("knn_distance_threshold", C.c_float),
+                ("neighbor_scan", C.c_int32), ("distance_threshold", C.c_float),
+                ("valid_points_threshold", C.c_float), ("use_all_points", C.c_int32),
+                ("planarity_threshold", C.c_float)]
+
+
+IMLS_PCA_PLANE_INVALID, IMLS_PCA_CANDIDATE = 1, 2
+
+
+def default_pca_params() -> ImlsPcaParams:
+    """The shipped config.json values (imls_default_pca_params() in the library)."""
+    p = ImlsPcaParams()
+    p.window_size, p.iter_step, p.knn_distance_threshold, p.neighbor_scan = 3, 1, 10.0, 0
+    p.distance_threshold, p.valid_points_threshold = 0.02, 0.8
+    p.use_all_points, p.planarity_threshold = 1, 0.05
+    return p
+
+
 def _bind(lib: C.CDLL) -> C.CDLL:
     P, VP, SZ = C.POINTER, C.c_void_p, C.c_size_t
     sig = {
@@ -118,6 +139,9 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_reset_timing": (C.c_int, [VP]),
         "imls_index_stats": (C.c_int, [VP, VP]),
         "imls_traversal_stats": (C.c_int, [VP, VP]),
+        "imls_default_pca_params": (None, [P(ImlsPcaParams)]),
+        "imls_ring_normals_pca": (C.c_int, [VP, P(ImlsPcaParams), VP, SZ, VP, C.c_int32, VP, VP, VP, VP, VP, VP,
+                                            P(SZ), VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -133,7 +157,7 @@ ABI_SYMBOLS = (
     "imls_set_target_tensors_device", "imls_tv_encode_pca", "imls_project", "imls_solve",
     "imls_solve_correspondences", "imls_register_frame", "imls_register_frame_async",
     "imls_register_frame_result", "imls_enable_timing", "imls_kernel_timing", "imls_reset_timing",
-    "imls_index_stats", "imls_traversal_stats",
+    "imls_index_stats", "imls_traversal_stats", "imls_default_pca_params", "imls_ring_normals_pca",
 )
 
 _LIB = None

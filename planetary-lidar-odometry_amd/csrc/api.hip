@@ -14,7 +14,7 @@
 
 using namespace imlsgpu;
 
-constexpr int kTimingKinds = 5;   // projection, index, solve chain, k_knn_wave, k_finish
+constexpr int kTimingKinds = 6;   // projection, index, solve chain, k_knn_wave, k_finish, k_ring_pca
 
 struct imls_ctx {
     int device = 0;
@@ -39,6 +39,7 @@ struct imls_ctx {
     DevBuf tkept;                         // target: filtered index → input index (tensor upload)
     DevBuf mten, upload_ten;              // tensor voting: input tensors (Morton order) + upload staging
     DevBuf tvn;                           // tensor voting: per-source voted normal + found flag (double4)
+    DevBuf pca_mem;                       // imls_ring_normals_pca scratch (upstream producer)
     size_t n_target_in = 0;               // input size of the last set_target (tensor arrays match it)
     bool has_tensors = false;
     int lane_mode = 0;
@@ -508,7 +509,7 @@ void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
+    DevBuf* bufs[] = {&c->pca_mem, &c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
                       &c->upload_t, &c->spt, &c->snr, &c->sscratch,
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
@@ -791,6 +792,48 @@ int imls_register_frame(imls_ctx* c, double pose_out[16], int* iters_run, int* s
     int rc = imls_register_frame_async(c);
     if (rc) return rc;
     return imls_register_frame_result(c, pose_out, iters_run, status, trace);
+}
+
+void imls_default_pca_params(imls_pca_params* p) {
+    // scan_registration section of the shipped config.json (read at scan_registration.cpp:1140-1145, 1451, 1133)
+    if (!p) return;
+    p->window_size = 3;
+    p->iter_step = 1;
+    p->knn_distance_threshold = 10.f;
+    p->neighbor_scan = 0;
+    p->distance_threshold = 0.02f;
+    p->valid_points_threshold = 0.8f;
+    p->use_all_points = 1;
+    p->planarity_threshold = 0.05f;
+}
+
+int imls_ring_normals_pca(imls_ctx* c, const imls_pca_params* p, const float* xyz, size_t stride,
+                          const int32_t* ring_sizes, int32_t n_rings, uint32_t* index_out, float* normal_out,
+                          float* evals_out, float* evecs_out, float* features_out, uint8_t* flags_out, size_t* n_out,
+                          uint64_t counters[2]) {
+    if (!c) return IMLS_ERR_ARG;
+    if (!p || !ring_sizes || n_rings <= 0 || n_rings > 4096 || stride < 3)
+        return fail(c, IMLS_ERR_ARG, "bad pca params / ring sizes / stride");
+    if (p->window_size < 0 || p->iter_step <= 0 || p->neighbor_scan < 0 || p->neighbor_scan > 1)
+        return fail(c, IMLS_ERR_ARG, "bad pca window_size / iter_step / neighbor_scan");
+    long long total = 0;
+    for (int i = 0; i < n_rings; ++i) total += ring_sizes[i];
+    if (total > 0 && !xyz) return fail(c, IMLS_ERR_ARG, "null xyz");
+    if (total >= (1ll << 31)) return fail(c, IMLS_ERR_CAPACITY, "cloud too large");
+    if (int rc = check_device(c)) return rc;
+    int slot = -1;
+    hipEvent_t marks[2];
+    hipEvent_t* mk = nullptr;
+    if (c->timing && (slot = ev_pair(c)) >= 0) {
+        marks[0] = c->ev[slot];
+        marks[1] = c->ev[slot + 1];
+        c->ev_pairs[5].push_back({slot, slot + 1});
+        mk = marks;
+    }
+    int rc = ring_pca_run(c->stream, *p, xyz, stride, ring_sizes, n_rings, c->pca_mem, mk, index_out, normal_out,
+                          evals_out, evecs_out, features_out, flags_out, n_out, counters, c->err);
+    if (c->timing) harvest_timing(c);
+    return rc;
 }
 
 int imls_enable_timing(imls_ctx* c, int enable) {

@@ -198,4 +198,10 @@ void launch_solve(hipStream_t s, const SolveLaunch& L);
 size_t ransac_bytes(int cap);
 void ransac_seed_host(uint32_t seed, int st[34]);
 
+// scanreg.hip — ring-neighbourhood PCA normals + geometric-features presample (imls_ring_normals_pca)
+int ring_pca_run(hipStream_t s, const imls_pca_params& p, const float* xyz, size_t stride, const int32_t* sizes,
+                 int n_rings, DevBuf& mem, hipEvent_t* marks, uint32_t* index_out, float* normal_out,
+                 float* evals_out, float* evecs_out, float* features_out, uint8_t* flags_out, size_t* n_out,
+                 uint64_t counters[2], std::string& err);
+
 }  // namespace imlsgpu

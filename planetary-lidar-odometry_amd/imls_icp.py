@@ -181,6 +181,31 @@ class ImlsContext:
         return pose.reshape(4, 4), iters.value, status.value
 
     # -- instrumentation ------------------------------------------------------------------------
+    def ring_normals_pca(self, xyz, ring_sizes, pca_params: Optional[_abi.ImlsPcaParams] = None) -> dict:
+        """scan_registration.cpp's "pca" normal estimation + geometric-features presample (1136-1229,
+        279-327, 1481-1489) on the ring-concatenated cloud `laserCloud` (1064-1069).
+        xyz: (n, 3+) float32 (stride = its row length); ring_sizes: points per scan line.
+        Returns the filteredLaserCloud rows: index (into xyz; = PCA centre + 5, the reference's own
+        offset), normal, evals, evecs (3x3 column-major), features (8), flags (IMLS_PCA_*), plus
+        the pca_failure / plane-check counters."""
+        a = np.ascontiguousarray(xyz, dtype=np.float32)
+        if a.ndim != 2 or a.shape[1] < 3:
+            raise ValueError("xyz must be (n, >=3)")
+        rs = np.ascontiguousarray(ring_sizes, dtype=np.int32)
+        if int(rs.sum()) != a.shape[0]:
+            raise ValueError("ring sizes must sum to the number of points")
+        p = pca_params if pca_params is not None else _abi.default_pca_params()
+        n = max(a.shape[0], 1)
+        idx = np.zeros(n, np.uint32); nrm = np.zeros((n, 3), np.float32); ev = np.zeros((n, 3), np.float32)
+        evec = np.zeros((n, 9), np.float32); feat = np.zeros((n, 8), np.float32); fl = np.zeros(n, np.uint8)
+        cnt = np.zeros(2, np.uint64); nout = C.c_size_t()
+        self._check(self.lib.imls_ring_normals_pca(self.ctx, C.byref(p), _ptr(a), a.shape[1], _ptr(rs), len(rs),
+                                                   _ptr(idx), _ptr(nrm), _ptr(ev), _ptr(evec), _ptr(feat), _ptr(fl),
+                                                   C.byref(nout), _ptr(cnt)))
+        k = nout.value
+        return dict(index=idx[:k], normal=nrm[:k], evals=ev[:k], evecs=evec[:k], features=feat[:k], flags=fl[:k],
+                    pca_failure=int(cnt[0]), plane_invalid=int(cnt[1]))
+
     def enable_timing(self, on=True):
         self._check(self.lib.imls_enable_timing(self.ctx, int(on)))
 

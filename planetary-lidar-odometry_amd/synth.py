@@ -415,3 +415,13 @@ def make_planetary_pair(map_scans: int = 1, scene_seed: int = 3, start: int = 30
     pr.meta["tensors"] = imls_icp.tv_encode_pca(evals, evecs, tensor_k)
     pr.meta["pca"] = (evals, evecs)
     return pr
+
+
+def ring_cloud(model: str = "hdl64", scene_seed: int = 0, noise_seed: int | None = None):
+    """One sweep at the origin as the upstream producer's input: the ring-concatenated cloud
+    `laserCloud` (scan_registration.cpp:1064-1069) as (n, 3) float32 xyz, plus the points per scan
+    line (laserCloudScans[i].size())."""
+    m = hdl64() if model == "hdl64" else vlp16()
+    cl = scan(make_scene(scene_seed), m, pose_xyyaw(0, 0, 0), seed=1000 + scene_seed if noise_seed is None else noise_seed)
+    sizes = np.bincount(np.floor(cl["intensity"]).astype(np.int64), minlength=len(m.rings)).astype(np.int32)
+    return np.stack([cl["x"], cl["y"], cl["z"]], 1).astype(np.float32), sizes
