@@ -279,12 +279,49 @@ int imls_ring_normals_pca(imls_ctx* ctx, const imls_pca_params* p, const float* 
                           float* evals_out, float* evecs_out, float* features_out, uint8_t* flags_out,
                           size_t* n_out, uint64_t counters[2]);
 
+/* scan_registration.sample_method (config.json; samplePointCloud, scan_registration.cpp:761-806).
+ * imls_default_sample_params() fills the shipped values of the chosen method. */
+typedef enum imls_sample_method {
+    IMLS_SAMPLE_NORMAL = 0,         /* "normal" — and "major_axis" on the first frame (783) */
+    IMLS_SAMPLE_MAJOR_AXIS = 1      /* "major_axis" from the second frame on (791-801) */
+} imls_sample_method;
+typedef struct imls_sample_params {
+    int32_t method;                 /* imls_sample_method */
+    float r, r_proj;                /* major_axis.r = 0.5, major_axis.r_proj = 1.5 */
+    int32_t max_total_points;       /* major_axis.max_total_points = 2000 */
+    int32_t azimuth_bins, elevation_bins;            /* 8, 8 */
+    int32_t min_points_per_bin, max_points_per_bin;  /* normal: 20, 100; major_axis: 20, 200 */
+    int32_t sampling_strategy;      /* 0 = "FPS", 1 = "random" (normal: random; major_axis: FPS) */
+    uint32_t shuffle_seed;          /* randomSampling's std::mt19937 seed: call k of one imls_sample_
+                                       point_cloud uses shuffle_seed + k (the reference seeds each call
+                                       from std::random_device, 571-572: not reproducible) */
+    uint32_t rand_seed;             /* srand() seed of the glibc rand() stream farthestPointSampling
+                                       draws its first index from (common.cpp:49); re-seeded per call
+                                       (the reference's stream runs on across frames from seed 1) */
+} imls_sample_params;
+void imls_default_sample_params(imls_sample_params* p, int32_t method);
+
+/* Replaces samplePointCloud for "normal" / "major_axis" (scan_registration.cpp:761-806):
+ * computeSphericalHistogram (536-564) of the candidates' normals, then normalSampling (584-629) or
+ * majorAxisSampling (631-759) — per-bin random subsets, the brute-force average distance to the
+ * previous frame's cloud (679-701, on the GPU), bin weights, per-bin farthestPointSampling
+ * (common.cpp:19-82, on the GPU) or random sampling.
+ *   xyz/nrm: pcl_cloud (the filtered cloud), point i at xyz + i*stride_floats (nrm likewise);
+ *   candidates[n_cand]: candidate_indices into it; last_xyz[m]: last_pcl_cloud (major_axis only).
+ * sampled_out (capacity n_cand + azimuth_bins·elevation_bins) receives sampled_indices in the
+ * reference's order; bin_weights_out (nullable, azimuth_bins·elevation_bins floats) the normalised
+ * major_axis weights. */
+int imls_sample_point_cloud(imls_ctx* ctx, const imls_sample_params* p, const float* xyz, const float* nrm,
+                            size_t stride_floats, size_t n, const int32_t* candidates, size_t n_cand,
+                            const float* last_xyz, size_t last_stride_floats, size_t m, int32_t* sampled_out,
+                            size_t* n_sampled, float* bin_weights_out);
+
 /* ---- instrumentation ------------------------------------------------------------------- */
 /* When enabled, HIP events bracket every launch of the projection kernel (on the stream it is
  * launched on); imls_kernel_timing returns the accumulated milliseconds and launch count since
  * the last reset.  kernel: 0 = projection (all its kernels), 1 = index build (all its kernels),
  * 2 = solve chain, 3 = k_knn_wave (packet traversal) alone, 4 = k_finish (exact stage) alone,
- * 5 = k_ring_pca (imls_ring_normals_pca's kernel). */
+ * 5 = k_ring_pca (imls_ring_normals_pca), 6 = k_major_avg (imls_sample_point_cloud, major_axis). */
 int imls_enable_timing(imls_ctx* ctx, int enable);
 int imls_kernel_timing(imls_ctx* ctx, int kernel, double* total_ms, uint64_t* launches);
 int imls_reset_timing(imls_ctx* ctx);

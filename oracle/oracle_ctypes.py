@@ -50,6 +50,8 @@ def lib():
         L.oracle_colpiv_qr_solve.argtypes = [VP, C.c_int, C.c_int, VP, VP]
         L.oracle_delta_from_x.argtypes = [VP, VP]
         L.oracle_sym_eig6.argtypes = [VP, VP, VP]
+        L.oracle_sample_point_cloud.argtypes = [P(abi.ImlsSampleParams), VP, VP, SZ, SZ, VP, SZ, VP, SZ, SZ, VP,
+                                                P(SZ), VP]
         L.oracle_ring_pca.argtypes = [VP, SZ, VP, C.c_int32, P(abi.ImlsPcaParams), VP, VP, VP, VP, VP, VP, VP,
                                       P(SZ), VP]
         _lib = L
@@ -177,3 +179,18 @@ def ring_pca(xyz, ring_sizes, pca_params):
     k = nout.value
     return dict(index=idx[:k], normal=nrm[:k], evals=ev[:k], evecs=evec[:k], features=feat[:k], flags=fl[:k],
                 margin=mg[:k], pca_failure=int(cnt[0]), plane_invalid=int(cnt[1]))
+
+
+def sample_point_cloud(xyz, nrm, candidates, last_xyz, sample_params):
+    """samplePointCloud "normal" / "major_axis" (scanreg_oracle.cpp): (sampled indices, bin weights)."""
+    a = np.ascontiguousarray(xyz, dtype=np.float32); nn = np.ascontiguousarray(nrm, dtype=np.float32)
+    assert a.shape == nn.shape and a.shape[1] >= 3
+    cand = np.ascontiguousarray(candidates, dtype=np.int32)
+    last = np.ascontiguousarray(last_xyz if last_xyz is not None else np.zeros((0, 3)), dtype=np.float32)
+    nb = sample_params.azimuth_bins * sample_params.elevation_bins
+    out = np.zeros(len(cand) + nb + 1, np.int32); w = np.zeros(nb, np.float32); k = C.c_size_t()
+    rc = lib().oracle_sample_point_cloud(C.byref(sample_params), _ptr(a), _ptr(nn), a.shape[1], a.shape[0], _ptr(cand),
+                                         len(cand), _ptr(last), last.shape[1] if last.ndim == 2 else 3, last.shape[0],
+                                         _ptr(out), C.byref(k), _ptr(w))
+    assert rc == 0
+    return out[:k.value], w

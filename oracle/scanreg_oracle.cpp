@@ -11,12 +11,17 @@
 //     float: the two agree to float rounding of well-separated eigenpairs).  Eigen's vectorised
 //     colwise().mean() / adjoint()*matrix reductions are restated as sequential float sums.
 // Build: oracle/Makefile (one .so with imls_oracle.cpp).
+#include <algorithm>
 #include <cmath>
 #include <cstddef>
 #include <cstdint>
+#include <random>
 #include <vector>
 
 #include "../include/imls_gpu.h"
+
+extern "C" int32_t oracle_rand_next(int32_t* state);   // glibc rand() restatement (imls_oracle.cpp)
+extern "C" void oracle_rand_seed(int32_t* state, uint32_t seed);
 
 namespace {
 
@@ -159,6 +164,99 @@ PcaOut compute_normal_pca(const std::vector<const P3*>& rings, const std::vector
     return o;
 }
 
+// ---- samplePointCloud: "normal" / "major_axis" (scan_registration.cpp:536-806, common.cpp:19-82) ----
+//
+// Further unpinned semantics, beyond the two above: randomSampling seeds a fresh std::mt19937 from
+// std::random_device per call (571-572) — restated with the seed shuffle_seed + k for the k-th call
+// (same libstdc++ std::shuffle); farthestPointSampling's first index is rand() % n from the
+// process-wide glibc stream — restated from srand(rand_seed) per call.  Eigen float/double 3-vector
+// norms: Vector3f.norm() = sqrt(c0 + (c1 + c2)) (Redux.h non-vectorised unroller, size 3 < 4 floats),
+// Vector3d.norm() = sqrt((c0 + c1) + c2) (SSE2: one 2-double packet + the tail).
+
+struct SampleCloud {
+    const float* xyz;
+    const float* nrm;
+    size_t stride;
+    P3 p(size_t i) const { return {xyz[i * stride], xyz[i * stride + 1], xyz[i * stride + 2]}; }
+    P3 n(size_t i) const { return {nrm[i * stride], nrm[i * stride + 1], nrm[i * stride + 2]}; }
+};
+
+inline float norm3f(float a, float b, float c) { return std::sqrt(a * a + (b * b + c * c)); }
+inline double norm3d(double a, double b, double c) { return std::sqrt((a * a + b * b) + c * c); }
+
+// computeSphericalHistogram (536-564): bins[az * elevation_bins + el] = candidate indices, in order.
+std::vector<std::vector<int>> spherical_histogram(const SampleCloud& c, const int32_t* cand, size_t n_cand, int az_bins,
+                                                  int el_bins) {
+    std::vector<std::vector<int>> h((size_t)az_bins * el_bins);
+    for (size_t k = 0; k < n_cand; ++k) {
+        const int idx = cand[k];
+        const P3 nn = c.n(idx);
+        float azimuth = std::atan2(nn.y, nn.x);        // `using std::atan2` (51): the float overload
+        float elevation = (float)::asin((double)nn.z); // ::asin(double) (no float overload in scope)
+        if (azimuth < 0) azimuth += 2 * M_PI;
+        elevation += M_PI / 2;
+        const int ai = std::min(static_cast<int>(azimuth / (2 * M_PI / az_bins)), az_bins - 1);
+        const int ei = std::min(static_cast<int>(elevation / (M_PI / el_bins)), el_bins - 1);
+        h[(size_t)ai * el_bins + ei].push_back(idx);
+    }
+    return h;
+}
+
+struct Rng {
+    uint32_t shuffle_seed;
+    uint32_t calls = 0;
+    int32_t glibc[34];
+};
+
+// randomSampling (566-582)
+void random_sampling(const std::vector<int>& cand, int max_points, std::vector<int>& out, Rng& rng) {
+    std::mt19937 gen(rng.shuffle_seed + rng.calls++);
+    std::vector<int> sh = cand;
+    std::shuffle(sh.begin(), sh.end(), gen);
+    const int cnt = std::min(max_points, (int)sh.size());
+    for (int i = 0; i < cnt; ++i) out.push_back(sh[i]);
+}
+
+// farthestPointSampling (common.cpp:19-82) over the sub-cloud `pts` (indices into c)
+void farthest_point_sampling(const SampleCloud& c, const std::vector<int>& pts, int num_samples, std::vector<int>& out,
+                             Rng& rng) {
+    const int n = (int)pts.size();
+    std::vector<double> md(n, INFINITY);
+    std::vector<char> taken(n, 0);
+    const int first = oracle_rand_next(rng.glibc) % n;            // 49
+    out.push_back(first);
+    taken[first] = 1;
+    const P3 f = c.p(pts[first]);
+    for (int i = 0; i < n; ++i) {
+        const P3 q = c.p(pts[i]);
+        md[i] = norm3d((double)f.x - q.x, (double)f.y - q.y, (double)f.z - q.z);
+    }
+    for (int s = 1; s < num_samples; ++s) {                        // 59-81
+        double best = -1.0;
+        int bi = -1;
+        for (int i = 0; i < n; ++i)
+            if (!taken[i] && md[i] > best) { best = md[i]; bi = i; }
+        out.push_back(bi);
+        taken[bi] = 1;
+        const P3 b = c.p(pts[bi]);
+        for (int i = 0; i < n; ++i) {
+            const P3 q = c.p(pts[i]);
+            md[i] = std::min(md[i], norm3d((double)b.x - q.x, (double)b.y - q.y, (double)b.z - q.z));
+        }
+    }
+}
+
+// the shared "sample a bin down to k points" step of normalSampling (603-622) / majorAxisSampling (735-752)
+void sample_bin(const SampleCloud& c, const std::vector<int>& bin, int k, int strategy, std::vector<int>& out, Rng& rng) {
+    if (strategy == 0) {
+        std::vector<int> loc;
+        farthest_point_sampling(c, bin, k, loc, rng);
+        for (int b : loc) out.push_back(bin[b]);
+    } else {
+        random_sampling(bin, k, out, rng);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -218,6 +316,82 @@ int oracle_ring_pca(const float* xyz, size_t stride, const int32_t* ring_sizes, 
     }
     if (n_out) *n_out = r;
     if (counters) { counters[0] = fail; counters[1] = invalid; }
+    return 0;
+}
+
+// samplePointCloud for "normal" / "major_axis" (scan_registration.cpp:761-806).  Same contract as
+// imls_sample_point_cloud (include/imls_gpu.h).
+int oracle_sample_point_cloud(const imls_sample_params* p, const float* xyz, const float* nrm, size_t stride, size_t n,
+                              const int32_t* cand, size_t n_cand, const float* last_xyz, size_t last_stride, size_t m,
+                              int32_t* sampled_out, size_t* n_sampled, float* bin_weights_out) {
+    const SampleCloud c{xyz, nrm, stride};
+    const int nb = p->azimuth_bins * p->elevation_bins;
+    auto hist = spherical_histogram(c, cand, n_cand, p->azimuth_bins, p->elevation_bins);
+    Rng rng{};
+    rng.shuffle_seed = p->shuffle_seed;
+    oracle_rand_seed(rng.glibc, p->rand_seed);
+    std::vector<int> out;
+    std::vector<float> w(nb, 0.0f);
+    if (p->method == IMLS_SAMPLE_NORMAL) {                         // normalSampling (584-629)
+        for (int b = 0; b < nb; ++b) {
+            const auto& bin = hist[b];
+            const int sz = (int)bin.size();
+            if (sz < p->min_points_per_bin) continue;
+            if (sz > p->max_points_per_bin) sample_bin(c, bin, p->max_points_per_bin, p->sampling_strategy, out, rng);
+            else out.insert(out.end(), bin.begin(), bin.end());
+        }
+    } else {                                                       // majorAxisSampling (631-759)
+        for (int b = 0; b < nb; ++b) {
+            const auto& bin = hist[b];
+            const int sz = (int)bin.size();
+            if (sz < p->min_points_per_bin) continue;
+            std::vector<int> sub;
+            if (sz > p->max_points_per_bin) random_sampling(bin, p->max_points_per_bin, sub, rng);
+            else sub = bin;
+            std::vector<float> distances(sub.size(), 0.0f);
+            int valid = 0;
+            for (int idx : sub) {                                  // 670-702
+                const P3 pt = c.p(idx), nn = c.n(idx);
+                int cnt = 0;
+                for (size_t j = 0; j < m; ++j) {                   // 679-686
+                    const float dx = pt.x - last_xyz[j * last_stride], dy = pt.y - last_xyz[j * last_stride + 1],
+                                dz = pt.z - last_xyz[j * last_stride + 2];
+                    const float cx = dy * nn.z - dz * nn.y, cy = dz * nn.x - dx * nn.z, cz = dx * nn.y - dy * nn.x;
+                    if (norm3f(dx, dy, dz) < p->r_proj && norm3f(cx, cy, cz) < p->r) cnt++;
+                }
+                if (cnt >= 3) {                                    // 689-701
+                    float avg = 0.0f;
+                    for (size_t j = 0; j < m; ++j) {
+                        const float dx = pt.x - last_xyz[j * last_stride], dy = pt.y - last_xyz[j * last_stride + 1],
+                                    dz = pt.z - last_xyz[j * last_stride + 2];
+                        const float cx = dy * nn.z - dz * nn.y, cy = dz * nn.x - dx * nn.z, cz = dx * nn.y - dy * nn.x;
+                        if (norm3f(dx, dy, dz) < p->r_proj && norm3f(cx, cy, cz) < p->r) avg += norm3f(dx, dy, dz);
+                    }
+                    avg /= (float)cnt;
+                    distances[valid++] = avg;
+                }
+            }
+            if (valid >= 3) {                                      // 704-711
+                float total = 0.0f;
+                for (float d : distances) total += d;
+                w[b] = total / valid;
+            }
+        }
+        float tw = 0.0f;                                           // 715-723
+        for (float x : w) tw += x;
+        for (float& x : w) x /= tw;
+        for (int b = 0; b < nb; ++b) {                             // 726-758
+            const auto& bin = hist[b];
+            const int sz = (int)bin.size();
+            if (sz < p->min_points_per_bin) continue;
+            const int k = std::min(static_cast<int>(w[b] * p->max_total_points), sz);
+            if (sz > k) sample_bin(c, bin, k, p->sampling_strategy, out, rng);
+            else out.insert(out.end(), bin.begin(), bin.end());
+        }
+    }
+    for (size_t k = 0; k < out.size(); ++k) sampled_out[k] = out[k];
+    if (n_sampled) *n_sampled = out.size();
+    if (bin_weights_out) for (int b = 0; b < nb; ++b) bin_weights_out[b] = w[b];
     return 0;
 }
 

@@ -110,6 +110,34 @@ def default_pca_params() -> ImlsPcaParams:
     return p
 
 
+class ImlsSampleParams(C.Structure):
+    """imls_sample_params (include/imls_gpu.h): scan_registration.sample_method (config.json,
+    read at scan_registration.cpp:784-799)."""
+    _fields_ = [("method", C.c_int32), ("r", C.c_float), ("r_proj", C.c_float), ("max_total_points", C.c_int32),
+                ("azimuth_bins", C.c_int32), ("elevation_bins", C.c_int32), ("min_points_per_bin", C.c_int32),
+                ("max_points_per_bin", C.c_int32), ("sampling_strategy", C.c_int32), ("shuffle_seed", C.c_uint32),
+                ("rand_seed", C.c_uint32)]
+
+
+IMLS_SAMPLE_NORMAL, IMLS_SAMPLE_MAJOR_AXIS = 0, 1
+SAMPLE_FPS, SAMPLE_RANDOM = 0, 1
+
+
+def default_sample_params(method: int = IMLS_SAMPLE_MAJOR_AXIS) -> ImlsSampleParams:
+    """The shipped config.json values (imls_default_sample_params() in the library)."""
+    p = ImlsSampleParams()
+    p.method = method
+    p.r, p.r_proj, p.max_total_points = 0.5, 1.5, 2000
+    p.azimuth_bins = p.elevation_bins = 8
+    p.min_points_per_bin = 20
+    if method == IMLS_SAMPLE_NORMAL:
+        p.max_points_per_bin, p.sampling_strategy = 100, SAMPLE_RANDOM
+    else:
+        p.max_points_per_bin, p.sampling_strategy = 200, SAMPLE_FPS
+    p.shuffle_seed, p.rand_seed = 0, 1
+    return p
+
+
 def _bind(lib: C.CDLL) -> C.CDLL:
     P, VP, SZ = C.POINTER, C.c_void_p, C.c_size_t
     sig = {
@@ -142,6 +170,9 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_default_pca_params": (None, [P(ImlsPcaParams)]),
         "imls_ring_normals_pca": (C.c_int, [VP, P(ImlsPcaParams), VP, SZ, VP, C.c_int32, VP, VP, VP, VP, VP, VP,
                                             P(SZ), VP]),
+        "imls_default_sample_params": (None, [P(ImlsSampleParams), C.c_int32]),
+        "imls_sample_point_cloud": (C.c_int, [VP, P(ImlsSampleParams), VP, VP, SZ, SZ, VP, SZ, VP, SZ, SZ, VP, P(SZ),
+                                              VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -158,6 +189,7 @@ ABI_SYMBOLS = (
     "imls_solve_correspondences", "imls_register_frame", "imls_register_frame_async",
     "imls_register_frame_result", "imls_enable_timing", "imls_kernel_timing", "imls_reset_timing",
     "imls_index_stats", "imls_traversal_stats", "imls_default_pca_params", "imls_ring_normals_pca",
+    "imls_default_sample_params", "imls_sample_point_cloud",
 )
 
 _LIB = None

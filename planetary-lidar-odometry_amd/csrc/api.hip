@@ -14,7 +14,7 @@
 
 using namespace imlsgpu;
 
-constexpr int kTimingKinds = 6;   // projection, index, solve chain, k_knn_wave, k_finish, k_ring_pca
+constexpr int kTimingKinds = 7;   // projection, index, solve chain, k_knn_wave, k_finish, k_ring_pca, k_major_avg
 
 struct imls_ctx {
     int device = 0;
@@ -40,6 +40,7 @@ struct imls_ctx {
     DevBuf mten, upload_ten;              // tensor voting: input tensors (Morton order) + upload staging
     DevBuf tvn;                           // tensor voting: per-source voted normal + found flag (double4)
     DevBuf pca_mem;                       // imls_ring_normals_pca scratch (upstream producer)
+    DevBuf sample_mem;                    // imls_sample_point_cloud scratch
     size_t n_target_in = 0;               // input size of the last set_target (tensor arrays match it)
     bool has_tensors = false;
     int lane_mode = 0;
@@ -509,7 +510,7 @@ void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->pca_mem, &c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
+    DevBuf* bufs[] = {&c->sample_mem, &c->pca_mem, &c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
                       &c->upload_t, &c->spt, &c->snr, &c->sscratch,
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
@@ -832,6 +833,52 @@ int imls_ring_normals_pca(imls_ctx* c, const imls_pca_params* p, const float* xy
     }
     int rc = ring_pca_run(c->stream, *p, xyz, stride, ring_sizes, n_rings, c->pca_mem, mk, index_out, normal_out,
                           evals_out, evecs_out, features_out, flags_out, n_out, counters, c->err);
+    if (c->timing) harvest_timing(c);
+    return rc;
+}
+
+void imls_default_sample_params(imls_sample_params* p, int32_t method) {
+    // scan_registration.sample_method.{normal, major_axis} of the shipped config.json (784-799)
+    if (!p) return;
+    p->method = method;
+    p->r = 0.5f;
+    p->r_proj = 1.5f;
+    p->max_total_points = 2000;
+    p->azimuth_bins = 8;
+    p->elevation_bins = 8;
+    p->min_points_per_bin = 20;
+    p->max_points_per_bin = method == IMLS_SAMPLE_NORMAL ? 100 : 200;
+    p->sampling_strategy = method == IMLS_SAMPLE_NORMAL ? 1 : 0;   // normal: "random", major_axis: "FPS"
+    p->shuffle_seed = 0;
+    p->rand_seed = 1;
+}
+
+int imls_sample_point_cloud(imls_ctx* c, const imls_sample_params* p, const float* xyz, const float* nrm,
+                            size_t stride, size_t n, const int32_t* candidates, size_t n_cand, const float* last_xyz,
+                            size_t last_stride, size_t m, int32_t* sampled_out, size_t* n_sampled,
+                            float* bin_weights_out) {
+    if (!c) return IMLS_ERR_ARG;
+    if (!p || stride < 3 || (n_cand > 0 && (!xyz || !nrm || !candidates || !sampled_out)))
+        return fail(c, IMLS_ERR_ARG, "bad sample params / pointers / stride");
+    if (p->method < 0 || p->method > 1 || p->azimuth_bins <= 0 || p->elevation_bins <= 0 || p->azimuth_bins > 1024 ||
+        p->elevation_bins > 1024 || p->sampling_strategy < 0 || p->sampling_strategy > 1)
+        return fail(c, IMLS_ERR_ARG, "bad sample method / bins / strategy");
+    if (p->method == IMLS_SAMPLE_MAJOR_AXIS && m > 0 && (!last_xyz || last_stride < 3))
+        return fail(c, IMLS_ERR_ARG, "major_axis needs last_pcl_cloud");
+    if (n >= (1ull << 31) || m >= (1ull << 31)) return fail(c, IMLS_ERR_CAPACITY, "cloud too large");
+    if (int rc = check_device(c)) return rc;
+    int slot = -1;
+    hipEvent_t marks[2];
+    hipEvent_t* mk = nullptr;
+    if (c->timing && (slot = ev_pair(c)) >= 0) {
+        marks[0] = c->ev[slot];
+        marks[1] = c->ev[slot + 1];
+        c->ev_pairs[6].push_back({slot, slot + 1});
+        mk = marks;
+    }
+    int rc = sample_run(c->stream, *p, xyz, nrm, stride, n, candidates, n_cand, last_xyz, last_stride, m,
+                        c->sample_mem, mk, sampled_out, n_sampled, bin_weights_out, c->err);
+    if (mk && rc == IMLS_OK && p->method != IMLS_SAMPLE_MAJOR_AXIS) c->ev_pairs[6].pop_back();   // no kernel recorded
     if (c->timing) harvest_timing(c);
     return rc;
 }

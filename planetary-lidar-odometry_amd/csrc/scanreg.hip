@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kPcaBlock) void k_ring_pca(const float4* __restrict
     float nx = E[6], ny = E[7], nz = E[8];
     const float z2 = __fadd_rn(__fadd_rn(__fmul_rn(nx, nx), __fmul_rn(ny, ny)), __fmul_rn(nz, nz));
     if (z2 > 0.f) {
-        const float sq = __fsqrt_rn(z2);
+        const float sq = (float)__dsqrt_rn((double)z2);   // correctly rounded (v_sqrt_f32 is 1 ulp)
         nx = __fdiv_rn(nx, sq); ny = __fdiv_rn(ny, sq); nz = __fdiv_rn(nz, sq);
     }
     if (nz < 0.f) { nx = -nx; ny = -ny; nz = -nz; }

@@ -206,6 +206,26 @@ class ImlsContext:
         return dict(index=idx[:k], normal=nrm[:k], evals=ev[:k], evecs=evec[:k], features=feat[:k], flags=fl[:k],
                     pca_failure=int(cnt[0]), plane_invalid=int(cnt[1]))
 
+    def sample_point_cloud(self, xyz, nrm, candidates, last_xyz=None,
+                           sample_params: Optional[_abi.ImlsSampleParams] = None):
+        """samplePointCloud "normal" / "major_axis" (scan_registration.cpp:761-806) of the filtered
+        cloud (xyz, nrm: (n, 3) float32) restricted to `candidates`, against the previous frame's
+        cloud last_xyz (major_axis).  Returns (sampled indices in the reference's order, bin weights)."""
+        a = np.ascontiguousarray(np.asarray(xyz, np.float32)[:, :3])
+        nn = np.ascontiguousarray(np.asarray(nrm, np.float32)[:, :3])
+        if a.shape != nn.shape:
+            raise ValueError("xyz and nrm must have the same shape")
+        cand = np.ascontiguousarray(candidates, dtype=np.int32)
+        last = np.ascontiguousarray(np.zeros((0, 3)) if last_xyz is None else np.asarray(last_xyz)[:, :3],
+                                    dtype=np.float32)
+        p = sample_params if sample_params is not None else _abi.default_sample_params()
+        nb = p.azimuth_bins * p.elevation_bins
+        out = np.zeros(len(cand) + nb + 1, np.int32); w = np.zeros(nb, np.float32); k = C.c_size_t()
+        self._check(self.lib.imls_sample_point_cloud(self.ctx, C.byref(p), _ptr(a), _ptr(nn), 3, a.shape[0],
+                                                     _ptr(cand), len(cand), _ptr(last), 3, last.shape[0],
+                                                     _ptr(out), C.byref(k), _ptr(w)))
+        return out[:k.value], w
+
     def enable_timing(self, on=True):
         self._check(self.lib.imls_enable_timing(self.ctx, int(on)))
 
