@@ -45,7 +45,10 @@ constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query
 constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
 constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
 constexpr int kSeedLeaves = 8;       // first-iteration seed pass: at most this many leaves per wave
-constexpr int kSeedChunk = 8;        // per-lane reseed: points loaded per batch
+#ifndef IMLS_SEED_CHUNK
+#define IMLS_SEED_CHUNK 8
+#endif
+constexpr int kSeedChunk = IMLS_SEED_CHUNK;   // per-lane reseed: points loaded per batch
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
 constexpr double kCertSlack = 1.0 + 4e-7;
 
@@ -286,8 +289,16 @@ __device__ __forceinline__ float need_key(const float (&lk)[KL], float r2, int K
     return cnt_r >= K ? fmaxf(dK, d1) : kInfF;
 }
 
+// Register cap of the packet traversal: 216 VGPRs (2 waves/SIMD) uncapped; capping at 3 waves/SIMD
+// (168 VGPRs) spills ~56 VGPRs of cold-path state to scratch and measured +4-5 % pairs/s with 4 pairs
+// in flight (more resident waves hide the dependent node/leaf loads).  Longer lists (KL > 24) keep
+// the uncapped allocation.
+#ifndef IMLS_KNN_WPE
+#define IMLS_KNN_WPE 3
+#endif
+#define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 24 ? IMLS_KNN_WPE : 1)))
 template <int KL, bool LOCKSTEP>
-__global__ __launch_bounds__(kWaveBlock) void k_knn_wave(TreeView t, const float4* __restrict__ spt,
+__global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
                                                          const double* __restrict__ pose,
                                                          const int* __restrict__ done, KParams kp,
@@ -894,8 +905,13 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
 // =============================================================================================
 // Exact stage + gates + IMLS (hot kernel 2): one lane per query
 // =============================================================================================
+#ifdef IMLS_FINISH_WPE   // experiment: cap the exact stage's registers for more resident waves
+#define IMLS_FINISH_ATTR __attribute__((amdgpu_waves_per_eu(IMLS_FINISH_WPE)))
+#else
+#define IMLS_FINISH_ATTR
+#endif
 template <int KL>
-__global__ __launch_bounds__(kWaveBlock) void k_finish(TreeView t, const float4* __restrict__ spt,
+__global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(TreeView t, const float4* __restrict__ spt,
                                                        const float4* __restrict__ snr,
                                                        const unsigned* __restrict__ qperm, int N,
                                                        const double* __restrict__ pose,

@@ -57,6 +57,35 @@ def test_struct_layout_matches_c(tmp_path):
         assert getattr(_abi.ImlsParams, f).offset == off, f
 
 
+@pytest.mark.parametrize("ctype,cname", [(_abi.ImlsPcaParams, "imls_pca_params"),
+                                          (_abi.ImlsSampleParams, "imls_sample_params")])
+def test_producer_struct_layouts_and_defaults(tmp_path, ctype, cname):
+    fields = [f for f, _ in ctype._fields_]
+    prog = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){",
+            f'printf("%zu\\n", sizeof({cname}));']
+    prog += [f'printf("%zu\\n", offsetof({cname}, {f}));' for f in fields]
+    prog += ["return 0;}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(prog))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(src)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[0] == C.sizeof(ctype)
+    for f, off in zip(fields, vals[1:]):
+        assert getattr(ctype, f).offset == off, f
+    lib = _abi.load_library()
+    as_dict = lambda p: {f: getattr(p, f) for f in fields}
+    if ctype is _abi.ImlsPcaParams:
+        p = ctype()
+        lib.imls_default_pca_params(C.byref(p))
+        assert as_dict(p) == as_dict(_abi.default_pca_params())
+    else:
+        for m in (_abi.IMLS_SAMPLE_NORMAL, _abi.IMLS_SAMPLE_MAJOR_AXIS):
+            p = ctype()
+            lib.imls_default_sample_params(C.byref(p), m)
+            assert as_dict(p) == as_dict(_abi.default_sample_params(m))
+
+
 def test_cpp_adapter_header_compiles(tmp_path):
     """include/imls_icp_hip.hpp (the reference-shaped C++ adapter) compiles against a PCL-shaped
     mock cloud with g++ alone."""
