@@ -921,9 +921,34 @@ inline void rotate_normal(const double T[16], float nx, float ny, float nz, floa
 
 struct Corr { std::vector<float> x, y, n; std::vector<uint32_t> idx; };
 
+int g_threads = 1;   // oracle_set_threads: the secondary (all-cores) CPU baseline, SURVEY §8(d)
+
 void project_all(const Matcher& m, const Cloud& src, const double T[16], bool rot_normals, Corr& c, uint64_t rej[6]) {
     for (int k = 0; k < 6; ++k) rej[k] = 0;
     c.x.clear(); c.y.clear(); c.n.clear(); c.idx.clear();
+    if (g_threads > 1) {
+        // queries are independent: evaluate them in parallel, then compact in source order (the
+        // same result as the sequential loop below)
+        const size_t N = src.size();
+        std::vector<float> X(3 * N), Y(3 * N), NN(3 * N);
+        std::vector<int> R(N);
+#pragma omp parallel for schedule(dynamic, 256) num_threads(g_threads)
+        for (long i = 0; i < (long)N; ++i) {
+            float ns[3] = {src.nx[i], src.ny[i], src.nz[i]};
+            transform_point(T, src.x[i], src.y[i], src.z[i], &X[3 * i]);
+            if (rot_normals) rotate_normal(T, src.nx[i], src.ny[i], src.nz[i], ns);
+            R[i] = m.P->matching_method == IMLS_MATCH_PLANE_ICP ? m.project_one_plane(&X[3 * i], ns, &Y[3 * i], &NN[3 * i])
+                                                                 : m.project_one(&X[3 * i], ns, &Y[3 * i], &NN[3 * i]);
+        }
+        for (size_t i = 0; i < N; ++i) {
+            if (R[i] >= 0) { rej[R[i]]++; continue; }
+            c.x.insert(c.x.end(), &X[3 * i], &X[3 * i] + 3);
+            c.y.insert(c.y.end(), &Y[3 * i], &Y[3 * i] + 3);
+            c.n.insert(c.n.end(), &NN[3 * i], &NN[3 * i] + 3);
+            c.idx.push_back((uint32_t)i);
+        }
+        return;
+    }
     for (size_t i = 0; i < src.size(); ++i) {
         float x[3], ns[3] = {src.nx[i], src.ny[i], src.nz[i]}, y[3], nn[3];
         transform_point(T, src.x[i], src.y[i], src.z[i], x);
@@ -1106,6 +1131,7 @@ int oracle_tv_normals(const float* tgt6, size_t M, const float* ten6, const floa
 }
 
 void oracle_rand_seed(int32_t* state, uint32_t seed) { rand_seed(state, seed); }
+void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
 int32_t oracle_rand_next(int32_t* state) { return rand_next(state); }
 
 int oracle_colpiv_qr_solve(const double* A, int rows, int cols, const double* b, double* x) {

@@ -46,6 +46,7 @@ def lib():
         L.oracle_tv_normals.argtypes = [VP, SZ, VP, VP, SZ, P(abi.ImlsParams), VP, VP, VP]
         L.oracle_rand_seed.argtypes = [VP, C.c_uint32]
         L.oracle_rand_next.argtypes = [VP]
+        L.oracle_set_threads.argtypes = [C.c_int]
         L.oracle_rand_next.restype = C.c_int32
         L.oracle_colpiv_qr_solve.argtypes = [VP, C.c_int, C.c_int, VP, VP]
         L.oracle_delta_from_x.argtypes = [VP, VP]
@@ -194,3 +195,8 @@ def sample_point_cloud(xyz, nrm, candidates, last_xyz, sample_params):
                                          _ptr(out), C.byref(k), _ptr(w))
     assert rc == 0
     return out[:k.value], w
+
+
+def set_threads(n: int):
+    """Threads of the oracle's per-query projection loop (1 = the reference's single thread)."""
+    lib().oracle_set_threads(int(n))

@@ -379,3 +379,19 @@ def test_tv_encode_pca_host_helper_matches_restatement():
     assert np.array_equal(imls_icp.tv_encode_pca(ev, ec, 50), imls_np.tv_encode_pca(ev, ec, 50))
     bad = np.array([[np.nan, 1.0, 0.5]], np.float32)
     assert np.array_equal(imls_icp.tv_encode_pca(bad, ec[:1], 50)[0], np.array([1, 0, 0, 1, 0, 1], np.float32))
+
+
+def test_threaded_oracle_matches_single_thread():
+    """The all-cores CPU baseline (OpenMP over queries) returns the single-thread result exactly."""
+    from planetary_lidar_odometry_amd import config, synth
+    pair = synth.make_pair("vlp16", map_scans=1, start=5)
+    src, tgt = synth.soa(pair.source), synth.soa(pair.target)
+    p = config.bench_params(3)
+    a = oc.register_frame(src, tgt, p)
+    oc.set_threads(4)
+    try:
+        b = oc.register_frame(src, tgt, p)
+    finally:
+        oc.set_threads(1)
+    assert np.array_equal(a["pose"], b["pose"]) and a["iters"] == b["iters"]
+    assert [list(t.reject) for t in a["trace"]] == [list(t.reject) for t in b["trace"]]
