@@ -741,8 +741,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
     static_assert(KL <= 64, "one list entry per lane");
     if (done && *done) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = 0u;   // k_finish's deferred-query counter
-    __shared__ int snode[kWaveBlock / 64][kStackDepth];
-    __shared__ float sdist[kWaveBlock / 64][kStackDepth];
+    __shared__ int snode[kWaveBlock / 64][kWaveStack];
+    __shared__ float sdist[kWaveBlock / 64][kWaveStack];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (kWaveBlock / 64) + wv);
@@ -835,23 +835,42 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
     if (nbr_stats && lane == 0 && skip) atomicAdd(&nbr_stats[kStatSkipped], 1ull);
     while (node) {
         if (node < P) {
+            // one step descends `sw` binary levels: lane k tests the box of descendant k (the 2^sw
+            // boxes sit in 2^(sw−1) consecutive records of the intermediate level, one parallel load
+            // per lane pair), the nearest wanted descendant is entered and the others are stacked
+            // (lower index popped first) — ⌈levels/3⌉ dependent loads per root-to-leaf walk
             ++n_inner;
-            const float4* rec = t.nodes + 3 * (size_t)node;
-            const float4 a = rec[0], b = rec[1], c = rec[2];
-            const float dl = box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
-            const float dr = box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w);
-            const float bs = bnd * kBoxSlack;
-            const bool nl = dl <= bs, nr = dr <= bs;
-            if (nl && nr) {
-                const bool lf = dl <= dr;
-                snode[wv][sp] = lf ? 2 * node + 1 : 2 * node;
-                sdist[wv][sp] = lf ? dr : dl;
-                ++sp;
-                node = lf ? 2 * node : 2 * node + 1;
+            const int lev = 31 - __builtin_clz(node);
+            const int sw = min(kp.wide, t.levels - lev);
+            const int nk = 1 << sw;
+            float d = kInfF;
+            if (lane < nk) {
+                const float4* rec = t.nodes + 3 * (((size_t)node << (sw - 1)) + (lane >> 1));
+                const float4 a = rec[0], b = rec[1], c = rec[2];
+                d = (lane & 1) ? box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w) : box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+            }
+            const unsigned long long want = __ballot(lane < nk && d <= bnd * kBoxSlack);
+            if (want) {
+                float dm = ((want >> lane) & 1ull) ? d : kInfF;
+                int km = lane;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const float od = __shfl_xor(dm, o, 64);
+                    const int ok = __shfl_xor(km, o, 64);
+                    if (od < dm || (od == dm && ok < km)) { dm = od; km = ok; }
+                }
+                km = __builtin_amdgcn_readfirstlane(km);
+                unsigned long long rest = want & ~(1ull << km);
+                while (rest) {
+                    const int kk = 63 - __builtin_clzll(rest);
+                    rest &= ~(1ull << kk);
+                    const float dk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), kk));
+                    if (lane == 0) { snode[wv][sp] = (node << sw) + kk; sdist[wv][sp] = dk; }
+                    ++sp;
+                }
+                node = (node << sw) + km;
                 continue;
             }
-            if (nl) { node = 2 * node; continue; }
-            if (nr) { node = 2 * node + 1; continue; }
         } else {
             ++n_leaf;
             const int leaf = node - P;
