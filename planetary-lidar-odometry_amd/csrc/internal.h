@@ -56,6 +56,7 @@ struct KParams {
     int qwave;                // traversal: 0 = packets of 64 queries per wave, 1 = one wave per query
     int wide;                 // packet traversal: binary levels descended per step (1..3)
     int verlet;               // reuse a query's list without traversal while its certification holds
+    int qverlet;              // the same for the wave-per-query traversal (off by default: measured slower)
     int lockstep;             // packet traversal: per-lane candidate masks, then lockstep insertion
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
     int tv;                   // tensor-voting normals (use_tensor_voting && !get_normals, IMLS matcher)

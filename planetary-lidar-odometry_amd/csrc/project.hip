@@ -755,6 +755,12 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
     float lkey = kInfF;     // lane k < KL: entry k of the ascending list
     int lpos = -1;
     const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
+    // h-gate search (IMLS matcher): a query with no map point within h is rejected as too far
+    // whatever lies between h and r (imls_icp.cpp:612-625), so while the list holds nothing within
+    // h the traversal bound is h², not r² (27× less volume for isolated queries, the launch's tail);
+    // a point found within h re-runs the traversal at the r bound (bounds never grow mid-walk)
+    const float h2s = (float)kp.h2 * kBoxSlack + 1e-30f;
+    bool hmode = false;
     float bnd = r2s;
     const int P = t.P, B = t.B, M = t.M;
     // insert (c, cp): entries ordered by (key, position); the tail shifts up by one lane
@@ -765,7 +771,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
         const int up = __shfl_up(lpos, 1, 64);
         if (lane > at && lane < KL) { lkey = uk; lpos = up; }
         if (lane == at) { lkey = c; lpos = cp; }
-        bnd = fminf(r2s, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), KL - 1)));
+        bnd = fminf(hmode ? h2s : r2s, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), KL - 1)));
     };
     auto worst = [&]() { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), KL - 1)); };
     int seed_lo = 0, seed_hi = -1;
@@ -785,7 +791,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
         const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
         greedy = disp * disp > kp.reseed * wlist[slot];
     }
-    if (!greedy && kp.verlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip);
+    if (!greedy && kp.qverlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip);
     if (skip) {
         // the list stays in place
     } else if (!greedy) {
@@ -831,8 +837,14 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
         }
     }
     unsigned n_inner = 0, n_leaf = 0;
-    int node = skip ? 0 : 1, sp = 0;
     if (nbr_stats && lane == 0 && skip) atomicAdd(&nbr_stats[kStatSkipped], 1ull);
+    auto nearest = [&]() { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(lkey))); };
+    if (!skip && kp.matcher == IMLS_MATCH_IMLS && !(nearest() <= h2s)) {
+        hmode = true;
+        bnd = fminf(bnd, h2s);
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+    int node = skip ? 0 : 1, sp = 0;
     while (node) {
         if (node < P) {
             // one step descends `sw` binary levels: lane k tests the box of descendant k (the 2^sw
@@ -898,6 +910,17 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
             if (sdist[wv][sp] <= bnd * kBoxSlack) { node = snode[wv][sp]; break; }
         }
         if (!node) break;
+    }
+    if (!hmode) break;
+    if (!(nearest() <= h2s)) {
+        // no map point within h: too far whatever the rest of the list holds — leave an empty list
+        // (k_finish: no NN-1 → "too far"; need_key = ∞ → never reused without a traversal)
+        lkey = kInfF;
+        lpos = -1;
+        break;
+    }
+    hmode = false;                     // a point within h: the full-r search, from the root
+    bnd = fminf(r2s, worst());
     }
     if (skip) {
         if (lane == 0) wlist[slot] = wskip;
