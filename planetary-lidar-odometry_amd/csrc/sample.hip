@@ -5,20 +5,22 @@
 // the reference evaluates them), randomSampling's shuffles (std::mt19937 + libstdc++ std::shuffle,
 // 566-582), the bin weights (704-723) and the output assembly in bin order.  Device:
 //   k_major_avg — the O(N_s·M) brute-force neighbour average of majorAxisSampling (670-702): one
-//     wave per sample, the previous frame's cloud streamed through a 2048-point LDS tile shared by
-//     the block's 16 waves (one HBM/L2 read per 16 samples), the two Eigen::Vector3f norm gates per
-//     (sample, point), a ballot of the lanes that pass and an in-order sum (v_readlane per set bit)
-//     so the float accumulation order is the reference's;
+//     wave per sample; the previous frame's cloud (scan-ring order) is cut into 64-point chunks whose
+//     boxes the lanes test 64 at a time, and only chunks that can hold a point within r_proj are
+//     scanned (exact: the skipped chunks provably contribute nothing); per pair the two
+//     Eigen::Vector3f norm gates as square-root-free thresholds, a ballot of the lanes that pass and
+//     an in-order sum (v_readlane per set bit) so the float accumulation order is the reference's;
 //   k_fps — farthestPointSampling of one histogram bin per block: fp64 distances from float
 //     coordinates, min-distance cache in HBM (L2-resident), block arg-max per step (largest distance,
 //     lowest index on ties = the reference's strict > scan), first index from the replayed glibc
 //     rand() stream.
-// Roofline: k_major_avg is VALU-bound (~25 flop per (sample, point) pair; the LDS tile makes HBM
-// traffic 16 B per point per 16 samples); k_fps is latency-bound (one block-wide arg-max per step).
+// Roofline: k_major_avg reads 32 B of chunk box per 64 points per sample plus the surviving chunks
+// (L2-resident: the previous cloud is ~2 MB); k_fps is latency-bound (one block-wide arg-max per step).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <random>
 #include <string>
 #include <vector>
@@ -29,61 +31,77 @@ namespace imlsgpu {
 namespace {
 
 constexpr int kAvgBlock = 1024;        // 16 waves = 16 samples per block
-constexpr int kAvgTile = 2048;         // previous-cloud points per LDS tile (32 KB)
 constexpr int kFpsBlock = 1024;
 
 // Correctly rounded float sqrt: v_sqrt_f32 is a 1-ulp approximation, so go through the correctly
 // rounded fp64 sqrt (rounding sqrt twice, 53 → 24 bits, is innocuous: 53 ≥ 2·24 + 2).
 __device__ __forceinline__ float sqrt_rn(float x) { return (float)__dsqrt_rn((double)x); }
-// Eigen::Vector3f::norm(): sqrt(c0 + (c1 + c2)) (non-vectorised unroller for 3 floats)
-__device__ __forceinline__ float norm3f(float a, float b, float c) {
-    return sqrt_rn(__fadd_rn(__fmul_rn(a, a), __fadd_rn(__fmul_rn(b, b), __fmul_rn(c, c))));
-}
+// (Eigen::Vector3f::norm() = sqrt(c0 + (c1 + c2)): the non-vectorised unroller for 3 floats — the
+// squared norms in k_major_avg keep that order)
 // Eigen::Vector3d::norm() under SSE2: sqrt((c0 + c1) + c2)
 __device__ __forceinline__ double norm3d(double a, double b, double c) {
     return __dsqrt_rn(__dadd_rn(__dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b)), __dmul_rn(c, c)));
 }
 
+// The gates `sqrt_rn(s) < r` are evaluated as `s < T(r)` with T(r) = the smallest float whose
+// correctly rounded sqrt is ≥ r (host, sqrt_threshold) — the same decisions without a square root
+// per pair; the root is taken only for the pairs that pass (their in-order sum needs it).
+// The previous cloud is in scan-ring order, so 64 consecutive points (a chunk) are spatially tight:
+// lanes first test 64 chunk boxes at once and only chunks whose box comes within r_proj (with a
+// 1e-4 relative margin over the float rounding of both sides) are scanned — point by point, in
+// ascending chunk order, so the surviving pairs and their float sum are exactly the exhaustive
+// loop's (679-696).
 __global__ __launch_bounds__(kAvgBlock) void k_major_avg(const float4* __restrict__ spt, const float4* __restrict__ snr,
-                                                         int ns, const float4* __restrict__ last, int m, float r,
-                                                         float r_proj, int* __restrict__ cnt_out,
-                                                         float* __restrict__ avg_out) {
-    __shared__ float4 tile[kAvgTile];
+                                                         int ns, const float4* __restrict__ last, int m,
+                                                         const float4* __restrict__ cbox, float t_r, float t_rproj,
+                                                         int* __restrict__ cnt_out, float* __restrict__ avg_out) {
     const int lane = threadIdx.x & 63;
     const int si = blockIdx.x * (kAvgBlock / 64) + (threadIdx.x >> 6);
-    const bool active = si < ns;
-    const float4 p = spt[active ? si : 0], n = snr[active ? si : 0];
+    if (si >= ns) return;                          // wave-uniform
+    const float4 p = spt[si], n = snr[si];
+    const int nchunks = (m + 63) >> 6;
+    const float cull = t_rproj * (1.0f + 1e-4f);
     int cnt = 0;
     float acc = 0.f;
-    for (int base = 0; base < m; base += kAvgTile) {
-        const int len = min(kAvgTile, m - base);
-        __syncthreads();
-        for (int k = threadIdx.x; k < len; k += kAvgBlock) tile[k] = last[base + k];
-        __syncthreads();
-        if (!active) continue;
-        for (int c = 0; c < len; c += 64) {
-            const int k = c + lane;
+    for (int c0 = 0; c0 < nchunks; c0 += 64) {
+        bool near = false;
+        if (c0 + lane < nchunks) {
+            const float4 lo = cbox[2 * (c0 + lane)], hi = cbox[2 * (c0 + lane) + 1];
+            const float ex = fmaxf(fmaxf(lo.x - p.x, p.x - hi.x), 0.f);
+            const float ey = fmaxf(fmaxf(lo.y - p.y, p.y - hi.y), 0.f);
+            const float ez = fmaxf(fmaxf(lo.z - p.z, p.z - hi.z), 0.f);
+            near = ex * ex + ey * ey + ez * ez <= cull;
+        }
+        unsigned long long cm = __ballot(near);
+        while (cm) {
+            const int c = c0 + (__ffsll((long long)cm) - 1);
+            cm &= cm - 1;
+            const int k = c * 64 + lane;
             bool hit = false;
             float nd = 0.f;
-            if (k < len) {
-                const float4 q = tile[k];
+            if (k < m) {
+                const float4 q = last[k];
                 const float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;   // pt − last_pt (683)
-                const float cx = __fsub_rn(__fmul_rn(dy, n.z), __fmul_rn(dz, n.y));
-                const float cy = __fsub_rn(__fmul_rn(dz, n.x), __fmul_rn(dx, n.z));
-                const float cz = __fsub_rn(__fmul_rn(dx, n.y), __fmul_rn(dy, n.x));
-                nd = norm3f(dx, dy, dz);
-                hit = nd < r_proj && norm3f(cx, cy, cz) < r;
+                const float sd = __fadd_rn(__fmul_rn(dx, dx), __fadd_rn(__fmul_rn(dy, dy), __fmul_rn(dz, dz)));
+                if (sd < t_rproj) {
+                    const float cx = __fsub_rn(__fmul_rn(dy, n.z), __fmul_rn(dz, n.y));
+                    const float cy = __fsub_rn(__fmul_rn(dz, n.x), __fmul_rn(dx, n.z));
+                    const float cz = __fsub_rn(__fmul_rn(dx, n.y), __fmul_rn(dy, n.x));
+                    const float sc = __fadd_rn(__fmul_rn(cx, cx), __fadd_rn(__fmul_rn(cy, cy), __fmul_rn(cz, cz)));
+                    hit = sc < t_r;
+                    if (hit) nd = sqrt_rn(sd);
+                }
             }
             unsigned long long mask = __ballot(hit);
             cnt += __popcll(mask);
             while (mask) {                         // in-order float sum of the nearby distances (691-696)
                 const int b = __ffsll((long long)mask) - 1;
-                acc = __fadd_rn(acc, __shfl(nd, b));
+                acc = __fadd_rn(acc, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), b)));
                 mask &= mask - 1;
             }
         }
     }
-    if (active && lane == 0) {
+    if (lane == 0) {
         cnt_out[si] = cnt;
         avg_out[si] = cnt >= 3 ? __fdiv_rn(acc, (float)cnt) : 0.f;   // 697
     }
@@ -151,6 +169,18 @@ int host_rand_next(int* st) {
 }
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Smallest float t ≥ 0 with sqrt(t) ≥ r in correctly rounded float arithmetic (x86 sqrtss is
+// correctly rounded, as is the device's sqrt_rn), so `sqrt(s) < r` ⇔ `s < t` for every float s ≥ 0.
+float sqrt_threshold(float r) {
+    if (!(r > 0.f)) return 0.f;                        // sqrt(s) < r never holds
+    if (std::isinf(r)) return INFINITY;
+    float t = r * r;
+    if (std::isinf(t)) t = std::numeric_limits<float>::max();
+    while (t > 0.f && std::sqrt(std::nextafter(t, 0.f)) >= r) t = std::nextafter(t, 0.f);
+    while (std::sqrt(t) < r) t = std::nextafter(t, INFINITY);
+    return t;
+}
 
 struct HostRng {
     uint32_t seed;
@@ -222,17 +252,33 @@ int sample_run(hipStream_t s, const imls_sample_params& p, const float* xyz, con
             }
             for (size_t j = 0; j < m; ++j)
                 hl[j] = make_float4(last_xyz[j * last_stride], last_xyz[j * last_stride + 1], last_xyz[j * last_stride + 2], 0.f);
-            const size_t o_s = 0, o_l = al256(o_s + hs.size() * 16), o_c = al256(o_l + m * 16),
-                         o_a = al256(o_c + (size_t)ns * 4), total = al256(o_a + (size_t)ns * 4);
+            const size_t nch = (m + 63) / 64;
+            std::vector<float4> hb(2 * nch);                               // AABB of every 64-point chunk
+            for (size_t c = 0; c < nch; ++c) {
+                float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+                for (size_t j = c * 64; j < std::min(m, c * 64 + 64); ++j) {
+                    lo.x = std::min(lo.x, hl[j].x); lo.y = std::min(lo.y, hl[j].y); lo.z = std::min(lo.z, hl[j].z);
+                    hi.x = std::max(hi.x, hl[j].x); hi.y = std::max(hi.y, hl[j].y); hi.z = std::max(hi.z, hl[j].z);
+                }
+                // a non-finite coordinate makes the box unbounded: the chunk is always scanned
+                if (!(std::isfinite(lo.x) && std::isfinite(lo.y) && std::isfinite(lo.z) && std::isfinite(hi.x) &&
+                      std::isfinite(hi.y) && std::isfinite(hi.z)))
+                    lo = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f), hi = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+                hb[2 * c] = lo;
+                hb[2 * c + 1] = hi;
+            }
+            const size_t o_s = 0, o_l = al256(o_s + hs.size() * 16), o_b = al256(o_l + m * 16),
+                         o_c = al256(o_b + nch * 32), o_a = al256(o_c + (size_t)ns * 4), total = al256(o_a + (size_t)ns * 4);
             if (!grow_buf(mem, total)) { err = "hipMalloc (sample scratch)"; return IMLS_ERR_DEVICE; }
             char* d = (char*)mem.p;
             bool ok = hipMemcpyAsync(d + o_s, hs.data(), hs.size() * 16, hipMemcpyHostToDevice, s) == hipSuccess;
             ok = ok && hipMemcpyAsync(d + o_l, hl.data(), m * 16, hipMemcpyHostToDevice, s) == hipSuccess;
+            ok = ok && hipMemcpyAsync(d + o_b, hb.data(), nch * 32, hipMemcpyHostToDevice, s) == hipSuccess;
             if (!ok) { err = "sample upload failed"; return IMLS_ERR_DEVICE; }
             if (marks) (void)hipEventRecord(marks[0], s);
             k_major_avg<<<(ns + kAvgBlock / 64 - 1) / (kAvgBlock / 64), kAvgBlock, 0, s>>>(
-                (const float4*)(d + o_s), (const float4*)(d + o_s) + ns, ns, (const float4*)(d + o_l), (int)m, p.r,
-                p.r_proj, (int*)(d + o_c), (float*)(d + o_a));
+                (const float4*)(d + o_s), (const float4*)(d + o_s) + ns, ns, (const float4*)(d + o_l), (int)m,
+                (const float4*)(d + o_b), sqrt_threshold(p.r), sqrt_threshold(p.r_proj), (int*)(d + o_c), (float*)(d + o_a));
             if (marks) (void)hipEventRecord(marks[1], s);
             ok = hipGetLastError() == hipSuccess;
             ok = ok && hipMemcpyAsync(cnt.data(), d + o_c, (size_t)ns * 4, hipMemcpyDeviceToHost, s) == hipSuccess;
