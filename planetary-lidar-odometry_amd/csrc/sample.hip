@@ -31,7 +31,7 @@ namespace imlsgpu {
 namespace {
 
 constexpr int kAvgBlock = 1024;        // 16 waves = 16 samples per block
-constexpr int kFpsBlock = 1024;
+constexpr int kFpsBlock = 512;          // 8 waves: up to 256 VGPRs for the register-resident bin
 
 // Correctly rounded float sqrt: v_sqrt_f32 is a 1-ulp approximation, so go through the correctly
 // rounded fp64 sqrt (rounding sqrt twice, 53 → 24 bits, is innocuous: 53 ≥ 2·24 + 2).
@@ -111,49 +111,84 @@ struct FpsJob {
     int off, n, k, first, out;   // points [off, off+n) of the packed bin clouds; k samples → out[out, out+k)
 };
 
+constexpr int kFpsPPT = 16;            // bin points per thread held in registers (bins ≤ 8192 points)
+
+// block arg-max of (value desc, index asc) — the first maximum of the reference's strict `>` scan
+__device__ __forceinline__ void fps_better(double& b, int& x, double ov, int oi) {
+    if (ov > b || (ov == b && oi < x)) { b = ov; x = oi; }
+}
+
 __global__ __launch_bounds__(kFpsBlock) void k_fps(const float4* __restrict__ pts, const FpsJob* __restrict__ jobs,
                                                    double* __restrict__ md, unsigned char* __restrict__ taken,
                                                    int* __restrict__ out) {
-    __shared__ double sv[kFpsBlock / 64];
-    __shared__ int si[kFpsBlock / 64];
-    __shared__ int chosen;
+    // one LDS slot pair per wave and iteration parity: a single barrier per sample (a wave cannot
+    // overwrite parity p before every wave has passed the next barrier, i.e. finished reading p)
+    __shared__ double sv[2][kFpsBlock / 64];
+    __shared__ int si[2][kFpsBlock / 64];
     const FpsJob J = jobs[blockIdx.x];
     const float4* P = pts + J.off;
-    double* D = md + J.off;
-    unsigned char* T = taken + J.off;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int last = J.first;
-    for (int i = threadIdx.x; i < J.n; i += kFpsBlock) { D[i] = INFINITY; T[i] = i == last; }
-    if (threadIdx.x == 0) out[J.out] = last;
-    __syncthreads();
+    if (tid == 0) out[J.out] = last;
+    const bool regs = J.n <= kFpsBlock * kFpsPPT;
+    double D[kFpsPPT];
+    float X[kFpsPPT], Y[kFpsPPT], Z[kFpsPPT];
+    unsigned tk = 0u;                                   // bit k: point tid + k·kFpsBlock already sampled
+    double* Dg = md + J.off;
+    unsigned char* Tg = taken + J.off;
+    if (regs) {
+#pragma unroll
+        for (int k = 0; k < kFpsPPT; ++k) {
+            const int i = tid + k * kFpsBlock;
+            const float4 q = P[i < J.n ? i : 0];
+            X[k] = q.x; Y[k] = q.y; Z[k] = q.z;
+            D[k] = INFINITY;
+            if (i == last) tk |= 1u << k;
+        }
+    } else {
+        for (int i = tid; i < J.n; i += kFpsBlock) { Dg[i] = INFINITY; Tg[i] = i == last; }
+        __syncthreads();
+    }
     for (int s = 1; s < J.k; ++s) {
-        const float4 f = P[last];
+        const float4 f = P[last];                       // one broadcast load
+        const double fx = f.x, fy = f.y, fz = f.z;
         double best = -1.0;
         int bi = 0x7fffffff;
-        for (int i = threadIdx.x; i < J.n; i += kFpsBlock) {
-            const float4 q = P[i];
-            const double d = norm3d((double)f.x - (double)q.x, (double)f.y - (double)q.y, (double)f.z - (double)q.z);
-            const double v = fmin(D[i], d);
-            D[i] = v;
-            if (!T[i] && v > best) { best = v; bi = i; }   // ascending i: the first maximum
+        if (regs) {
+#pragma unroll
+            for (int k = 0; k < kFpsPPT; ++k) {
+                const int i = tid + k * kFpsBlock;
+                if (i < J.n) {
+                    const double v = fmin(D[k], norm3d(fx - (double)X[k], fy - (double)Y[k], fz - (double)Z[k]));
+                    D[k] = v;
+                    if (!((tk >> k) & 1u) && v > best) { best = v; bi = i; }   // ascending i: the first maximum
+                }
+            }
+        } else {
+            for (int i = tid; i < J.n; i += kFpsBlock) {
+                const float4 q = P[i];
+                const double v = fmin(Dg[i], norm3d(fx - (double)q.x, fy - (double)q.y, fz - (double)q.z));
+                Dg[i] = v;
+                if (!Tg[i] && v > best) { best = v; bi = i; }
+            }
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            const double ov = __shfl_xor(best, o);
-            const int oi = __shfl_xor(bi, o);
-            if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
-        }
-        if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = best; si[threadIdx.x >> 6] = bi; }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) fps_better(best, bi, __shfl_xor(best, o), __shfl_xor(bi, o));
+        const int par = s & 1;
+        if (lane == 0) { sv[par][wv] = best; si[par][wv] = bi; }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            double b = sv[0];
-            int x = si[0];
-            for (int w = 1; w < kFpsBlock / 64; ++w)
-                if (sv[w] > b || (sv[w] == b && si[w] < x)) { b = sv[w]; x = si[w]; }
-            chosen = x;
-            out[J.out + s] = x;
-            T[x] = 1;
+        double b = sv[par][0];
+        int x = si[par][0];
+#pragma unroll
+        for (int w = 1; w < kFpsBlock / 64; ++w) fps_better(b, x, sv[par][w], si[par][w]);
+        last = x;
+        if (tid == 0) out[J.out + s] = x;
+        if (regs) {
+            if ((x & (kFpsBlock - 1)) == tid) tk |= 1u << (x / kFpsBlock);
+        } else {
+            if (tid == 0) Tg[x] = 1;
+            __syncthreads();
         }
-        __syncthreads();
-        last = chosen;
     }
 }
 
