@@ -1283,7 +1283,9 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
     // (fb_count is re-zeroed by the traversal kernel's first thread)
     if (K <= 8) launch_wave<12>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
-    else if (K <= 20) launch_wave<24>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
+    // K ≤ 20 (the shipped 20): two slack entries certify every query on config B (KL 21 left a few
+    // uncertified → the slow exact fallback, −30 %; KL 22 vs 24 measured +6.7 % pairs/s, 4 in flight)
+    else if (K <= 20) launch_wave<22>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     // exact fallback for uncertified queries (usually none; the launch exits at once then)
     if (K <= 8) launch_lane<8>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
