@@ -232,6 +232,31 @@ int imls_register_frame_async(imls_ctx* ctx);
 int imls_register_frame_result(imls_ctx* ctx, double pose_out[16], int* iters_run, int* status,
                                imls_iter_trace* trace);
 
+/* ---- many independent pairs (configs C/D: a KITTI stream, many sequences per GPU) -------- */
+/* Every frame's registration starts from rPose = I against the raw previous scan(s)
+ * (laser_odometry.cpp:484-485, 116-136), so frames are independent: a batch keeps `streams`
+ * contexts (one HIP stream each) and keeps that many registrations in flight, overlapping one
+ * pair's host upload and index build with the others' ICP loops.  One batch per host thread. */
+typedef struct imls_batch imls_batch;
+typedef struct imls_pair_input {
+    const float* src_xyz;             /* the flat (source) cloud, as imls_set_source */
+    const float* src_nrm;
+    size_t n_src;
+    const float* tgt_xyz;             /* the accumulated map, as imls_set_target */
+    const float* tgt_nrm;
+    size_t n_tgt;
+    size_t stride_floats;             /* stride of all four arrays */
+} imls_pair_input;
+imls_batch* imls_batch_create(int device, const imls_params* p, int32_t streams);
+void imls_batch_destroy(imls_batch* b);
+const char* imls_batch_last_error(const imls_batch* b);
+/* Registers pairs[0..n_pairs) (each exactly as imls_set_target + imls_set_source +
+ * imls_register_frame would); poses_out[16·i] (row-major), iters_out[i] and status_out[i]
+ * (imls_frame_status; each nullable) receive pair i's result.  Returns the first error (the
+ * message names the pair); the pairs in flight are drained before returning. */
+int imls_register_batch(imls_batch* b, size_t n_pairs, const imls_pair_input* pairs, double* poses_out,
+                        int32_t* iters_out, int32_t* status_out);
+
 /* ---- upstream producer: ring-neighbourhood PCA normals (scan_registration) ------------- */
 /* scan_registration.compute_normal_method.pca + presample_method.geometric_features
  * (config.json; read at scan_registration.cpp:1140-1145, 1451, 1133).  imls_default_pca_params()

@@ -138,6 +138,13 @@ def default_sample_params(method: int = IMLS_SAMPLE_MAJOR_AXIS) -> ImlsSamplePar
     return p
 
 
+class ImlsPairInput(C.Structure):
+    """imls_pair_input (include/imls_gpu.h)."""
+    _fields_ = [("src_xyz", C.c_void_p), ("src_nrm", C.c_void_p), ("n_src", C.c_size_t),
+                ("tgt_xyz", C.c_void_p), ("tgt_nrm", C.c_void_p), ("n_tgt", C.c_size_t),
+                ("stride_floats", C.c_size_t)]
+
+
 def _bind(lib: C.CDLL) -> C.CDLL:
     P, VP, SZ = C.POINTER, C.c_void_p, C.c_size_t
     sig = {
@@ -171,6 +178,10 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_ring_normals_pca": (C.c_int, [VP, P(ImlsPcaParams), VP, SZ, VP, C.c_int32, VP, VP, VP, VP, VP, VP,
                                             P(SZ), VP]),
         "imls_default_sample_params": (None, [P(ImlsSampleParams), C.c_int32]),
+        "imls_batch_create": (VP, [C.c_int, P(ImlsParams), C.c_int32]),
+        "imls_batch_destroy": (None, [VP]),
+        "imls_batch_last_error": (C.c_char_p, [VP]),
+        "imls_register_batch": (C.c_int, [VP, SZ, VP, VP, VP, VP]),
         "imls_sample_point_cloud": (C.c_int, [VP, P(ImlsSampleParams), VP, VP, SZ, SZ, VP, SZ, VP, SZ, SZ, VP, P(SZ),
                                               VP]),
     }
@@ -189,7 +200,8 @@ ABI_SYMBOLS = (
     "imls_solve_correspondences", "imls_register_frame", "imls_register_frame_async",
     "imls_register_frame_result", "imls_enable_timing", "imls_kernel_timing", "imls_reset_timing",
     "imls_index_stats", "imls_traversal_stats", "imls_default_pca_params", "imls_ring_normals_pca",
-    "imls_default_sample_params", "imls_sample_point_cloud",
+    "imls_default_sample_params", "imls_sample_point_cloud", "imls_batch_create", "imls_batch_destroy",
+    "imls_batch_last_error", "imls_register_batch",
 )
 
 _LIB = None

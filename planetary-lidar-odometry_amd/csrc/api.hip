@@ -798,6 +798,82 @@ int imls_register_frame(imls_ctx* c, double pose_out[16], int* iters_run, int* s
     return imls_register_frame_result(c, pose_out, iters_run, status, trace);
 }
 
+}  // extern "C"
+
+struct imls_batch {
+    std::vector<imls_ctx*> ctx;
+    std::string err;
+};
+
+extern "C" {
+
+imls_batch* imls_batch_create(int device, const imls_params* p, int32_t streams) {
+    if (streams < 1 || streams > 16) return nullptr;
+    imls_batch* b = new imls_batch();
+    for (int s = 0; s < streams; ++s) {
+        imls_ctx* c = imls_create(device, p);
+        if (!c) {
+            imls_batch_destroy(b);
+            return nullptr;
+        }
+        b->ctx.push_back(c);
+    }
+    return b;
+}
+
+void imls_batch_destroy(imls_batch* b) {
+    if (!b) return;
+    for (imls_ctx* c : b->ctx) imls_destroy(c);
+    delete b;
+}
+
+const char* imls_batch_last_error(const imls_batch* b) { return b ? b->err.c_str() : "null batch"; }
+
+int imls_register_batch(imls_batch* b, size_t n_pairs, const imls_pair_input* pairs, double* poses_out,
+                        int32_t* iters_out, int32_t* status_out) {
+    if (!b) return IMLS_ERR_ARG;
+    if (n_pairs > 0 && !pairs) { b->err = "null pairs"; return IMLS_ERR_ARG; }
+    const size_t S = b->ctx.size();
+    std::vector<long long> owner(S, -1);      // pair in flight on each context
+    int first_rc = IMLS_OK;
+    auto collect = [&](size_t s) {
+        const long long i = owner[s];
+        if (i < 0) return;
+        owner[s] = -1;
+        double pose[16];
+        int it = 0, st = 0;
+        const int rc = imls_register_frame_result(b->ctx[s], pose, &it, &st, nullptr);
+        if (rc != IMLS_OK) {
+            if (first_rc == IMLS_OK) {
+                first_rc = rc;
+                b->err = "pair " + std::to_string(i) + ": " + imls_last_error(b->ctx[s]);
+            }
+            return;
+        }
+        if (poses_out) std::memcpy(poses_out + 16 * i, pose, sizeof(pose));
+        if (iters_out) iters_out[i] = it;
+        if (status_out) status_out[i] = st;
+    };
+    for (size_t i = 0; i < n_pairs && first_rc == IMLS_OK; ++i) {
+        const size_t s = i % S;
+        collect(s);                           // the context's previous pair first (its stream is then idle)
+        if (first_rc != IMLS_OK) break;
+        imls_ctx* c = b->ctx[s];
+        const imls_pair_input& q = pairs[i];
+        int rc = imls_set_target(c, q.tgt_xyz, q.tgt_nrm, q.n_tgt, q.stride_floats, nullptr);
+        if (rc == IMLS_OK) rc = imls_set_source(c, q.src_xyz, q.src_nrm, q.n_src, q.stride_floats, nullptr, nullptr);
+        if (rc == IMLS_OK) rc = imls_register_frame_async(c);
+        if (rc != IMLS_OK) {
+            first_rc = rc;
+            b->err = "pair " + std::to_string(i) + ": " + imls_last_error(c);
+            break;
+        }
+        owner[s] = (long long)i;
+    }
+    for (size_t s = 0; s < S; ++s) collect(s);   // drain
+    return first_rc;
+}
+
 void imls_default_pca_params(imls_pca_params* p) {
     // scan_registration section of the shipped config.json (read at scan_registration.cpp:1140-1145, 1451, 1133)
     if (!p) return;

@@ -253,6 +253,52 @@ class ImlsContext:
 # ================================================================================================
 # Reference-shaped API
 # ================================================================================================
+class ImlsBatch:
+    """Many independent scan pairs kept in flight over `streams` contexts (imls_register_batch):
+    each pair is registered exactly as set_target + set_source + register_frame."""
+
+    def __init__(self, params: Optional[_abi.ImlsParams] = None, device: int = 0, streams: int = 4):
+        self.lib = _abi.load_library()
+        p = params if params is not None else _abi.default_params()
+        self._params = p
+        self.b = self.lib.imls_batch_create(device, C.byref(p), streams)
+        if not self.b:
+            raise _abi.ImlsError(_abi.IMLS_ERR_DEVICE, "imls_batch_create failed (no MI355X?)")
+
+    def close(self):
+        if getattr(self, "b", None):
+            self.lib.imls_batch_destroy(self.b)
+            self.b = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def register(self, pairs):
+        """pairs: list of (source_cloud, target_cloud) in any layout set_source/set_target accept.
+        Returns (poses (n,4,4), iterations (n,), statuses (n,))."""
+        keep, arr = [], (_abi.ImlsPairInput * max(len(pairs), 1))()
+        for k, (src, tgt) in enumerate(pairs):
+            s, t = _as_xyzn(src), _as_xyzn(tgt)
+            keep += [s, t]
+            arr[k] = _abi.ImlsPairInput(s.ctypes.data, s.ctypes.data + 12, s.shape[0],
+                                        t.ctypes.data, t.ctypes.data + 12, t.shape[0], 6)
+        n = len(pairs)
+        poses = np.zeros((max(n, 1), 16)); iters = np.zeros(max(n, 1), np.int32); st = np.zeros(max(n, 1), np.int32)
+        rc = self.lib.imls_register_batch(self.b, n, arr, _ptr(poses), _ptr(iters), _ptr(st))
+        if rc != 0:
+            raise _abi.ImlsError(rc, (self.lib.imls_batch_last_error(self.b) or b"").decode())
+        return poses[:n].reshape(n, 4, 4), iters[:n], st[:n]
+
+
 class IMLSICPMatcher:
     """Drop-in mirror of IMLSICPMatcher (imls_icp.h:45-147) backed by the HIP path.
 
