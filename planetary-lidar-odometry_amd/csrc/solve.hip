@@ -386,6 +386,7 @@ __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, S
 // instead of five launches whose fixed latency dominates at this size.  Same arithmetic and the
 // same exact (|r|, row) order as the chain.
 constexpr int kSmallBlock = 256;     // 4 waves: cheap barriers for the sort and reductions
+constexpr unsigned long long kNoKey = ~0ull;   // k_solve_small: slot of an invalid row
 constexpr int kSmallBins = 4096;     // LDS histogram: top 12 bits of the float image of |r| (1/16 octave)
 __device__ __forceinline__ int small_bin(unsigned long long keybits) {
     return (int)(__float_as_uint((float)__longlong_as_double((long long)keybits)) >> 19);
@@ -448,17 +449,20 @@ __global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, c
     __syncthreads();
     DBG_STAMP(1);
     if (stop) return;
-    // |r| under the first solution, valid rows only (solver.cpp:110-122)
+    // |r| under the first solution, valid rows only (solver.cpp:110-122).  Keys stay at their row's
+    // slot (invalid rows hold a sentinel) so every later pass walks the rows in a fixed order: the
+    // second reduction's float sums are then the same run to run (an append order would not be)
     for (int i = t; i < N; i += kSmallBlock) {
         double a[6], b, wt;
+        unsigned long long kb = kNoKey;
         if (rows.get(i, a, b, wt)) {
             double v = a[0] * xs[0];
             for (int k = 1; k < 6; ++k) v = v + a[k] * xs[k];
-            const double key = fabs(v - b);
-            const int at = atomicAdd(&nkey, 1);
-            ck[at] = (unsigned long long)__double_as_longlong(key);
-            cr[at] = (unsigned)i;
+            kb = (unsigned long long)__double_as_longlong(fabs(v - b));
+            atomicAdd(&nkey, 1);
         }
+        ck[i] = kb;
+        cr[i] = (unsigned)i;
     }
     __syncthreads();
     DBG_STAMP(2);
@@ -470,7 +474,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, c
     // (monotone) locates the boundary bins; only their rows are sorted by (|r| bits, row)
     for (int b = t; b < kSmallBins; b += kSmallBlock) hist[b] = 0u;
     __syncthreads();
-    for (int r = t; r < n; r += kSmallBlock) atomicAdd(&hist[small_bin(ck[r])], 1u);
+    for (int r = t; r < N; r += kSmallBlock)
+        if (ck[r] != kNoKey) atomicAdd(&hist[small_bin(ck[r])], 1u);
     __syncthreads();
     {
         constexpr int per = kSmallBins / kSmallBlock;
@@ -496,7 +501,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, c
     __syncthreads();
     const int blo = bsel[0], bhi = bsel[1];
     if (t == 0) bsel[4] = (int)hist[blo];           // candidates of the lower boundary bin
-    for (int r = t; r < n; r += kSmallBlock) {
+    for (int r = t; r < N; r += kSmallBlock) {
+        if (ck[r] == kNoKey) continue;
         const int b = small_bin(ck[r]);
         if (b == blo || b == bhi) {
             const int at = atomicAdd(&ncand, 1);
@@ -523,7 +529,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, c
         for (int p = 0; p < 6; ++p) loc[21 + p] += a[p] * b;
         loc[27] += 1.0;
     };
-    for (int r = t; r < n; r += kSmallBlock) {     // interior bins: kept without ranking
+    for (int r = t; r < N; r += kSmallBlock) {     // interior bins: kept without ranking, row order
+        if (ck[r] == kNoKey) continue;
         const int b = small_bin(ck[r]);
         if (b > blo && b < bhi) add_row(cr[r]);
     }
