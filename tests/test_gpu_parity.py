@@ -261,3 +261,27 @@ def test_config_b_frame_properties(ctx, config_b):
     ctx.set_target(config_b.target[perm])
     b = ctx.project(r1["pose"])
     assert np.array_equal(a[3], b[3]) and np.array_equal(a[1], b[1])
+
+
+def test_non_finite_points_are_dropped_like_the_reference(ctx, traversal):
+    """RemoveNANandINFData (imls_icp.cpp:58-78, 80-103): points with a non-finite xyz are erased from
+    both clouds in place (order kept) before anything else; normals are not checked there (a NaN map
+    normal is rejected later as "invalid normal", 672-679)."""
+    g = golden("vlp16_pair")
+    src, tgt = g["src"].copy(), g["tgt"].copy()
+    rng = np.random.default_rng(11)
+    for cloud in (src, tgt):
+        bad = rng.choice(cloud.shape[1], 40, replace=False)
+        cloud[rng.integers(0, 3, 40), bad] = rng.choice([np.nan, np.inf, -np.inf], 40)
+    tgt[3:6, rng.choice(tgt.shape[1], 25, replace=False)] = np.nan          # NaN map normals
+    p = gparams()
+    ctx.set_params(p)
+    assert ctx.set_target(soa_to_rows(tgt)) == int(np.isfinite(tgt[:3]).all(axis=0).sum())
+    ctx.set_source(soa_to_rows(src))
+    pose = g["pose1"]
+    want = oc.project(src[:, np.isfinite(src[:3]).all(axis=0)], tgt, pose, p)
+    check_projection(ctx.project(pose), want[3], want[4], want[0], want[1], want[2])
+    r = ctx.register_frame()
+    o = oc.register_frame(src[:, np.isfinite(src[:3]).all(axis=0)], tgt, p)
+    assert r["iters"] == o["iters"] and r["status"] == o["status"]
+    assert np.abs(r["pose"] - o["pose"]).max() < POSE_TOL
