@@ -384,7 +384,8 @@ int oracle_sample_point_cloud(const imls_sample_params* p, const float* xyz, con
             const auto& bin = hist[b];
             const int sz = (int)bin.size();
             if (sz < p->min_points_per_bin) continue;
-            const int k = std::min(static_cast<int>(w[b] * p->max_total_points), sz);
+            const float wk = w[b] * p->max_total_points;        // x86 cvttss2si: NaN / out of range → INT_MIN
+            const int k = std::min((wk > -2147483904.0f && wk < 2147483648.0f) ? static_cast<int>(wk) : INT32_MIN, sz);
             if (sz > k) sample_bin(c, bin, k, p->sampling_strategy, out, rng);
             else out.insert(out.end(), bin.begin(), bin.end());
         }

@@ -205,6 +205,13 @@ int host_rand_next(int* st) {
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// static_cast<int>(float) as the reference's x86-64 build evaluates it (cvttss2si): truncation, and
+// the "integer indefinite" INT_MIN for NaN / out-of-range (all-zero weights make them NaN, 721-723)
+// — spelled out here because the C++ cast is undefined there.
+int x86_float_to_int(float v) {
+    return (v > -2147483904.0f && v < 2147483648.0f) ? static_cast<int>(v) : std::numeric_limits<int>::min();
+}
+
 // Smallest float t ≥ 0 with sqrt(t) ≥ r in correctly rounded float arithmetic (x86 sqrtss is
 // correctly rounded, as is the device's sqrt_rn), so `sqrt(s) < r` ⇔ `s < t` for every float s ≥ 0.
 float sqrt_threshold(float r) {
@@ -350,7 +357,7 @@ int sample_run(hipStream_t s, const imls_sample_params& p, const float* xyz, con
         plan[b].kind = -1;
         if (sz < p.min_points_per_bin) continue;
         const int k = p.method == IMLS_SAMPLE_MAJOR_AXIS
-                          ? std::min(static_cast<int>(w[b] * p.max_total_points), sz)   // 732
+                          ? std::min(x86_float_to_int(w[b] * p.max_total_points), sz)   // 732
                           : p.max_points_per_bin;                                        // 603
         if (sz <= k) { plan[b].kind = 0; continue; }
         if (p.sampling_strategy == 0) {
