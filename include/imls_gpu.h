@@ -50,7 +50,9 @@ typedef enum imls_match_method {
 typedef enum imls_solve_method {
     IMLS_SOLVE_LS = 0,          /* "LS"     → SolveMotionEstimationProblemLS (solver.cpp:74-166) */
     IMLS_SOLVE_RANSAC = 1,      /* "RANSAC" → SolveMotionEstimationProblemRANSAC (solver.cpp:222-385) */
-    IMLS_SOLVE_WEIGHTED_LS = 2  /* "Weighted LS" (solver.cpp:168-220); unit weights when used directly */
+    IMLS_SOLVE_WEIGHTED_LS = 2, /* "Weighted LS" (solver.cpp:168-220); unit weights when used directly */
+    IMLS_SOLVE_DRPM = 3         /* SolveMotionEstimationProblemDRPM (solver.cpp:499-603) on caller rows:
+                                   imls_solve_correspondences only (RANSAC's final, not a loop method) */
 } imls_solve_method;
 
 /* solve_method.RANSAC.final_solve_method (config.json; solver.cpp:368-384) */
@@ -133,7 +135,10 @@ typedef struct imls_params {
     double drpm_threshold;
     double drpm_stdev_points;
     double drpm_stdev_normals;
-    uint32_t ransac_seed;             /* glibc rand() seed; 1 = the reference's unseeded process */
+    uint32_t ransac_seed;             /* glibc rand() seed of the context's stream; 1 = the reference's
+                                         unseeded process.  Applied at imls_create and whenever
+                                         imls_set_params changes it; the stream then runs on across
+                                         every RANSAC solve and frame (see imls_seed_rng) */
 
     /* laser_odometry */
     int32_t transform_normal;         /* laser_odometry.transform_normal (laser_odometry.cpp:541-548) */
@@ -167,6 +172,20 @@ const char* imls_last_error(const imls_ctx* ctx);
 int imls_set_stream(imls_ctx* ctx, void* hip_stream);
 int imls_synchronize(imls_ctx* ctx);
 
+/* glibc rand() stream of the RANSAC solver.  The reference draws its hypotheses from the one
+ * process-wide rand() stream (common.cpp:49 via solver.cpp:245-262; srand is never called, so it
+ * starts from seed 1 and runs on across every ICP iteration and every frame).  A context keeps its
+ * own device-resident copy of that stream and continues it across imls_solve,
+ * imls_solve_correspondences and imls_register_frame exactly as the reference's sequential calls
+ * consume it.  imls_seed_rng restarts it (= srand(seed)); imls_get_rng_state / imls_set_rng_state
+ * (the glibc TYPE_3 state: 31 words, front index, rear index, 0) hand one stream from a context to
+ * another, e.g. when a caller creates a fresh context per frame as the reference creates a fresh
+ * matcher (laser_odometry.cpp:489).  Contexts used concurrently (imls_register_batch) each run
+ * their own stream. */
+int imls_seed_rng(imls_ctx* ctx, uint32_t seed);
+int imls_get_rng_state(imls_ctx* ctx, int32_t state[34]);
+int imls_set_rng_state(imls_ctx* ctx, const int32_t state[34]);
+
 /* ---- clouds ---------------------------------------------------------------------------- */
 /* Replaces IMLSICPMatcher::setTargetPointCloud (imls_icp.cpp:80-103): drops points with
  * non-finite xyz (RemoveNANandINFData, imls_icp.cpp:58-72), keeps order, builds the index.
@@ -182,6 +201,22 @@ int imls_set_source(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n,
  * (x[], y[], z[], nx[], ny[], nz[]) — inputs stay in HBM, no PCIe in the hot loop. */
 int imls_set_target_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
 int imls_set_source_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
+
+/* Map FIFO kept in HBM: replaces accumulateTargetCloud(newCloud, max_queue_size, ...)
+ * (laser_odometry.cpp:116-136, called at 663-664) followed by the next frame's
+ * setTargetPointCloud(accumulatedTargetCloud) (509-510; imls_icp.cpp:80-103).  The new filtered
+ * scan (untransformed, as the reference keeps it) becomes the FIFO's newest entry; when the FIFO
+ * then holds more than params.max_queue_size entries the oldest is dropped (once, like the
+ * reference's `if`); the entries are concatenated oldest first on the device and the target index
+ * is rebuilt over the concatenation (NaN filter included).  Only the new scan crosses PCIe: the
+ * older ones stay resident.  n_map (nullable) receives the map size after the NaN filter.
+ * imls_set_target replaces the index without touching the FIFO. */
+int imls_map_push(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n, size_t stride_floats,
+                  size_t* n_map);
+int imls_map_push_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_map);
+int imls_map_clear(imls_ctx* ctx);
+/* FIFO entries and their total point count (before the NaN filter). */
+int imls_map_size(imls_ctx* ctx, size_t* entries, size_t* points);
 
 /* Tensor voting input (use_tensor_voting): the target's per-point input tensors T — what
  * VoteForAny's tv_input.encode(m_targetPointCloudDP, AWARE_TENSOR) produces (imls_icp.cpp:179,
@@ -213,8 +248,10 @@ int imls_project(imls_ctx* ctx, const double pose[16], float* x_out, float* y_ou
 /* Replaces solveMotionEstimationProblem(solve_method, ...) (laser_odometry.cpp:173-275) on the
  * device-resident correspondences of the last imls_project.  *ok mirrors the bool return. */
 int imls_solve(imls_ctx* ctx, double delta_out[16], int* ok);
-/* Replaces SolveMotionEstimationProblemLS / WeightedLS (solver.cpp:74-220) on host arrays of
- * N double triples (s = source, d = target, n = target normal; weights nullable = unit). */
+/* Replaces SolveMotionEstimationProblemLS / WeightedLS / RANSAC / DRPM (solver.cpp:74-385,
+ * 499-603) on host arrays of N double triples (s = source, d = target, n = target normal; weights
+ * nullable = unit; LS uses params.ls_threshold, RANSAC the ransac_* fields and the context's rand()
+ * stream, DRPM drpm_threshold / drpm_stdev_points / drpm_stdev_normals). */
 int imls_solve_correspondences(imls_ctx* ctx, int32_t method, const double* s, const double* d,
                                const double* n, const double* weights, size_t N,
                                double delta_out[16], int* ok);

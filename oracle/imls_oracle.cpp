@@ -12,6 +12,7 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <limits>
 #include <numeric>
@@ -968,6 +969,11 @@ bool solve_dispatch(int method, const double* s, const double* d, const double* 
         case IMLS_SOLVE_LS: return solve_ls(s, d, n, N, p->ls_threshold, D, kept);
         case IMLS_SOLVE_WEIGHTED_LS: return solve_wls(s, d, n, w, N, D);
         case IMLS_SOLVE_RANSAC: return solve_ransac(s, d, n, N, p, rs, D);
+        case IMLS_SOLVE_DRPM: {   // stand-alone SolveMotionEstimationProblemDRPM; null weights = unit
+            std::vector<double> ones;
+            if (!w) { ones.assign(N, 1.0); w = ones.data(); }
+            return solve_drpm(s, d, n, w, N, p->drpm_threshold, p->drpm_stdev_points, p->drpm_stdev_normals, D);
+        }
         default: return false;
     }
 }
@@ -1055,6 +1061,16 @@ int oracle_register_frame_tv(const float* src6, size_t N, const float* tgt6, siz
                              const imls_params* p, double pose_out[16], int* iters_run, int* status,
                              imls_iter_trace* trace, int corr_iter, float* corr, size_t* corr_n,
                              double* seconds_index, double* seconds_total) {
+    return oracle_register_frame_rs(src6, N, tgt6, M, ten6, p, nullptr, pose_out, iters_run, status, trace, corr_iter,
+                                    corr, corr_n, seconds_index, seconds_total);
+}
+
+// rand_state (nullable, int32[34]): the process-wide glibc rand() stream RANSAC draws from, carried
+// across frames like the reference's (it never calls srand); null = a fresh stream from ransac_seed.
+int oracle_register_frame_rs(const float* src6, size_t N, const float* tgt6, size_t M, const float* ten6,
+                             const imls_params* p, int32_t* rand_state, double pose_out[16], int* iters_run,
+                             int* status, imls_iter_trace* trace, int corr_iter, float* corr, size_t* corr_n,
+                             double* seconds_index, double* seconds_total) {
     if (!p || p->search_number <= 0 || p->search_number > 64) return IMLS_ERR_ARG;
     if (p->use_tensor_voting && (p->tensor_k <= 0 || p->tensor_k > 64)) return IMLS_ERR_ARG;
     auto t0 = std::chrono::steady_clock::now();
@@ -1062,8 +1078,9 @@ int oracle_register_frame_tv(const float* src6, size_t N, const float* tgt6, siz
     Matcher m{p, load_filtered(tgt6, M), {}, load_tensors(tgt6, M, ten6)};
     m.tree.build(m.tgt);
     auto t1 = std::chrono::steady_clock::now();
-    int32_t rs[34];
-    rand_seed(rs, p->ransac_seed);
+    int32_t local[34];
+    int32_t* rs = rand_state;
+    if (!rs) { rand_seed(local, p->ransac_seed); rs = local; }
     Mat4 pose = mat4_identity();
     int st = IMLS_FRAME_MAX_ITERS, it = 0;
     Corr c;
@@ -1131,6 +1148,45 @@ int oracle_tv_normals(const float* tgt6, size_t M, const float* ten6, const floa
 }
 
 void oracle_rand_seed(int32_t* state, uint32_t seed) { rand_seed(state, seed); }
+
+// nowPose = prevLaserPose * rPose (laser_odometry.cpp:652): Eigen's 4x4 product, k = 0..3 in order.
+void oracle_chain_pose(const double prev[16], const double rel[16], double out[16]) {
+    Mat4 a, b;
+    std::memcpy(a.m, prev, sizeof(a.m));
+    std::memcpy(b.m, rel, sizeof(b.m));
+    Mat4 c = mat4_mul(a, b);
+    std::memcpy(out, c.m, sizeof(c.m));
+}
+
+// savePoseToFile (saver.cpp:46-54): Eigen::Quaterniond(Matrix3d) (Eigen's quaternionbase_assign_impl
+// for a 3x3: trace branch, else the largest-diagonal branch with strict '>'), then
+// `std::fixed << std::setprecision(6)`: ts tx ty tz qx qy qz qw.  Returns the line length.
+int oracle_format_pose(const double P[16], const char* timestamp, char* buf, size_t cap) {
+    auto m = [&](int r, int c) { return P[r * 4 + c]; };
+    double q[4];   // x y z w
+    double t = (m(0, 0) + m(1, 1)) + m(2, 2);
+    if (t > 0.0) {
+        t = std::sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m(2, 1) - m(1, 2)) * t;
+        q[1] = (m(0, 2) - m(2, 0)) * t;
+        q[2] = (m(1, 0) - m(0, 1)) * t;
+    } else {
+        int i = 0;
+        if (m(1, 1) > m(0, 0)) i = 1;
+        if (m(2, 2) > m(i, i)) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = std::sqrt(((m(i, i) - m(j, j)) - m(k, k)) + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m(k, j) - m(j, k)) * t;
+        q[j] = (m(j, i) + m(i, j)) * t;
+        q[k] = (m(k, i) + m(i, k)) * t;
+    }
+    return std::snprintf(buf, cap, "%s %.6f %.6f %.6f %.6f %.6f %.6f %.6f\n", timestamp, m(0, 3), m(1, 3), m(2, 3), q[0],
+                         q[1], q[2], q[3]);
+}
 void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
 int32_t oracle_rand_next(int32_t* state) { return rand_next(state); }
 

@@ -70,6 +70,19 @@ int oracle_register_frame_tv(const float* src6, size_t N, const float* tgt6, siz
                              float* corr, size_t* corr_n, double* seconds_index,
                              double* seconds_total);
 
+/* oracle_register_frame_tv with the RANSAC rand() stream carried in `rand_state` (nullable,
+ * int32[34]; null = a fresh stream from p->ransac_seed), as the reference's process-wide rand(). */
+int oracle_register_frame_rs(const float* src6, size_t N, const float* tgt6, size_t M,
+                             const float* ten6, const imls_params* p, int32_t* rand_state,
+                             double pose_out[16], int* iters_run, int* status,
+                             imls_iter_trace* trace, int corr_iter, float* corr, size_t* corr_n,
+                             double* seconds_index, double* seconds_total);
+
+/* nowPose = prevLaserPose * rPose (laser_odometry.cpp:652) and one savePoseToFile line
+ * (saver.cpp:46-54, Eigen quaternion + fixed/6) into buf; returns its length. */
+void oracle_chain_pose(const double prev[16], const double rel[16], double out[16]);
+int oracle_format_pose(const double pose[16], const char* timestamp, char* buf, size_t cap);
+
 /* glibc rand() restated (common.cpp:49 consumes it).  Fills 34-word state for srand(seed). */
 void oracle_rand_seed(int32_t* state, uint32_t seed);
 int32_t oracle_rand_next(int32_t* state);

@@ -43,6 +43,10 @@ def lib():
         L.oracle_project_tv.argtypes = [VP, SZ, VP, SZ, VP, VP, P(abi.ImlsParams), VP, VP, VP, VP, P(SZ), VP]
         L.oracle_register_frame_tv.argtypes = [VP, SZ, VP, SZ, VP, P(abi.ImlsParams), VP, P(C.c_int), P(C.c_int), VP,
                                                C.c_int, VP, P(SZ), P(C.c_double), P(C.c_double)]
+        L.oracle_register_frame_rs.argtypes = [VP, SZ, VP, SZ, VP, P(abi.ImlsParams), VP, VP, P(C.c_int), P(C.c_int),
+                                               VP, C.c_int, VP, P(SZ), P(C.c_double), P(C.c_double)]
+        L.oracle_chain_pose.argtypes = [VP, VP, VP]
+        L.oracle_format_pose.argtypes = [VP, C.c_char_p, C.c_char_p, SZ]
         L.oracle_tv_normals.argtypes = [VP, SZ, VP, VP, SZ, P(abi.ImlsParams), VP, VP, VP]
         L.oracle_rand_seed.argtypes = [VP, C.c_uint32]
         L.oracle_rand_next.argtypes = [VP]
@@ -124,7 +128,9 @@ def tv_normals(tgt6, tensors, q3, params):
     return nrm, found, acc.reshape(Q, 3, 3)
 
 
-def register_frame(src6, tgt6, params, corr_iter=-1, tensors=None):
+def register_frame(src6, tgt6, params, corr_iter=-1, tensors=None, rand_state=None):
+    """One frame (laser_odometry.cpp:478-660).  rand_state (int32[34], updated in place) carries the
+    RANSAC rand() stream across frames; None = a fresh stream from params.ransac_seed."""
     src6, tgt6 = _soa6(src6), _soa6(tgt6)
     ten = _ten6(tensors, tgt6.shape[1])
     abi = _abi()
@@ -134,16 +140,42 @@ def register_frame(src6, tgt6, params, corr_iter=-1, tensors=None):
     N = src6.shape[1]
     corr = np.zeros((N, 9), np.float32) if corr_iter >= 0 else None
     cn = C.c_size_t(); ti = C.c_double(); tt = C.c_double()
-    rc = lib().oracle_register_frame_tv(_ptr(src6), N, _ptr(tgt6), tgt6.shape[1], None if ten is None else _ptr(ten),
-                                        C.byref(params), _ptr(pose),
-                                     C.byref(iters), C.byref(status), trace, corr_iter,
-                                     None if corr is None else _ptr(corr), C.byref(cn), C.byref(ti), C.byref(tt))
+    if rand_state is not None:
+        assert rand_state.dtype == np.int32 and rand_state.shape == (34,) and rand_state.flags.c_contiguous
+    rc = lib().oracle_register_frame_rs(_ptr(src6), N, _ptr(tgt6), tgt6.shape[1], None if ten is None else _ptr(ten),
+                                        C.byref(params), None if rand_state is None else _ptr(rand_state), _ptr(pose),
+                                        C.byref(iters), C.byref(status), trace, corr_iter,
+                                        None if corr is None else _ptr(corr), C.byref(cn), C.byref(ti), C.byref(tt))
     assert rc == 0
     out = dict(pose=pose.reshape(4, 4), iters=iters.value, status=status.value,
                trace=[trace[k] for k in range(iters.value)], seconds_index=ti.value, seconds_total=tt.value)
     if corr is not None:
         out["corr"] = corr[:cn.value]
     return out
+
+
+def rand_state(seed=1):
+    """glibc srand(seed) state (int32[34])."""
+    st = np.zeros(34, np.int32)
+    lib().oracle_rand_seed(_ptr(st), seed)
+    return st
+
+
+def chain_pose(prev, rel):
+    a = np.ascontiguousarray(prev, dtype=np.float64).reshape(16)
+    b = np.ascontiguousarray(rel, dtype=np.float64).reshape(16)
+    out = np.zeros(16)
+    lib().oracle_chain_pose(_ptr(a), _ptr(b), _ptr(out))
+    return out.reshape(4, 4)
+
+
+def format_pose(pose, timestamp: str) -> str:
+    """savePoseToFile's line (saver.cpp:46-54)."""
+    P = np.ascontiguousarray(pose, dtype=np.float64).reshape(16)
+    buf = C.create_string_buffer(512)
+    n = lib().oracle_format_pose(_ptr(P), timestamp.encode(), buf, 512)
+    assert 0 < n < 512
+    return buf.value.decode()
 
 
 def rand_sequence(seed, n):

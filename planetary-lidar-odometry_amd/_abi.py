@@ -15,7 +15,7 @@ LIB_PATH = PKG_DIR / "csrc" / "libimls_gpu.so"
 
 IMLS_OK, IMLS_ERR_ARG, IMLS_ERR_DEVICE, IMLS_ERR_STATE, IMLS_ERR_UNSUPPORTED, IMLS_ERR_CAPACITY = 0, -1, -2, -3, -4, -5
 IMLS_MATCH_IMLS, IMLS_MATCH_PLANE_ICP = 0, 1
-IMLS_SOLVE_LS, IMLS_SOLVE_RANSAC, IMLS_SOLVE_WEIGHTED_LS = 0, 1, 2
+IMLS_SOLVE_LS, IMLS_SOLVE_RANSAC, IMLS_SOLVE_WEIGHTED_LS, IMLS_SOLVE_DRPM = 0, 1, 2, 3
 IMLS_FINAL_LS, IMLS_FINAL_WEIGHTED_LS, IMLS_FINAL_DRPM = 0, 1, 2
 IMLS_FRAME_MAX_ITERS, IMLS_FRAME_CONVERGED, IMLS_FRAME_TOO_FEW, IMLS_FRAME_SOLVE_FAILED = 0, 1, 2, 3
 REJECT_NAMES = ("no_normal", "too_far", "invalid_normal", "normal_constraint", "mls_fail", "nan_inf_height")
@@ -184,6 +184,13 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_register_batch": (C.c_int, [VP, SZ, VP, VP, VP, VP]),
         "imls_sample_point_cloud": (C.c_int, [VP, P(ImlsSampleParams), VP, VP, SZ, SZ, VP, SZ, VP, SZ, SZ, VP, P(SZ),
                                               VP]),
+        "imls_seed_rng": (C.c_int, [VP, C.c_uint32]),
+        "imls_get_rng_state": (C.c_int, [VP, VP]),
+        "imls_set_rng_state": (C.c_int, [VP, VP]),
+        "imls_map_push": (C.c_int, [VP, VP, VP, SZ, SZ, P(SZ)]),
+        "imls_map_push_device": (C.c_int, [VP, VP, SZ, P(SZ)]),
+        "imls_map_clear": (C.c_int, [VP]),
+        "imls_map_size": (C.c_int, [VP, P(SZ), P(SZ)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -201,7 +208,8 @@ ABI_SYMBOLS = (
     "imls_register_frame_result", "imls_enable_timing", "imls_kernel_timing", "imls_reset_timing",
     "imls_index_stats", "imls_traversal_stats", "imls_default_pca_params", "imls_ring_normals_pca",
     "imls_default_sample_params", "imls_sample_point_cloud", "imls_batch_create", "imls_batch_destroy",
-    "imls_batch_last_error", "imls_register_batch",
+    "imls_batch_last_error", "imls_register_batch", "imls_seed_rng", "imls_get_rng_state",
+    "imls_set_rng_state", "imls_map_push", "imls_map_push_device", "imls_map_clear", "imls_map_size",
 )
 
 _LIB = None

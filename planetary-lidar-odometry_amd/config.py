@@ -16,7 +16,11 @@ from . import _abi
 DEFAULT_CONFIG = pathlib.Path(__file__).resolve().parent / "config" / "config.json"
 
 MATCHING = {"IMLS": _abi.IMLS_MATCH_IMLS, "plane_ICP": _abi.IMLS_MATCH_PLANE_ICP}
-SOLVING = {"LS": _abi.IMLS_SOLVE_LS, "RANSAC": _abi.IMLS_SOLVE_RANSAC, "Weighted LS": _abi.IMLS_SOLVE_WEIGHTED_LS}
+# The top-level solve_method names the reference's dispatcher accepts (laser_odometry.cpp:183-272).
+# "Weighted LS" is only a RANSAC final method there: as a top-level name it hits "Invalid
+# SOLVE_METHOD!", so it is rejected here too (the C ABI's IMLS_SOLVE_WEIGHTED_LS is an extension
+# for callers that want a unit-weight WLS loop, never produced from a config file).
+SOLVING = {"LS": _abi.IMLS_SOLVE_LS, "RANSAC": _abi.IMLS_SOLVE_RANSAC}
 FINAL = {"LS": _abi.IMLS_FINAL_LS, "Weighted LS": _abi.IMLS_FINAL_WEIGHTED_LS, "DRPM": _abi.IMLS_FINAL_DRPM}
 # Third-party solver engines (solver.cpp:25-72, 387-483): outside the GPU path.
 UNSUPPORTED_SOLVERS = ("Ceres", "ICP", "Teaser")
@@ -36,8 +40,10 @@ def load(path: str | pathlib.Path | None = None) -> dict:
 
 
 def params_from_config(cfg: dict) -> _abi.ImlsParams:
-    """Build imls_params from the reference key paths.  Unknown method names raise ConfigError
-    (the reference prints "Invalid MATCHING_METHOD!" / "Invalid SOLVE_METHOD!" and fails)."""
+    """Build imls_params from the reference key paths.  Unknown method names raise ConfigError.
+    Deliberate change, documented in INTEGRATION.md: the reference prints "Invalid
+    MATCHING_METHOD!" / "Invalid SOLVE_METHOD!" and keeps running with every frame's solve failing
+    (rPose = I for every frame); this fails once, at configuration time."""
     lo = cfg["laser_odometry"]
     mm = lo["matching_method"]
     sm = lo["solve_method"]

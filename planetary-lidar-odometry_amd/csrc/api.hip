@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -28,7 +29,14 @@ struct imls_ctx {
     int M = 0, Pl = 0, levels = 0;
     bool has_target = false;
     // source
-    DevBuf spt, snr, sscratch, qperm, upload_s;
+    DevBuf spt, snr, sscratch, qperm, upload_s, skept;
+    // map FIFO (accumulateTargetCloud, laser_odometry.cpp:116-136): the last max_queue_size filtered
+    // scans, each SoA6 in its own slot, and their concatenation (oldest first) the index is built from
+    struct MapSlot { DevBuf buf; size_t n = 0; };
+    std::deque<MapSlot> fifo;
+    std::vector<DevBuf> slot_pool;        // freed slots, reused (no allocation per frame)
+    DevBuf macc;
+    size_t map_points = 0;                // Σ n over the FIFO (before the NaN filter)
     DevBuf fb;                            // fallback query list + count
     DevBuf lkeys;                         // leaf first Morton keys + quantisation (seed search)
     DevBuf rnr;                           // recomputed map normals (count mode), Morton order
@@ -51,6 +59,8 @@ struct imls_ctx {
     DevBuf cs, cd, cn, solve_mem, trace_mem, stats, rows_d, pose_tmp;
     DevBuf ransac_mem, rng;               // RANSAC scratch + the glibc rand() state (34 words)
     int rng_seed_state[34] = {};          // host copy of the seeded state (source of the async upload)
+    bool rng_dirty = true;                // upload rng_seed_state to the device before its next use
+    bool rng_init = false;                // seeded from params.ransac_seed (first imls_set_params)
     SolveState st{};
     int st_N = -1, trace_cap = 0;
     bool has_corr = false;
@@ -233,14 +243,27 @@ RansacParams ransac_params(const imls_params& p) {
     return r;
 }
 
-// RANSAC scratch for `rows` rows and the rand() state re-seeded from params.ransac_seed (per frame
-// and per stand-alone solve, as the oracle does); async on the context stream.
+// The context's glibc rand() state lives on the device and runs on across every RANSAC solve and
+// every frame, like the reference's one process-wide rand() stream (solver.cpp / common.cpp:49 never
+// call srand).  It is seeded from params.ransac_seed at context creation, when imls_set_params
+// changes ransac_seed, and by imls_seed_rng; imls_set_rng_state hands a stream from one context to
+// the next.  Async on the context stream.
+int sync_rng(imls_ctx* c) {
+    if (!grow(c->rng, 34 * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (rand state)");
+    if (!c->rng_dirty) return IMLS_OK;
+    if (hipMemcpyAsync(c->rng.p, c->rng_seed_state, 34 * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "rand state upload");
+    // the source must stay valid until the copy ran: wait (seeding is rare)
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "rand state upload");
+    c->rng_dirty = false;
+    return IMLS_OK;
+}
+
+// RANSAC scratch for `rows` rows and the (persistent) rand() state.
 int prepare_ransac(imls_ctx* c, int rows) {
     if (c->P.solve_method != IMLS_SOLVE_RANSAC) return IMLS_OK;
-    if (!grow(c->ransac_mem, ransac_bytes(rows)) || !grow(c->rng, 34 * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (RANSAC)");
-    ransac_seed_host(c->P.ransac_seed, c->rng_seed_state);
-    hipMemcpyAsync(c->rng.p, c->rng_seed_state, 34 * 4, hipMemcpyHostToDevice, c->stream);
-    return IMLS_OK;
+    if (!grow(c->ransac_mem, ransac_bytes(rows))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (RANSAC)");
+    return sync_rng(c);
 }
 
 TreeView tree_view(imls_ctx* c);
@@ -396,11 +419,8 @@ int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
 }
 
 int do_set_source(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept, uint32_t* kept_index) {
-    std::vector<uint32_t> kept;
-    int rc = load_source(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, c->qperm, &c->N,
-                         kept_index ? &kept : nullptr, c->err);
+    int rc = load_source(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, c->qperm, &c->N, c->skept, kept_index, c->err);
     if (rc) return rc;
-    if (kept_index && !kept.empty()) std::memcpy(kept_index, kept.data(), kept.size() * 4);
     c->has_source = c->N > 0;
     c->has_corr = false;
     if (n_kept) *n_kept = (size_t)c->N;
@@ -518,6 +538,10 @@ void imls_destroy(imls_ctx* c) {
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
+    for (auto& sl : c->fifo) if (sl.buf.p) (void)hipFree(sl.buf.p);
+    for (auto& b : c->slot_pool) if (b.p) (void)hipFree(b.p);
+    if (c->macc.p) (void)hipFree(c->macc.p);
+    if (c->skept.p) (void)hipFree(c->skept.p);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->h_trace) (void)hipHostFree(c->h_trace);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
@@ -529,12 +553,47 @@ int imls_set_params(imls_ctx* c, const imls_params* p) {
     if (!c) return IMLS_ERR_ARG;
     int rc = check_params(c, p);
     if (rc) return rc;
+    if (!c->rng_init || p->ransac_seed != c->P.ransac_seed) {   // creation, or a new seed: restart the stream
+        c->rng_init = true;
+        ransac_seed_host(p->ransac_seed, c->rng_seed_state);
+        c->rng_dirty = true;
+    }
     c->P = *p;
     c->kp = make_kparams(*p);
     return IMLS_OK;
 }
 
 const char* imls_last_error(const imls_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int imls_seed_rng(imls_ctx* c, uint32_t seed) {
+    if (!c) return IMLS_ERR_ARG;
+    c->P.ransac_seed = seed;
+    ransac_seed_host(seed, c->rng_seed_state);
+    c->rng_dirty = true;
+    return IMLS_OK;
+}
+
+int imls_get_rng_state(imls_ctx* c, int32_t state[34]) {
+    if (!c || !state) return IMLS_ERR_ARG;
+    if (c->rng_dirty || !c->rng.p) {                  // not on the device yet: the pending seed is the state
+        std::memcpy(state, c->rng_seed_state, 34 * 4);
+        return IMLS_OK;
+    }
+    if (int rc = check_device(c)) return rc;
+    if (hipMemcpyAsync(state, c->rng.p, 34 * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "rand state download");
+    return IMLS_OK;
+}
+
+int imls_set_rng_state(imls_ctx* c, const int32_t state[34]) {
+    if (!c || !state) return IMLS_ERR_ARG;
+    const int f = state[31], r = state[32];
+    if (f < 0 || f > 30 || r < 0 || r > 30 || (f - r + 31) % 31 != 3) return fail(c, IMLS_ERR_ARG, "not a glibc TYPE_3 rand() state");
+    std::memcpy(c->rng_seed_state, state, 34 * 4);
+    c->rng_dirty = true;
+    return IMLS_OK;
+}
 
 int imls_set_stream(imls_ctx* c, void* s) {
     if (!c) return IMLS_ERR_ARG;
@@ -558,6 +617,83 @@ int imls_set_target_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n
     if (!c || !d_soa6) return IMLS_ERR_ARG;
     if (int rc = check_device(c)) return rc;
     return do_set_target(c, d_soa6, n, n_kept);
+}
+
+// accumulateTargetCloud (laser_odometry.cpp:116-136) + setTargetPointCloud(accumulatedTargetCloud)
+// (imls_icp.cpp:80-103): the new scan goes to a FIFO slot (`from_host`: packed + uploaded, the only
+// PCIe traffic; else copied device-to-device), the oldest entry is dropped once when the FIFO holds
+// more than max_queue_size (the reference's `if`, not a loop), the entries are concatenated oldest
+// first into one SoA6 map in HBM (one 2-D device copy per entry) and the index is rebuilt over it.
+static int map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, size_t stride, const float* d_soa6,
+                    size_t* n_map) {
+    if (n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "scan too large");
+    imls_ctx::MapSlot sl;
+    if (!c->slot_pool.empty()) { sl.buf = c->slot_pool.back(); c->slot_pool.pop_back(); }
+    sl.n = n;
+    if (n > 0) {
+        if (!grow(sl.buf, n * 24)) { c->slot_pool.push_back(sl.buf); return fail(c, IMLS_ERR_DEVICE, "hipMalloc (map slot)"); }
+        int rc = IMLS_OK;
+        if (d_soa6) {
+            if (hipMemcpyAsync(sl.buf.p, d_soa6, n * 24, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+                rc = fail(c, IMLS_ERR_DEVICE, "map slot copy");
+        } else {
+            rc = upload_soa6(c, sl.buf, xyz, nrm, n, stride);
+        }
+        if (rc) { c->slot_pool.push_back(sl.buf); return rc; }
+    }
+    c->fifo.push_back(sl);
+    c->map_points += n;
+    if (c->fifo.size() > (size_t)std::max(c->P.max_queue_size, 0)) {
+        c->map_points -= c->fifo.front().n;
+        c->slot_pool.push_back(c->fifo.front().buf);
+        c->fifo.pop_front();
+    }
+    const size_t M = c->map_points;
+    if (M == 0) {                     // empty map (max_queue_size 0 or empty scans): no target
+        c->has_target = false;
+        c->has_corr = false;
+        c->M = 0;
+        if (n_map) *n_map = 0;
+        return IMLS_OK;
+    }
+    if (!grow(c->macc, M * 24)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (map)");
+    size_t off = 0;
+    for (const auto& e : c->fifo) {
+        if (e.n == 0) continue;
+        if (hipMemcpy2DAsync((float*)c->macc.p + off, M * 4, e.buf.p, e.n * 4, e.n * 4, 6, hipMemcpyDeviceToDevice,
+                             c->stream) != hipSuccess)
+            return fail(c, IMLS_ERR_DEVICE, "map assembly copy");
+        off += e.n;
+    }
+    return do_set_target(c, (const float*)c->macc.p, M, n_map);
+}
+
+int imls_map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, size_t stride, size_t* n_map) {
+    if (!c) return IMLS_ERR_ARG;
+    if (n > 0 && (!xyz || !nrm || stride < 3)) return fail(c, IMLS_ERR_ARG, "bad cloud pointer/stride");
+    if (int rc = check_device(c)) return rc;
+    return map_push(c, xyz, nrm, n, stride, nullptr, n_map);
+}
+
+int imls_map_push_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_map) {
+    if (!c || (n > 0 && !d_soa6)) return IMLS_ERR_ARG;
+    if (int rc = check_device(c)) return rc;
+    return map_push(c, nullptr, nullptr, n, 0, d_soa6, n_map);
+}
+
+int imls_map_clear(imls_ctx* c) {
+    if (!c) return IMLS_ERR_ARG;
+    for (auto& e : c->fifo) c->slot_pool.push_back(e.buf);
+    c->fifo.clear();
+    c->map_points = 0;
+    return IMLS_OK;
+}
+
+int imls_map_size(imls_ctx* c, size_t* entries, size_t* points) {
+    if (!c) return IMLS_ERR_ARG;
+    if (entries) *entries = c->fifo.size();
+    if (points) *points = c->map_points;
+    return IMLS_OK;
 }
 
 int imls_set_target_tensors(imls_ctx* c, const float* tens, size_t n, size_t stride) {
@@ -690,7 +826,8 @@ int imls_solve(imls_ctx* c, double delta_out[16], int* ok) {
 int imls_solve_correspondences(imls_ctx* c, int32_t method, const double* s, const double* d, const double* n,
                                const double* w, size_t N, double delta_out[16], int* ok) {
     if (!c || !s || !d || !n || !delta_out) return IMLS_ERR_ARG;
-    if (method != IMLS_SOLVE_LS && method != IMLS_SOLVE_WEIGHTED_LS && method != IMLS_SOLVE_RANSAC)
+    if (method != IMLS_SOLVE_LS && method != IMLS_SOLVE_WEIGHTED_LS && method != IMLS_SOLVE_RANSAC &&
+        method != IMLS_SOLVE_DRPM)
         return fail(c, IMLS_ERR_UNSUPPORTED, "method");
     if (N > (size_t)0x3fffffff) return fail(c, IMLS_ERR_ARG, "N too large");
     if (int rc = check_device(c)) return rc;
@@ -713,6 +850,8 @@ int imls_solve_correspondences(imls_ctx* c, int32_t method, const double* s, con
     const int rc0 = prepare_ransac(c, (int)std::max<size_t>(N, 1));
     c->P.solve_method = saved;
     if (rc0) return rc0;
+    if (method == IMLS_SOLVE_DRPM && !grow(c->ransac_mem, ransac_bytes((int)std::max<size_t>(N, 1))))
+        return fail(c, IMLS_ERR_DEVICE, "hipMalloc (DRPM)");
     SolveLaunch L = solve_launch(c, nullptr, 0);
     L.N = (int)N;
     L.blocks1 = 0;
@@ -765,6 +904,7 @@ int imls_register_frame_async(imls_ctx* c) {
     }
     hipMemcpyAsync(c->h_misc, c->st.pose, 16 * 8, hipMemcpyDeviceToHost, c->stream);
     hipMemcpyAsync(c->h_misc + 16, c->st.iters, 16, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(c->h_misc + 18, c->st.status, 4, hipMemcpyDeviceToHost, c->stream);
     if (iters > 0)
         hipMemcpyAsync(c->h_trace, tr, (size_t)iters * sizeof(imls_iter_trace), hipMemcpyDeviceToHost, c->stream);
     if (hipGetLastError() != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "launch failed");
@@ -781,10 +921,8 @@ int imls_register_frame_result(imls_ctx* c, double pose_out[16], int* iters_run,
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return fail(c, IMLS_ERR_DEVICE, std::string("frame failed: ") + hipGetErrorString(e));
     harvest_timing(c);
-    const int* misc = (const int*)(c->h_misc + 16);
-    // misc[0] = iters, misc[?]: status lives in its own 16-B slot; fetch synchronously
-    int st = 0;
-    if (hipMemcpy(&st, c->st.status, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "status copy");
+    const int* misc = (const int*)(c->h_misc + 16);     // iters (pinned, copied by register_frame_async)
+    const int st = *(const int*)(c->h_misc + 18);       // status
     if (pose_out) std::memcpy(pose_out, c->h_misc, 16 * 8);
     if (iters_run) *iters_run = misc[0];
     if (status) *status = st;

@@ -304,21 +304,20 @@ int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int buck
 }
 
 int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, DevBuf& snr, DevBuf& scratch,
-                DevBuf& qperm, int* N_out, std::vector<uint32_t>* kept, std::string& err) {
+                DevBuf& qperm, int* N_out, DevBuf& keptbuf, uint32_t* kept, std::string& err) {
     if (n_in == 0 || n_in > (size_t)0x7fffffff) { err = "source size out of range"; return IMLS_ERR_ARG; }
-    DevBuf keptbuf;
     unsigned* dk = nullptr;
-    if (kept) {
-        if (hipMalloc(&keptbuf.p, n_in * 4) != hipSuccess) { err = "hipMalloc failed"; return IMLS_ERR_DEVICE; }
+    if (kept) {   // the context's persistent kept-index buffer (no allocation per call)
+        if (!ensure(keptbuf, n_in * 4, err)) return IMLS_ERR_DEVICE;
         dk = (unsigned*)keptbuf.p;
     }
     int N = 0;
     int rc = filter_compact(s, d_soa6, n_in, spt, snr, scratch, &N, dk, err);
-    if (!rc && kept) {
-        kept->resize(N);
-        if (N) hipMemcpy(kept->data(), dk, (size_t)N * 4, hipMemcpyDeviceToHost);
+    if (!rc && kept && N > 0 &&
+        (hipMemcpyAsync(kept, dk, (size_t)N * 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)) {
+        err = "kept index download failed";
+        return IMLS_ERR_DEVICE;
     }
-    if (keptbuf.p) (void)hipFree(keptbuf.p);
     *N_out = N;
     if (!rc && N > 0) rc = morton_perm(s, (const float4*)spt.p, N, scratch, qperm, err);
     return rc;

@@ -130,7 +130,7 @@ int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int buck
                        std::string& err, unsigned* kept = nullptr);
 // also computes qperm: the source in Morton order (query order of the wave kernel)
 int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, DevBuf& snr,
-                DevBuf& scratch, DevBuf& qperm, int* N_out, std::vector<uint32_t>* kept, std::string& err);
+                DevBuf& scratch, DevBuf& qperm, int* N_out, DevBuf& keptbuf, uint32_t* kept, std::string& err);
 
 // project.hip
 // k_knn_wave → k_finish (+ the exact k_project_lane fallback for uncertified queries); lane_mode

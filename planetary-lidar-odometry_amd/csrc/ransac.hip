@@ -191,6 +191,11 @@ struct RansacDev {
     int* active;       // [1] the frame was still running when this solve began
 };
 
+// stand-alone DRPM with no rows fails like the oracle's solve_drpm (N == 0 → false)
+__global__ void k_drpm_guard(const int* __restrict__ c, SolveState st) {
+    if (threadIdx.x == 0 && *c == 0) { *st.status = IMLS_FRAME_SOLVE_FAILED; *st.done = 1; }
+}
+
 __global__ void k_set_count(int* __restrict__ c, int v) {
     if (threadIdx.x == 0) *c = v;
 }
@@ -711,6 +716,29 @@ size_t ransac_bytes(int cap) {
 void launch_solve(hipStream_t s, const SolveLaunch& L) {
     const KParams& kp = L.kp;
     SolveState st = L.st;
+    if (kp.solve_method == IMLS_SOLVE_DRPM) {
+        // stand-alone SolveMotionEstimationProblemDRPM (solver.cpp:499-603) on host fp64 rows + weights
+        const int cap = std::max(L.N, 1);
+        const int b1 = solve_blocks(cap);
+        char* p = (char*)L.scratch;
+        auto carve = [&](size_t bytes) { char* r = p; p += (bytes + 255) / 256 * 256; return r; };
+        int* cnt = (int*)carve(64);
+        DrpmDev Dv;
+        Dv.H = (double*)carve(36 * 8);
+        Dv.g = (double*)carve(6 * 8);
+        Dv.U = (double*)carve(36 * 8);
+        Dv.ev = (double*)carve(6 * 8);
+        Dv.slabs = (double*)carve((size_t)(b1 + 1) * kDrpmSlab * 8);
+        const size_t c = (size_t)L.N;
+        k_set_count<<<1, 64, 0, s>>>(cnt, L.N);
+        k_drpm_guard<<<1, 64, 0, s>>>(cnt, L.st);
+        Rows rows{nullptr, nullptr, nullptr, L.rows_d, L.rows_d + 3 * c, L.rows_d + 6 * c, L.weights, 1, cnt, nullptr};
+        launch_rows_pass1(s, rows, cap, L.st.partial1, b1);
+        k_drpm_eig<<<1, 256, 0, s>>>(L.st.partial1, b1, L.st, Dv);
+        k_drpm_noise<<<b1, kBlock, 0, s>>>(rows, cap, L.st, Dv, L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals);
+        k_drpm_final<<<1, 256, 0, s>>>(b1, L.st, Dv, L.tr, kp, L.ransac.drpm_threshold, cnt, cnt, L.update_pose);
+        return;
+    }
     if (kp.solve_method != IMLS_SOLVE_RANSAC) {
         launch_solve_chain(s, L.N, L.blocks1, kp, L.cs, L.cd, L.cn, L.rows_d, L.weights, st, L.tr, L.update_pose,
                            L.rows_are_double, L.count);

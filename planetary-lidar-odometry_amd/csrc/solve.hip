@@ -470,6 +470,10 @@ __global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, c
     const long long lo = (long long)(kp.ls_threshold * (double)n);
     long long hi = (long long)((1 - kp.ls_threshold) * (double)n);
     if (hi > n - 1) hi = n - 1;       // Q11
+    if (n == 0 || lo > hi) {          // no valid row (stand-alone solve, or correspond_number <= 0): as the oracle
+        if (t == 0) { *st.status = IMLS_FRAME_SOLVE_FAILED; *st.done = 1; }
+        return;                       // n, lo, hi are block-uniform: every thread leaves here
+    }
     // exact ranks at the two trim boundaries: a 4096-bin LDS histogram of the float image of |r|
     // (monotone) locates the boundary bins; only their rows are sorted by (|r| bits, row)
     for (int b = t; b < kSmallBins; b += kSmallBlock) hist[b] = 0u;

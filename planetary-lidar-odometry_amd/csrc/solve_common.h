@@ -300,6 +300,11 @@ __device__ void solve_first_block(const double* __restrict__ partial, int blocks
     long long lo = (long long)(kp.ls_threshold * (double)N);
     long long hi = (long long)((1 - kp.ls_threshold) * (double)N);
     if (hi > N - 1) hi = N - 1;       // Q11
+    if (N == 0 || lo > hi) {          // no valid row: solve fails (the oracle's solve_ls returns false)
+        *st.status = IMLS_FRAME_SOLVE_FAILED;
+        *st.done = 1;
+        return;
+    }
     st.sel[4] = (int)lo;
     st.sel[5] = (int)hi;
     st.sel[6] = (int)N;

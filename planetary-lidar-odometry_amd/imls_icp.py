@@ -53,11 +53,6 @@ class ImlsContext:
     def __init__(self, params: Optional[_abi.ImlsParams] = None, device: int = 0):
         self.lib = _abi.load_library()
         self.params = params if params is not None else _config.params_from_config(_config.load())
-        if self.params.solve_method == _abi.IMLS_SOLVE_RANSAC:
-            # the shipped config's solver; the fused GPU loop needs an LS-family method here
-            p = _abi.ImlsParams.from_buffer_copy(self.params)
-            p.solve_method = _abi.IMLS_SOLVE_LS
-            self.params = p
         self.ctx = self.lib.imls_create(device, C.byref(self.params))
         if not self.ctx:
             raise _abi.ImlsError(_abi.IMLS_ERR_DEVICE, f"imls_create(device={device}) failed: no MI355X visible "
@@ -137,6 +132,50 @@ class ImlsContext:
         self._check(self.lib.imls_set_source_device(self.ctx, C.c_void_p(soa6_ptr), n, C.byref(k)))
         self.n_source = k.value
         return k.value
+
+    # -- map FIFO (accumulateTargetCloud, laser_odometry.cpp:116-136) ---------------------------
+    def map_push(self, cloud) -> int:
+        """accumulateTargetCloud(cloud, max_queue_size) + setTargetPointCloud(accumulatedTargetCloud):
+        the scan joins the device-resident FIFO (only it crosses PCIe) and the index is rebuilt over
+        the FIFO's scans, oldest first.  Returns the map size after the NaN filter."""
+        a = _as_xyzn(cloud)
+        n = C.c_size_t()
+        if a.shape[0] == 0:
+            self._check(self.lib.imls_map_push(self.ctx, None, None, 0, 6, C.byref(n)))
+        else:
+            self._check(self.lib.imls_map_push(self.ctx, _ptr(a), C.c_void_p(a.ctypes.data + 12), a.shape[0], 6,
+                                               C.byref(n)))
+        self.n_target = n.value
+        return n.value
+
+    def map_push_device(self, soa6_ptr: int, n: int) -> int:
+        k = C.c_size_t()
+        self._check(self.lib.imls_map_push_device(self.ctx, C.c_void_p(soa6_ptr), n, C.byref(k)))
+        self.n_target = k.value
+        return k.value
+
+    def map_clear(self):
+        self._check(self.lib.imls_map_clear(self.ctx))
+
+    def map_size(self):
+        e, p = C.c_size_t(), C.c_size_t()
+        self._check(self.lib.imls_map_size(self.ctx, C.byref(e), C.byref(p)))
+        return e.value, p.value
+
+    # -- RANSAC rand() stream ---------------------------------------------------------------------
+    def seed_rng(self, seed: int):
+        self._check(self.lib.imls_seed_rng(self.ctx, int(seed)))
+
+    def rng_state(self) -> np.ndarray:
+        st = np.zeros(34, np.int32)
+        self._check(self.lib.imls_get_rng_state(self.ctx, _ptr(st)))
+        return st
+
+    def set_rng_state(self, state):
+        st = np.ascontiguousarray(state, dtype=np.int32)
+        if st.shape != (34,):
+            raise ValueError("rand() state is int32[34]")
+        self._check(self.lib.imls_set_rng_state(self.ctx, _ptr(st)))
 
     # -- matching / solving -------------------------------------------------------------------
     def project(self, pose=None):
@@ -380,11 +419,11 @@ _SOLVER_CTX: Optional[ImlsContext] = None
 
 
 def _solver_ctx() -> ImlsContext:
+    """The free-function solvers' context (one per process, like the reference's free functions).
+    Its RANSAC rand() stream runs on across every call, as the reference's process-wide rand()."""
     global _SOLVER_CTX
     if _SOLVER_CTX is None:
-        p = _config.params_from_config(_config.load())
-        p.solve_method = _abi.IMLS_SOLVE_LS
-        _SOLVER_CTX = ImlsContext(p)
+        _SOLVER_CTX = ImlsContext(_config.params_from_config(_config.load()))
     return _SOLVER_CTX
 
 
@@ -393,7 +432,6 @@ def SolveMotionEstimationProblemLS(source_cloud, ref_cloud, ref_normals, timesta
     ctx = _solver_ctx()
     p = _abi.ImlsParams.from_buffer_copy(ctx.params)
     p.ls_threshold = float(threshold)
-    p.solve_method = _abi.IMLS_SOLVE_LS
     ctx.set_params(p)
     return ctx.solve_correspondences(_abi.IMLS_SOLVE_LS, _triples(source_cloud), _triples(ref_cloud), _triples(ref_normals))
 
@@ -404,77 +442,160 @@ def SolveMotionEstimationProblemWeightedLS(source_cloud, ref_cloud, ref_normals,
                                                _triples(ref_normals), np.asarray(weights, dtype=np.float64))
 
 
+def SolveMotionEstimationProblemRANSAC(source_cloud, ref_cloud, ref_normals, timestamp: str = "",
+                                       max_iterations: int = 5000, distance_threshold: float = 0.8,
+                                       min_inliers_percentage: float = 0.95, huber_threshold: float = 0.648,
+                                       final_solve_method: str = "DRPM", ls_threshold: float = 0.02,
+                                       drpm_threshold: float = 0.05, drpm_stdev_points: float = 0.02,
+                                       drpm_stdev_normals: float = 0.05):
+    """solver.cpp:222-385 (+ the LS / Weighted LS / DRPM finals, 368-384, 486-603) → (flag, deltaTrans).
+    An unknown final_solve_method returns False like solver.cpp:380-384."""
+    if final_solve_method not in _config.FINAL:
+        return False, np.eye(4)
+    ctx = _solver_ctx()
+    p = _abi.ImlsParams.from_buffer_copy(ctx.params)
+    p.ransac_max_iterations = int(max_iterations)
+    p.ransac_distance_threshold = float(distance_threshold)
+    p.ransac_min_inliers_percentage = float(min_inliers_percentage)
+    p.ransac_huber_threshold = float(huber_threshold)
+    p.ransac_final_method = _config.FINAL[final_solve_method]
+    p.ransac_ls_threshold = float(ls_threshold)
+    p.drpm_threshold = float(drpm_threshold)
+    p.drpm_stdev_points = float(drpm_stdev_points)
+    p.drpm_stdev_normals = float(drpm_stdev_normals)
+    ctx.set_params(p)
+    return ctx.solve_correspondences(_abi.IMLS_SOLVE_RANSAC, _triples(source_cloud), _triples(ref_cloud),
+                                     _triples(ref_normals))
+
+
+def SolveMotionEstimationProblemDRPM(source_cloud, ref_cloud, ref_normals, weights, timestamp: str = "",
+                                     threshold: float = 0.05, stdev_points: float = 0.02, stdev_normals: float = 0.05):
+    """solver.cpp:499-603 (degeneracy-aware solve with DRPM probabilities) → (flag, deltaTrans)."""
+    ctx = _solver_ctx()
+    p = _abi.ImlsParams.from_buffer_copy(ctx.params)
+    p.drpm_threshold, p.drpm_stdev_points, p.drpm_stdev_normals = float(threshold), float(stdev_points), float(stdev_normals)
+    ctx.set_params(p)
+    return ctx.solve_correspondences(_abi.IMLS_SOLVE_DRPM, _triples(source_cloud), _triples(ref_cloud),
+                                     _triples(ref_normals), np.asarray(weights, dtype=np.float64))
+
+
 def solveMotionEstimationProblem(solve_method: str, in_cloud_vec, ref_cloud_vec, ref_normal, timestamp: str = "",
                                  cfg: Optional[dict] = None):
-    """laser_odometry.cpp:173-275: string dispatch with parameters read from the config."""
+    """laser_odometry.cpp:173-275: string dispatch with parameters read from the config each call."""
     cfg = cfg if cfg is not None else _config.load()
     sm = cfg["laser_odometry"]["solve_method"]
     if solve_method == "LS":
         return SolveMotionEstimationProblemLS(in_cloud_vec, ref_cloud_vec, ref_normal, timestamp, float(sm["LS"]["threshold"]))
-    if solve_method in _config.UNSUPPORTED_SOLVERS or solve_method == "RANSAC":
+    if solve_method == "RANSAC":
+        rs = sm["RANSAC"]
+        return SolveMotionEstimationProblemRANSAC(
+            in_cloud_vec, ref_cloud_vec, ref_normal, timestamp, int(rs["max_iterations"]),
+            float(rs["distance_threshold"]), float(rs["min_inliers_percentage"]), float(rs["huber_threshold"]),
+            str(rs["final_solve_method"]), float(rs["LS_threshold"]), float(rs["DRPM_threshold"]),
+            float(rs["DRPM_stdev_points"]), float(rs["DRPM_stdev_normals"]))
+    if solve_method in _config.UNSUPPORTED_SOLVERS:
         raise _abi.ImlsError(_abi.IMLS_ERR_UNSUPPORTED, f"solve_method {solve_method!r} is not on the GPU path")
-    # the reference prints "Invalid SOLVE_METHOD!" and returns false
+    # the reference prints "Invalid SOLVE_METHOD!" and returns false (laser_odometry.cpp:269-272)
     return False, np.eye(4)
 
 
 # ================================================================================================
-# Per-frame driver (laser_odometry.cpp:416-683 without ROS / file I/O)
+# Per-frame driver (laser_odometry.cpp:416-683 without ROS)
 # ================================================================================================
-class LaserOdometry:
-    """Streams (filtered cloud, flat cloud) frames like processData: the first frame only seeds
-    the map (Q13); every later frame registers its flat cloud against the FIFO map of the last
-    `max_queue_size` filtered clouds (untransformed, oldest first — accumulateTargetCloud), and
-    chains nowPose = prevLaserPose · rPose."""
+def chain_pose(prev, rel) -> np.ndarray:
+    """nowPose = prevLaserPose * rPose (laser_odometry.cpp:652) in Eigen's 4×4 product order
+    (res(i,j) = ((a(i,0)b(0,j) + a(i,1)b(1,j)) + a(i,2)b(2,j)) + a(i,3)b(3,j)): identical doubles
+    on every host, unlike a BLAS matmul."""
+    a = np.asarray(prev, dtype=np.float64).reshape(4, 4).tolist()
+    b = np.asarray(rel, dtype=np.float64).reshape(4, 4).tolist()
+    return np.array([[((a[i][0] * b[0][j] + a[i][1] * b[1][j]) + a[i][2] * b[2][j]) + a[i][3] * b[3][j]
+                      for j in range(4)] for i in range(4)])
 
-    def __init__(self, params: Optional[_abi.ImlsParams] = None, device: int = 0):
+
+class LaserOdometry:
+    """processData (laser_odometry.cpp:416-683) minus ROS: per (filteredLaserCloud, flatCloud)
+    frame, the first frame only seeds the map (Q13); every later frame registers its flat cloud
+    against the map FIFO (rPose = I, the fused device loop), chains nowPose = prevLaserPose·rPose
+    and appends it to `pose_file` (savePoseToFile, 659); then the filtered cloud joins the FIFO
+    (accumulateTargetCloud, 663-664).  The FIFO lives in HBM (ImlsContext.map_push): only the new
+    scan crosses PCIe each frame.  The context (and its RANSAC rand() stream) persists across frames."""
+
+    def __init__(self, params: Optional[_abi.ImlsParams] = None, device: int = 0, pose_file: Optional[str] = None):
         self.ctx = ImlsContext(params, device)
-        self.queue: deque = deque()
         self.prev_pose = np.eye(4)
         self.frame_count = 0
-        self.poses: list = []           # (timestamp, 4×4) per registered frame
+        self.pose_file = pose_file
+        self.poses: list = []           # (timestamp, nowPose 4×4) per registered frame
+        self.results: list = []         # (timestamp, rPose, iterations, status) per registered frame
+
+    def close(self):
+        self.ctx.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
     def process(self, filtered_cloud, flat_cloud, timestamp: str = ""):
         result = None
         if self.frame_count != 0:
-            target = np.concatenate(list(self.queue)) if len(self.queue) > 1 else self.queue[0]
-            self.ctx.set_target(target)
-            self.ctx.set_source(flat_cloud)
-            result = self.ctx.register_frame()
-            now = self.prev_pose @ result["pose"]
+            n_flat = len(flat_cloud)
+            if n_flat == 0 or self.ctx.n_target == 0:
+                # in_cloud / the map is empty: the first iteration's gate breaks with rPose = I (570-576)
+                result = dict(pose=np.eye(4), iters=0, status=_abi.IMLS_FRAME_TOO_FEW, trace=[])
+            else:
+                self.ctx.set_source(flat_cloud)
+                result = self.ctx.register_frame()
+            now = chain_pose(self.prev_pose, result["pose"])
             self.prev_pose = now
             self.poses.append((timestamp, now))
-        self.queue.append(filtered_cloud)
-        while len(self.queue) > max(1, self.ctx.params.max_queue_size):
-            self.queue.popleft()
+            self.results.append((timestamp, result["pose"], result["iters"], result["status"]))
+            if self.pose_file:
+                savePoseToFile(now, self.pose_file, timestamp)
+        self.ctx.map_push(filtered_cloud)
         self.frame_count += 1
         return result
 
 
-def _quat_xyzw(R: np.ndarray):
-    """Rotation matrix → (x, y, z, w) as Eigen::Quaterniond(Matrix3d) (Shepperd's method)."""
-    t = np.trace(R)
-    if t > 0:
-        s = math.sqrt(t + 1.0) * 2
-        w, x, y, z = 0.25 * s, (R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s
+def _quat_xyzw(R) -> tuple:
+    """Eigen::Quaterniond(Matrix3d) (Eigen's quaternionbase_assign_impl for a 3×3): the trace branch,
+    else the largest-diagonal branch chosen with strict '>'."""
+    m = np.asarray(R, dtype=np.float64).tolist()
+    t = (m[0][0] + m[1][1]) + m[2][2]
+    q = [0.0, 0.0, 0.0]
+    if t > 0.0:
+        t = math.sqrt(t + 1.0)
+        w = 0.5 * t
+        t = 0.5 / t
+        q = [(m[2][1] - m[1][2]) * t, (m[0][2] - m[2][0]) * t, (m[1][0] - m[0][1]) * t]
     else:
-        i = int(np.argmax(np.diag(R)))
+        i = 0
+        if m[1][1] > m[0][0]:
+            i = 1
+        if m[2][2] > m[i][i]:
+            i = 2
         j, k = (i + 1) % 3, (i + 2) % 3
-        s = math.sqrt(R[i, i] - R[j, j] - R[k, k] + 1.0) * 2
-        q = [0.0, 0.0, 0.0]
-        q[i] = 0.25 * s
-        q[j] = (R[j, i] + R[i, j]) / s
-        q[k] = (R[k, i] + R[i, k]) / s
-        w = (R[k, j] - R[j, k]) / s
-        x, y, z = q
-    return x, y, z, w
+        t = math.sqrt(((m[i][i] - m[j][j]) - m[k][k]) + 1.0)
+        q[i] = 0.5 * t
+        t = 0.5 / t
+        w = (m[k][j] - m[j][k]) * t
+        q[j] = (m[j][i] + m[i][j]) * t
+        q[k] = (m[k][i] + m[i][k]) * t
+    return q[0], q[1], q[2], w
+
+
+def format_pose_line(pose, timestamp: str) -> str:
+    """One savePoseToFile line: `ts tx ty tz qx qy qz qw`, std::fixed, 6 decimals."""
+    P = np.asarray(pose, dtype=np.float64)
+    x, y, z, w = _quat_xyzw(P[:3, :3])
+    return f"{timestamp} {P[0, 3]:.6f} {P[1, 3]:.6f} {P[2, 3]:.6f} {x:.6f} {y:.6f} {z:.6f} {w:.6f}\n"
 
 
 def savePoseToFile(pose, filename: str, timestamp: str):
     """saver.cpp:46-54: append `ts tx ty tz qx qy qz qw`, fixed, 6 decimals."""
-    P = np.asarray(pose, dtype=np.float64)
-    x, y, z, w = _quat_xyzw(P[:3, :3])
     with open(filename, "a") as f:
-        f.write(f"{timestamp} {P[0, 3]:.6f} {P[1, 3]:.6f} {P[2, 3]:.6f} {x:.6f} {y:.6f} {z:.6f} {w:.6f}\n")
+        f.write(format_pose_line(pose, timestamp))
 
 
 def saveMatchedPointsToFile(source_cloud, matched_cloud, filename: str):
@@ -482,4 +603,9 @@ def saveMatchedPointsToFile(source_cloud, matched_cloud, filename: str):
     s, d = _triples(source_cloud), _triples(matched_cloud)
     with open(filename, "a") as f:
         for a, b in zip(s, d):
-            f.write(" ".join(f"{v:.6g}" for v in (*a, *b)) + "\n")
+            f.write(" ".join(_g6(v) for v in (*a, *b)) + "\n")
+
+
+def _g6(v: float) -> str:
+    """std::ostream's default float format (%g with precision 6; 'inf'/'nan' as glibc prints them)."""
+    return "%g" % v

@@ -88,28 +88,50 @@ def test_producer_struct_layouts_and_defaults(tmp_path, ctype, cname):
 
 def test_cpp_adapter_header_compiles(tmp_path):
     """include/imls_icp_hip.hpp (the reference-shaped C++ adapter) compiles against a PCL-shaped
-    mock cloud with g++ alone."""
+    mock cloud with g++ alone, with the solver calls spelled exactly as laser_odometry.cpp:183-229
+    spells them (solver.h:84-139 argument lists: no extra context argument)."""
     src = tmp_path / "adapter.cpp"
     src.write_text(f'''
+#include <array>
 #include <memory>
 #include <vector>
 #include "{ROOT / "include" / "imls_icp_hip.hpp"}"
 struct Pt {{ float x, y, z, _p0, normal_x, normal_y, normal_z, _p1, intensity, curvature, _p2, _p3; }};
 struct Cloud {{ std::vector<Pt> points; size_t size() const {{ return points.size(); }}
   void push_back(const Pt& p) {{ points.push_back(p); }} void clear() {{ points.clear(); }} }};
+struct Mat4 {{ double m[16]; double& operator()(int r, int c) {{ return m[r * 4 + c]; }} }};
+using namespace imls_hip;
 int main() {{
-  imls_params p; imls_hip::IMLSICPMatcherHip m(0, nullptr);
+  IMLSICPMatcherHip m;                       // was: IMLSICPMatcher matcher;
   auto a = std::make_shared<Cloud>(); auto b = std::make_shared<Cloud>();
   m.setSourcePointCloud(a); m.setTargetPointCloud(a);
-  m.ProjSourcePtToSurface(a, b, std::string("0"), 0, nullptr);
-  std::vector<std::array<double,3>> s, d, n; double D[16];
-  bool ok = imls_hip::SolveMotionEstimationProblemLS(m, s, d, n, D, "0", 0.02);
+  m.setParameters(30, 1.0, 3.0, 1.0, 0.8, false, true, false, 50, 0.2, 0.6, 10, 20, true, 30.0, "out/");
+  m.ProjSourcePtToSurface(a, b, std::string("0"), 0);
+  std::vector<std::array<double,3>> s, d, n; Mat4 D; std::vector<double> w; std::string ts = "0";
+  bool ok = SolveMotionEstimationProblemLS(s, d, n, D, ts, 0.02);
+  ok = ok && SolveMotionEstimationProblemWeightedLS(s, d, n, D, w, ts);
+  ok = ok && SolveMotionEstimationProblemRANSAC(s, d, n, D, ts, 5000, 0.8, 0.95, 0.648, "DRPM", 0.02, 0.05, 0.02, 0.05);
+  ok = ok && SolveMotionEstimationProblemDRPM(s, d, n, D, w, ts, 0.05, 0.02, 0.05);
   m.planeICPProj(a, b, 1.5, false, 0.8, true, 30.0);
-  ok = ok && imls_hip::SolveMotionEstimationProblemRANSAC(m, s, d, n, D, "0", 5000, 0.8, 0.95, 0.648, "DRPM",
-                                                        0.02, 0.05, 0.02, 0.05);
-  (void)ok; (void)p; return 0; }}
+  double P[16]; m.registerFrame(P);
+  (void)ok; return 0; }}
 ''')
-    subprocess.run(["g++", "-std=c++17", "-fsyntax-only", str(src)], check=True)
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-fsyntax-only", f"-I{ROOT / 'include'}", str(src)],
+                   check=True)
+
+
+def test_type_swap_program_links_against_the_library():
+    """tests/cpp/type_swap (the reference loop over the adapter) is built by build() and links
+    libimls_gpu.so; without a GPU it must fail loudly (no CPU fallback), not compute."""
+    exe = ROOT / "tests" / "cpp" / "type_swap"
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(exe.parent)], check=True)
+    out = subprocess.run(["ldd", str(exe)], capture_output=True, text=True, check=True).stdout
+    assert "libimls_gpu.so" in out and "not found" not in out
+    import torch
+    if not torch.cuda.is_available():
+        r = subprocess.run([str(exe), "LS", "3", "/nonexistent", "/nonexistent"], capture_output=True, text=True)
+        assert r.returncode != 0
 
 
 def test_product_path_fails_loudly_without_gpu():

@@ -26,7 +26,9 @@ def test_config_method_names():
         c = copy.deepcopy(cfg)
         c["laser_odometry"]["solve_method"]["method"] = name
         assert config.params_from_config(c).solve_method == val
-    for bad in ("Ceres", "ICP", "Teaser", "nope"):
+    # "Weighted LS" is a RANSAC final method only: as a top-level name the reference's dispatcher
+    # prints "Invalid SOLVE_METHOD!" (laser_odometry.cpp:269-272), so the config is rejected
+    for bad in ("Ceres", "ICP", "Teaser", "nope", "Weighted LS"):
         c = copy.deepcopy(cfg)
         c["laser_odometry"]["solve_method"]["method"] = bad
         with pytest.raises(config.ConfigError):
@@ -97,3 +99,25 @@ def test_gather_relative_poses_gloo_world2():
     want = np.array([synth.pose_xyyaw(0.1 * k, 0.0, 0.001 * k) for k in range(n_units)])
     for _, allp in res:
         assert np.array_equal(allp, want)
+
+
+def test_weighted_ls_top_level_rejected_but_final_accepted():
+    cfg = config.load()
+    c = copy.deepcopy(cfg)
+    c["laser_odometry"]["solve_method"]["method"] = "Weighted LS"
+    with pytest.raises(config.ConfigError, match="Invalid SOLVE_METHOD"):
+        config.params_from_config(c)
+    for name, val in config.FINAL.items():
+        c = copy.deepcopy(cfg)
+        c["laser_odometry"]["solve_method"]["RANSAC"]["final_solve_method"] = name
+        assert config.params_from_config(c).ransac_final_method == val
+
+
+def test_chain_pose_is_eigen_order():
+    from planetary_lidar_odometry_amd import imls_icp
+    rng = np.random.default_rng(3)
+    a, b = rng.normal(size=(4, 4)), rng.normal(size=(4, 4))
+    got = imls_icp.chain_pose(a, b)
+    want = np.array([[((a[i, 0] * b[0, j] + a[i, 1] * b[1, j]) + a[i, 2] * b[2, j]) + a[i, 3] * b[3, j]
+                      for j in range(4)] for i in range(4)])
+    assert np.array_equal(got, want)

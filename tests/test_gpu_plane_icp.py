@@ -61,6 +61,7 @@ def test_plane_icp_register_frame(ctx, name, solver):
     g = golden(name)
     p = picp_params(iters=8, solver=solver)
     ctx.set_params(p)
+    ctx.seed_rng(p.ransac_seed)        # a fresh rand() stream, as the oracle frame starts one
     ctx.set_target(soa_to_rows(g["tgt"]))
     ctx.set_source(soa_to_rows(g["src"]))
     r = ctx.register_frame()

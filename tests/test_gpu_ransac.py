@@ -68,6 +68,7 @@ def test_ransac_golden_correspondences(ctx, final):
     s, d, n = (g[k].astype(np.float64) for k in ("x1", "y1", "n1"))
     p = shipped_params(final=final)
     ctx.set_params(p)
+    ctx.seed_rng(p.ransac_seed)        # restart the stream: the oracle call starts a fresh one
     ok, D = ctx.solve_correspondences(_abi.IMLS_SOLVE_RANSAC, s, d, n)
     okr, Dr = oc.solve(_abi.IMLS_SOLVE_RANSAC, s, d, n, p)
     assert ok == okr
@@ -84,6 +85,7 @@ def test_ransac_hypothesis_chunks(ctx, final, pct, iters):
     p.ransac_min_inliers_percentage = pct
     p.ransac_max_iterations = iters
     ctx.set_params(p)
+    ctx.seed_rng(p.ransac_seed)        # restart the stream: the oracle call starts a fresh one
     ok, D = ctx.solve_correspondences(_abi.IMLS_SOLVE_RANSAC, s, d, n)
     okr, Dr = oc.solve(_abi.IMLS_SOLVE_RANSAC, s, d, n, p)
     assert ok == okr
@@ -99,6 +101,7 @@ def test_ransac_seed_changes_result(ctx):
         p.ransac_max_iterations = 8
         p.ransac_seed = seed
         ctx.set_params(p)
+        ctx.seed_rng(p.ransac_seed)
         ok, D = ctx.solve_correspondences(_abi.IMLS_SOLVE_RANSAC, s, d, n)
         okr, Dr = oc.solve(_abi.IMLS_SOLVE_RANSAC, s, d, n, p)
         assert np.abs(D - Dr).max() < POSE_TOL
@@ -117,6 +120,7 @@ def test_drpm_degenerate_plane(ctx):
     d = s + np.array([0.2, 0.1, 0.05])
     p = shipped_params(final="DRPM")
     ctx.set_params(p)
+    ctx.seed_rng(p.ransac_seed)        # restart the stream: the oracle call starts a fresh one
     ok, D = ctx.solve_correspondences(_abi.IMLS_SOLVE_RANSAC, s, d, nrm)
     okr, Dr = oc.solve(_abi.IMLS_SOLVE_RANSAC, s, d, nrm, p)
     assert ok == okr and np.abs(D - Dr).max() < DRPM_TOL
@@ -129,6 +133,7 @@ def test_register_frame_shipped_ransac(ctx, name, final):
     g = golden(name)
     p = shipped_params(iters=8, final=final)
     ctx.set_params(p)
+    ctx.seed_rng(p.ransac_seed)        # restart the stream: the oracle call starts a fresh one
     ctx.set_target(soa_to_rows(g["tgt"]))
     ctx.set_source(soa_to_rows(g["src"]))
     r = ctx.register_frame()
@@ -139,3 +144,72 @@ def test_register_frame_shipped_ransac(ctx, name, final):
     for t, u in zip(r["trace"], want["trace"]):
         assert t.n_valid == u.n_valid
         assert np.abs(np.array(t.delta) - np.array(u.delta)).max() < tol
+
+
+def test_rand_stream_runs_on_across_solves(ctx):
+    """the reference never calls srand, so its second RANSAC call draws where the first
+    stopped.  Two consecutive stand-alone solves on one context equal two oracle solves sharing one
+    carried glibc state; a third after imls_seed_rng equals a fresh oracle solve."""
+    s, d, n = outlier_set(frac=0.35, seed=5)
+    p = shipped_params(final="LS")
+    p.ransac_min_inliers_percentage = 0.99
+    p.ransac_max_iterations = 24
+    ctx.set_params(p)
+    ctx.seed_rng(p.ransac_seed)
+    st = oc.rand_state(p.ransac_seed)
+    got, want = [], []
+    for _ in range(2):
+        got.append(ctx.solve_correspondences(_abi.IMLS_SOLVE_RANSAC, s, d, n)[1])
+        want.append(oc.solve(_abi.IMLS_SOLVE_RANSAC, s, d, n, p, rand_state=st)[1])
+    for a, b in zip(got, want):
+        assert np.abs(a - b).max() < POSE_TOL
+    assert np.abs(got[0] - got[1]).max() > 0            # the second solve drew other hypotheses
+    assert np.array_equal(ctx.rng_state(), st)           # device state == the carried glibc state
+    ctx.seed_rng(p.ransac_seed)
+    D = ctx.solve_correspondences(_abi.IMLS_SOLVE_RANSAC, s, d, n)[1]
+    assert np.abs(D - want[0]).max() < POSE_TOL
+    ctx.set_rng_state(st)                                # hand the stream over
+    assert np.array_equal(ctx.rng_state(), st)
+
+
+def test_rand_stream_runs_on_across_frames(ctx):
+    """Two consecutive fused frames on one context continue one stream, like the oracle with a
+    carried state (the second frame differs from a fresh-stream frame)."""
+    g = golden("vlp16_pair")
+    p = shipped_params(iters=4, final="LS")
+    p.ransac_min_inliers_percentage = 0.999             # no early exit: every frame draws many
+    p.ransac_max_iterations = 40
+    ctx.set_params(p)
+    ctx.seed_rng(p.ransac_seed)
+    ctx.set_target(soa_to_rows(g["tgt"]))
+    ctx.set_source(soa_to_rows(g["src"]))
+    st = oc.rand_state(p.ransac_seed)
+    for _ in range(2):
+        r = ctx.register_frame()
+        want = oc.register_frame(g["src"], g["tgt"], p, rand_state=st)
+        assert r["iters"] == want["iters"] and r["status"] == want["status"]
+        assert np.abs(r["pose"] - want["pose"]).max() < POSE_TOL
+    assert np.array_equal(ctx.rng_state(), st)
+
+
+def test_standalone_drpm_matches_oracle(ctx):
+    """SolveMotionEstimationProblemDRPM (solver.cpp:499-603) on caller rows + weights (RANSAC's
+    final step as a free function), well-conditioned and degenerate-plane inputs, unit weights too."""
+    rng = np.random.default_rng(21)
+    s, d, n = outlier_set(n=2500, frac=0.0, seed=9)
+    w = rng.uniform(0.1, 1.0, len(s))
+    w /= w.sum()
+    p = shipped_params(final="DRPM")
+    ctx.set_params(p)
+    for weights in (w, None):
+        ok, D = ctx.solve_correspondences(_abi.IMLS_SOLVE_DRPM, s, d, n, weights)
+        okr, Dr = oc.solve(_abi.IMLS_SOLVE_DRPM, s, d, n, p, weights=weights)
+        assert ok and okr and np.abs(D - Dr).max() < DRPM_TOL
+    sp = np.column_stack([rng.uniform(-10, 10, 2000), rng.uniform(-10, 10, 2000), rng.normal(0, 0.01, 2000)])
+    nn = np.tile([0.0, 0.0, 1.0], (2000, 1)) + rng.normal(0, 0.02, (2000, 3))
+    nn /= np.linalg.norm(nn, axis=1, keepdims=True)
+    ok, D = ctx.solve_correspondences(_abi.IMLS_SOLVE_DRPM, sp, sp + [0.2, 0.1, 0.05], nn, np.full(2000, 1 / 2000))
+    okr, Dr = oc.solve(_abi.IMLS_SOLVE_DRPM, sp, sp + [0.2, 0.1, 0.05], nn, p, weights=np.full(2000, 1 / 2000))
+    assert ok == okr and np.abs(D - Dr).max() < DRPM_TOL
+    ok, _ = ctx.solve_correspondences(_abi.IMLS_SOLVE_DRPM, s[:0], d[:0], n[:0], w[:0])
+    assert not ok                                       # no rows: false, like the oracle

@@ -395,3 +395,46 @@ def test_threaded_oracle_matches_single_thread():
         oc.set_threads(1)
     assert np.array_equal(a["pose"], b["pose"]) and a["iters"] == b["iters"]
     assert [list(t.reject) for t in a["trace"]] == [list(t.reject) for t in b["trace"]]
+
+
+def _rot(axis, ang):
+    a = np.asarray(axis, float) / np.linalg.norm(axis)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    return np.eye(3) + math.sin(ang) * K + (1 - math.cos(ang)) * K @ K
+
+
+def test_pose_line_and_chain_match_oracle():
+    """savePoseToFile (saver.cpp:46-54) and nowPose = prevLaserPose·rPose (laser_odometry.cpp:652):
+    the Python product path and the oracle print byte-identical lines, including the quaternion
+    branches taken when trace(R) <= 0 (rotations near π about each axis)."""
+    from planetary_lidar_odometry_amd import imls_icp
+    rng = np.random.default_rng(7)
+    poses = [np.eye(4)]
+    for axis in ([1, 0, 0], [0, 1, 0], [0, 0, 1], [1, 1, 0], [0.3, -1, 2]):
+        for ang in (1e-9, 0.3, 2.0, math.pi - 1e-3, math.pi):
+            P = np.eye(4)
+            P[:3, :3] = _rot(axis, ang)
+            P[:3, 3] = rng.normal(scale=50, size=3)
+            poses.append(P)
+    for k, P in enumerate(poses):
+        ts = f"{1317384506.0 + 0.1 * k:f}"
+        assert imls_icp.format_pose_line(P, ts) == oc.format_pose(P, ts), (k, P)
+    prev = np.eye(4)
+    for P in poses:
+        a = imls_icp.chain_pose(prev, P)
+        assert np.array_equal(a, oc.chain_pose(prev, P))
+        prev = a
+
+
+def test_oracle_rand_state_carries_across_frames():
+    """A frame with a carried rand() state continues the stream: two RANSAC frames with one carried
+    state equal (frame 1 fresh, frame 2 from frame 1's final state), and the state advanced."""
+    g = golden("vlp16_pair")
+    p = config.params_from_config(config.load())      # shipped: RANSAC -> DRPM
+    p.iterations = 2
+    st = oc.rand_state(p.ransac_seed)
+    st0 = st.copy()
+    a = oc.register_frame(g["src"], g["tgt"], p, rand_state=st)
+    assert not np.array_equal(st, st0)
+    fresh = oc.register_frame(g["src"], g["tgt"], p)
+    assert np.array_equal(a["pose"], fresh["pose"])   # first frame: the stream starts at the seed either way
