@@ -1,15 +1,29 @@
-"""Benchmark: IMLS-ICP scan-pairs/s on BASELINE config B.
+"""Benchmark: IMLS-ICP scan-pairs/s on BASELINE config B, plus the other configs.
 
-Workload (one "step" = one scan-pair registration, inputs already resident in HBM):
-  synthetic HDL-64 scan (~126k points, all used as queries) vs a 10-scan local map (~1.26M
-  points); index build (NaN filter, Morton sort, tree) + 20 ICP iterations (fixed: delta
-  thresholds −1), each = fused transform/kNN/IMLS projection + trimmed-LS solve + pose update,
-  all on device, one host sync per pair.  LS, t = 0.02; shipped IMLS parameters (h=1, r=3, K=20,
-  30° normal gate).
+Workloads (--workload):
+  B       (default, the headline)  synthetic HDL-64 scan (~126k points, all used as queries) vs a
+          10-scan local map (~1.26M points); one "step" = `--inflight` independent scan pairs in
+          flight, each = index build + 20 ICP iterations (fixed: delta thresholds −1), inputs already
+          resident in HBM, one host sync per pair.  Shipped IMLS parameters (h=1, r=3, K=20, 30°).
+  stream  config C/D-like: `--inflight` independent sequences, each a seeded HDL-64 drive through
+          the GPU producer (ring PCA → geometric-features presample → major_axis sampling, ≤ 2000
+          flat points); a step = one frame per sequence: the previous filtered scan joins the
+          device map FIFO (map_push: only that scan crosses PCIe), the flat cloud is uploaded, and
+          the frame is registered — host buffers in, pose out (PCIe included).
+  A       config A: VLP-16 scan (~13k queries) vs the previous scan, inputs resident in HBM.
+--solver LS (default) or RANSAC_DRPM (the shipped config.json solver: RANSAC → DRPM).
+
+Measurement: the timed region (barrier + synchronize on both sides, max over ranks) carries no
+instrumentation.  A separate probe afterwards registers `--latency-pairs` pairs ONE AT A TIME with
+HIP events around every projection launch (on the stream it runs on): single-pair latency
+(median / p90), single-pair ms per ICP iteration, and the dominant kernel's serialised duration,
+which is what roofline.achieved divides the algorithmic bytes by (and what rocprofv3 --stats of the
+same command reports).  The CPU baseline (rank 0, N = 1) is the oracle — test infrastructure, timed
+here only as the reported baseline.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, each registers its own independent pairs (weak scaling); the only exchange is
-one RCCL all-gather of the relative poses for trajectory chaining; max-over-ranks timing.
+GPU, each registers its own independent pairs (weak scaling); the only exchange is one
+all-gather of the relative poses for trajectory chaining (RCCL; --backend gloo for CPU rehearsal).
 
 Prints ONE JSON line (rank 0).  Progress goes to stderr.
 """
@@ -19,6 +33,7 @@ import argparse
 import json
 import os
 import pathlib
+import platform
 import sys
 import time
 
@@ -33,7 +48,7 @@ os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("IMLS_BENCH_HW_QUEUES", "8")
 import plo_amd  # noqa: E402
 
 plo_amd.load()
-from planetary_lidar_odometry_amd import config, imls_icp, sequences, synth  # noqa: E402
+from planetary_lidar_odometry_amd import _abi, config, imls_icp, sequences, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E nominal (MI355X_MICROARCH.md chip table)
 
@@ -42,6 +57,147 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# ------------------------------------------------------------------------------------------------
+# distributed plumbing (shared with tests/test_bench_dist.py, which runs it on gloo)
+# ------------------------------------------------------------------------------------------------
+def dist_setup(backend: str = "auto"):
+    """(world, rank, local_rank, torch device); initialises the process group when WORLD_SIZE > 1."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "auto":
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    use_cuda = backend == "nccl" or torch.cuda.is_available()
+    if use_cuda:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, local, dev
+
+
+def timed_steps(step, steps: int, world: int, dev, sync=None):
+    """Run `steps` calls of step() between barrier + sync on both sides.  Returns (elapsed = max over
+    ranks, per-step seconds of this rank, the concatenated per-step results)."""
+    import torch.distributed as dist
+    sync = sync or (lambda: None)
+    if world > 1:
+        dist.barrier()
+    sync()
+    per, out = [], []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ts = time.perf_counter()
+        out.extend(step())
+        per.append(time.perf_counter() - ts)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        elapsed = float(tt.item())
+    return elapsed, per, out
+
+
+def exchange_poses(local_poses, world: int):
+    """The one collective: all-gather of every rank's relative poses (unit order = rank-major blocks,
+    sequences.shard_range) and the chained trajectory nowPose_k = prevLaserPose·rPose_k."""
+    local_poses = np.asarray(local_poses, dtype=np.float64).reshape(-1, 4, 4)
+    if world == 1:
+        allp = local_poses
+    else:
+        allp = sequences.gather_relative_poses(local_poses, world * len(local_poses))
+    return allp, sequences.chain_trajectory(allp)
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline (oracle: test infrastructure, used here only as the timed reported baseline)
+# ------------------------------------------------------------------------------------------------
+def host_info() -> dict:
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    return dict(cpu_model=model, os_cpu_count=os.cpu_count(), affinity_cpus=len(allowed),
+                omp_num_threads=os.environ.get("OMP_NUM_THREADS"))
+
+
+class _Pinned:
+    """Pin this process to one CPU for the 1-thread leg (restored on exit)."""
+
+    def __enter__(self):
+        self.prev = os.sched_getaffinity(0)
+        self.cpu = min(self.prev)
+        os.sched_setaffinity(0, {self.cpu})
+        return self
+
+    def __exit__(self, *a):
+        os.sched_setaffinity(0, self.prev)
+
+
+def cpu_baseline(src, tgt, p, label: str, min_seconds: float = 10.0, max_pairs: int = 4, faithful_iters: int = 2):
+    """The oracle on the same pair (same parameters): (1) "efficient" port, 1 thread pinned: whole
+    registrations repeated to >= min_seconds (<= max_pairs); (2) "faithful": the reference's
+    container costs (erase per rejection, AoS copies, per-query heap vectors), 1 thread pinned, on
+    the first `faithful_iters` ICP iterations, extrapolated per pair; (3) all cores: the per-query
+    loop on every CPU this process may use (OpenMP)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_ctypes as oc
+    info = host_info()
+    iters = p.iterations
+    with _Pinned() as pin:
+        total, n, t_idx = 0.0, 0, 0.0
+        while n < max_pairs and (n == 0 or total < min_seconds):
+            r = oc.register_frame(src, tgt, p)
+            total += r["seconds_total"]
+            t_idx += r["seconds_index"]
+            n += 1
+        pf = _abi.ImlsParams.from_buffer_copy(p)
+        pf.iterations = min(faithful_iters, iters)
+        oc.set_faithful(True)
+        try:
+            rf = oc.register_frame(src, tgt, pf)
+        finally:
+            oc.set_faithful(False)
+    t_iter_f = (rf["seconds_total"] - rf["seconds_index"]) / max(rf["iters"], 1)
+    faithful_pair = rf["seconds_index"] + iters * t_iter_f
+    threads = max(1, min(info["affinity_cpus"], int(os.environ.get("OMP_NUM_THREADS") or 10 ** 6)))
+    oc.set_threads(threads)
+    try:
+        r2 = oc.register_frame(src, tgt, p)
+    finally:
+        oc.set_threads(1)
+    return dict(
+        value=n / total, unit="scan-pairs/s", cores=1, kind="port",
+        sample=f"{n} whole registration(s) of the {label} pair ({src.shape[1]} queries vs {tgt.shape[1]}-pt map, "
+               f"{r['iters']} ICP iterations each) in {total:.1f} s, index build {t_idx / n:.2f} s/pair; "
+               f"oracle/imls_oracle.cpp -O3 (efficient port: stable compaction), 1 thread pinned to CPU {pin.cpu}",
+        seconds_per_pair=total / n,
+        faithful={"value": 1.0 / faithful_pair, "cores": 1, "seconds_per_pair": faithful_pair,
+                  "sample": f"index build + {rf['iters']} of {iters} ICP iterations with the reference's container "
+                            f"costs (erase per rejected point, AoS copy per iteration, per-query heap vectors), "
+                            f"{rf['seconds_total']:.1f} s, extrapolated to {iters} iterations"},
+        all_cores={"value": 1.0 / r2["seconds_total"], "cores": threads,
+                   "sample": f"1 whole registration, per-query projection loop OpenMP over {threads} threads "
+                             f"(index build and solver sequential)"},
+        host=info)
+
+
+# ------------------------------------------------------------------------------------------------
+# workloads
+# ------------------------------------------------------------------------------------------------
 def soa_tensor(cloud, dev):
     import torch
     return torch.from_numpy(np.ascontiguousarray(synth.soa(cloud))).to(dev).contiguous()
@@ -54,35 +210,115 @@ def algorithmic_bytes_per_launch(stats: dict, trace, iters: int) -> float:
     return 24.0 * stats["queries"] + 24.0 * stats["nn_found"] / iters + 24.0 * stats["sum_kq"] / iters + 40.0 * n_valid
 
 
-def cpu_baseline(pair, iters_full: int, min_seconds: float = 10.0, max_pairs: int = 4):
-    """The oracle (C++ restatement, -O3, 1 thread) on the same pair: whole registrations (index
-    build + `iters_full` ICP iterations, the same fixed-iteration parameters as the GPU leg),
-    repeated until at least `min_seconds` of CPU work (bounded sample)."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle_ctypes as oc
-    p = config.bench_params(iters_full)
-    src, tgt = synth.soa(pair.source), synth.soa(pair.target)
-    total, n, t_idx = 0.0, 0, 0.0
-    while n < max_pairs and (n == 0 or total < min_seconds):
-        r = oc.register_frame(src, tgt, p)
-        total += r["seconds_total"]
-        t_idx += r["seconds_index"]
-        n += 1
-    # secondary (SURVEY §8(d)): the same oracle with its per-query projection loop on all host cores
-    # this process may use (OpenMP; the index build and the solver stay sequential)
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
-    oc.set_threads(threads)
-    try:
-        r2 = oc.register_frame(src, tgt, p)
-    finally:
-        oc.set_threads(1)
-    return dict(value=n / total, unit="scan-pairs/s", cores=1, kind="port",
-                sample=f"{n} whole pair registration(s) ({pair.source.size} queries vs {pair.target.size}-pt map, "
-                       f"{r['iters']} ICP iterations each) in {total:.1f} s, index build {t_idx / n:.2f} s/pair; "
-                       f"oracle/imls_oracle.cpp -O3, 1 thread",
-                seconds_per_pair=total / n,
-                all_cores={"value": 1.0 / r2["seconds_total"], "cores": threads,
-                           "sample": f"1 whole pair registration, projection loop OpenMP over {threads} threads"})
+def solver_params(solver: str, iters: int) -> _abi.ImlsParams:
+    p = config.bench_params(iters)                      # LS, fixed iteration count
+    if solver == "RANSAC_DRPM":
+        shipped = config.params_from_config(config.load())
+        p.solve_method = shipped.solve_method           # RANSAC
+        p.ransac_final_method = shipped.ransac_final_method   # DRPM
+    return p
+
+
+class PairRunner:
+    """Configs A / B: independent pairs, inputs resident in HBM, one context (= stream) per pair."""
+
+    def __init__(self, pairs, p, dev, local):
+        self.pairs = pairs
+        self.s_dev = [soa_tensor(q.source, dev) for q in pairs]
+        self.t_dev = [soa_tensor(q.target, dev) for q in pairs]
+        self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in pairs]
+
+    def step(self, ctxs=None, idx=None):
+        ctxs = ctxs or self.ctxs
+        idx = idx if idx is not None else range(len(self.pairs))
+        for c, k in zip(ctxs, idx):
+            q = self.pairs[k]
+            c.set_target_device(self.t_dev[k].data_ptr(), q.target.size)
+            c.set_source_device(self.s_dev[k].data_ptr(), q.source.size)
+            c.register_frame_async()
+        return [c.register_frame_result() for c in ctxs]
+
+    def close(self):
+        for c in self.ctxs:
+            c.close()
+
+
+class StreamRunner:
+    """Config C/D-like: `n_seq` independent sequences (one context each); each step processes one
+    frame per sequence exactly as LaserOdometry.process does (map_push of the previous filtered
+    scan, set_source of the flat cloud, register), host buffers in.  A sequence ping-pongs over its
+    F produced frames (0 … F−1 … 0 …) so every step registers two adjacent frames."""
+
+    def __init__(self, n_seq, p, local, rank, frames_per_seq=5):
+        from planetary_lidar_odometry_amd import producer
+        sm = synth.hdl64()
+        self.seqs = []
+        with imls_icp.ImlsContext(device=local) as pctx:
+            for q in range(n_seq):
+                scene = synth.make_scene(17 * rank + q)
+                poses = synth.trajectory(frames_per_seq + 3, 2000 + 31 * rank + q)
+                sr = producer.ScanRegistration(ctx=pctx, shuffle_seed=q, rand_seed=1 + q)
+                frames = []
+                for k in range(frames_per_seq):
+                    sw = synth.scan(scene, sm, poses[3 + k], seed=5000 + 100 * q + k)
+                    xyz, sizes, inten = producer.sweep_inputs(sw, len(sm.rings))
+                    frames.append(sr.process(xyz, sizes, inten))
+                self.seqs.append(frames)
+        self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in range(n_seq)]
+        self.pos = [0] * n_seq
+        self.dir = [1] * n_seq
+        # frame 0 only seeds the map (Q13); afterwards each registered frame's filtered scan joins
+        # the FIFO at the start of that sequence's next step, as LaserOdometry.process orders it
+        self.pending = [fr[0][0] for fr in self.seqs]
+
+    def _advance(self, q):
+        F = len(self.seqs[q])
+        nxt = self.pos[q] + self.dir[q]
+        if nxt < 0 or nxt >= F:
+            self.dir[q] = -self.dir[q]
+            nxt = self.pos[q] + self.dir[q]
+        return nxt
+
+    def step(self):
+        for q, c in enumerate(self.ctxs):
+            c.map_push(self.pending[q])                  # only the new scan crosses PCIe
+            k = self._advance(q)
+            c.set_source(self.seqs[q][k][1])
+            c.register_frame_async()
+            self.pending[q] = self.seqs[q][k][0]
+            self.pos[q] = k
+        return [c.register_frame_result() for c in self.ctxs]
+
+    @property
+    def queries(self):
+        return int(np.mean([len(f[1]) for s in self.seqs for f in s]))
+
+    @property
+    def map_points(self):
+        return int(np.mean([len(f[0]) for s in self.seqs for f in s]))
+
+    def close(self):
+        for c in self.ctxs:
+            c.close()
+
+
+def latency_probe(run_one, ctx, n_pairs: int, iters: int):
+    """Pairs registered one at a time with per-launch HIP events (on the context's stream)."""
+    ctx.enable_timing(True)
+    ctx.reset_timing()
+    lat = []
+    for _ in range(n_pairs):
+        t = time.perf_counter()
+        run_one()
+        lat.append(time.perf_counter() - t)
+    ctx.enable_timing(False)
+    k = {name: ctx.kernel_timing(i) for i, name in enumerate(("projection", "index", "solve", "k_knn_wave", "k_finish"))}
+    lat = np.array(lat) * 1e3
+    idx_ms = k["index"][0] / max(k["index"][1], 1)
+    return dict(pairs=n_pairs, median_ms=float(np.median(lat)), p90_ms=float(np.percentile(lat, 90)),
+                ms_per_iteration=float((np.median(lat) - idx_ms) / iters),
+                kernel_avg_ms={n: v[0] / max(v[1], 1) for n, v in k.items()},
+                launches={n: int(v[1]) for n, v in k.items()})
 
 
 def main():
@@ -91,119 +327,69 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--queries", type=int, default=0, help="0 = all source points; else FPS subsample")
-    ap.add_argument("--inflight", type=int, default=4, help="independent scan pairs in flight (one stream each)")
+    ap.add_argument("--queries", type=int, default=0, help="config B: 0 = all source points; else FPS subsample")
+    ap.add_argument("--inflight", type=int, default=4, help="independent pairs / sequences in flight (a stream each)")
+    ap.add_argument("--latency-pairs", type=int, default=50, help="single-pair latency / roofline probe size")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
+    ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
-    ap.add_argument("--workload", choices=["B", "stream"], default="B",
-                    help="B: config B (the headline); stream: config C-like frames — 2000 FPS queries "
-                         "(config.json major_axis max_total_points) vs the previous scan")
+    ap.add_argument("--workload", choices=["B", "stream", "A"], default="B")
+    ap.add_argument("--solver", choices=["LS", "RANSAC_DRPM"], default="LS")
     args = ap.parse_args()
-    stream = args.workload == "stream"
-    map_scans = 1 if stream else 10
-    if stream and args.queries <= 0:
-        args.queries = 2000
 
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    t0 = time.time()
+    world, rank, local, dev = dist_setup(args.backend)
     P = max(1, args.inflight)
-    pairs = synth.make_pairs(P, "hdl64", map_scans=map_scans, scene_seed=rank, traj_seed=2000 + rank,
-                             noise_seed=1000 + 97 * rank)
-    if args.queries > 0:
-        pairs = [synth.Pair(synth.fps_subsample(q.source, args.queries, seed=rank), q.target, q.true_pose, q.meta)
-                 for q in pairs]
-    log(f"[rank {rank}] {P} pair(s) generated in {time.time() - t0:.1f}s: "
-        f"{[q.source.size for q in pairs]} queries, maps {[q.target.size for q in pairs]}")
-    s_dev = [soa_tensor(q.source, dev) for q in pairs]
-    t_dev = [soa_tensor(q.target, dev) for q in pairs]
+    p = solver_params(args.solver, args.iters)
+    t0 = time.time()
+    if args.workload == "stream":
+        runner = StreamRunner(P, p, local, rank)
+        probe_ctx = runner.ctxs[0]
+        queries, map_points = runner.queries, runner.map_points
+        single = None
+    else:
+        model, map_scans = ("vlp16", 1) if args.workload == "A" else ("hdl64", 10)
+        pairs = synth.make_pairs(P, model, map_scans=map_scans, scene_seed=rank, traj_seed=2000 + rank,
+                                 noise_seed=1000 + 97 * rank)
+        if args.queries > 0:
+            pairs = [synth.Pair(synth.fps_subsample(q.source, args.queries, seed=rank), q.target, q.true_pose, q.meta)
+                     for q in pairs]
+        runner = PairRunner(pairs, p, dev, local)
+        probe_ctx = runner.ctxs[0]
+        queries, map_points = pairs[0].source.size, pairs[0].target.size
+        single = lambda: runner.step([probe_ctx], [0])   # noqa: E731
+    log(f"[rank {rank}] workload {args.workload} set up in {time.time() - t0:.1f}s: {P} in flight, "
+        f"~{queries} queries vs ~{map_points}-pt maps, solver {args.solver}")
     torch.cuda.synchronize()
-
-    p = config.bench_params(args.iters)
-    ctxs = [imls_icp.ImlsContext(p, device=local) for _ in range(P)]   # one context (= stream) per pair in flight
-
-    def step():
-        # P independent pairs in flight: each context's index build + fused 20-iteration loop is
-        # enqueued on its own stream; results are collected after all are enqueued
-        for c, q, sd, td in zip(ctxs, pairs, s_dev, t_dev):
-            c.set_target_device(td.data_ptr(), q.target.size)
-            c.set_source_device(sd.data_ptr(), q.source.size)
-            c.register_frame_async()
-        return [c.register_frame_result() for c in ctxs]
 
     for _ in range(args.warmup):
-        res = step()
-    errs = [np.linalg.norm(r[0][:3, 3] - q.true_pose[:3, 3]) for r, q in zip(res, pairs)]
-    err = float(max(errs))
-    log(f"[rank {rank}] warmup done; max pose error vs truth {err * 100:.2f} cm")
+        res = runner.step()
+    if args.workload != "stream":
+        errs = [np.linalg.norm(r[0][:3, 3] - q.true_pose[:3, 3]) for r, q in zip(res, runner.pairs)]
+        log(f"[rank {rank}] warmup done; max pose error vs truth {max(errs) * 100:.2f} cm")
 
-    for c in ctxs:
-        c.enable_timing(True)
-        c.reset_timing()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    poses = []
-    for _ in range(args.steps):
-        res = step()
-        poses.extend(r[0] for r in res)
-    if world > 1:
-        n_units = world * args.steps * P
-        allp = sequences.gather_relative_poses(np.array(poses), n_units)   # the one RCCL exchange
-        traj = sequences.chain_trajectory(allp)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dist.barrier()
-        elapsed = float(tt.item())
-    for c in ctxs:
-        c.enable_timing(False)
-
-    def tsum(k):
-        ms = sum(c.kernel_timing(k)[0] for c in ctxs)
-        n = sum(c.kernel_timing(k)[1] for c in ctxs)
-        return ms, n
-    proj_ms, proj_n = tsum(0)
-    idx_ms, idx_n = tsum(1)
-    sol_ms, sol_n = tsum(2)
-    knn_ms, knn_n = tsum(3)
-    fin_ms, fin_n = tsum(4)
-    ctx = ctxs[0]
-    stats = ctx.index_stats()
-    trav = ctx.traversal_stats()
-    log(f"[rank {rank}] traversal (last frame of pair 0, {args.iters} iterations): {trav}")
-    # n_valid per iteration of pair 0's last frame for the byte count
-    bytes_launch = algorithmic_bytes_per_launch(stats, ctx.last_trace, args.iters)
-    avg_proj_s = proj_ms / max(proj_n, 1) / 1e3
-    achieved = bytes_launch / avg_proj_s / 1e9 if avg_proj_s > 0 else 0.0
+    elapsed, per_step, res = timed_steps(runner.step, args.steps, world, dev, torch.cuda.synchronize)
+    poses = [r[0] for r in res]
+    allp, traj = exchange_poses(poses, world)          # the one RCCL exchange (trajectory chaining)
     n_pairs = args.steps * P
-    aggregate = bytes_launch * args.iters * n_pairs / elapsed / 1e9
+    value = world * n_pairs / elapsed
+
+    # single-pair latency + serialised per-launch kernel durations (roofline), outside the timed region
+    probe = latency_probe(single, probe_ctx, args.latency_pairs, args.iters) if single else None
+    stats = probe_ctx.index_stats()
+    trav = probe_ctx.traversal_stats()
+    bytes_launch = algorithmic_bytes_per_launch(stats, probe_ctx.last_trace, args.iters)
 
     if rank != 0:
-        for c in ctxs:
-            c.close()
+        runner.close()
         if world > 1:
             dist.destroy_process_group()
         return
 
-    # HBM traffic per projection launch from the committed PMC pass (tools/pmc_traffic.py):
-    # 2·FETCH_SIZE + WRITE_SIZE of k_knn_wave + k_finish (gfx950 FETCH_SIZE counts ½ of wide reads)
     traffic = None
     tj = pathlib.Path(args.traffic_json)
-    if tj.exists():
+    if tj.exists() and args.workload == "B":
         try:
             tdat = json.loads(tj.read_text())
             if tdat.get("queries") == stats["queries"] and tdat.get("iters") == args.iters:
@@ -212,69 +398,80 @@ def main():
             traffic = None
 
     cpu = None
-    if world == 1 and not args.no_cpu:
-        log("[rank 0] CPU baseline (oracle, 1 thread) ...")
-        cpu = cpu_baseline(pairs[0], args.iters)
-        log(f"[rank 0] CPU baseline {cpu['value']:.4f} pairs/s")
+    if world == 1 and not args.no_cpu and args.workload != "stream":
+        log("[rank 0] CPU baseline (oracle) ...")
+        q0 = runner.pairs[0]
+        cpu = cpu_baseline(synth.soa(q0.source), synth.soa(q0.target), p, f"config {args.workload}")
+        log(f"[rank 0] CPU baseline {cpu['value']:.4f} pairs/s (faithful {cpu['faithful']['value']:.4f}, "
+            f"{cpu['all_cores']['cores']} cores {cpu['all_cores']['value']:.3f})")
 
-    value = world * n_pairs / elapsed
-    ms_step = elapsed / args.steps * 1e3
+    roof = None
+    if probe:
+        kd = probe["kernel_avg_ms"]
+        dom_ms = kd["k_knn_wave"] + kd["k_finish"]
+        achieved = bytes_launch / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
+        roof = {
+            "bound": "hbm",
+            "kernel": "projection step = k_knn_wave (packet traversal) + k_finish (exact re-rank, gates, IMLS, "
+                      "pass-1 normal equations); serialised per-launch HIP-event duration, one pair in flight",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_launch,
+            "avg_launch_ms": dom_ms,
+            "kernel_avg_ms": kd,
+            "aggregate_algorithmic_GBps": bytes_launch * args.iters * n_pairs * world / elapsed / 1e9,
+            "aggregate_frac": bytes_launch * args.iters * n_pairs * world / elapsed / 1e9 / HBM_PEAK_GBS,
+        }
+    solver_txt = "LS (trimmed, t=0.02)" if args.solver == "LS" else "RANSAC -> DRPM (shipped config.json solver)"
+    if args.workload == "B":
+        metric = "IMLS-ICP scan-pairs/s (HDL-64 ~120k-pt scan vs 10-scan map, 20 ICP iterations)"
+        workload = f"config B: HDL-64 scan vs 10-scan local map; a step = {P} independent scan pairs in flight"
+        unit = "scan-pairs/s"
+    elif args.workload == "A":
+        metric = "IMLS-ICP scan-pairs/s (config A: VLP-16 scan vs 1-scan map, 20 ICP iterations)"
+        workload = f"config A: VLP-16 scan vs the previous scan; a step = {P} independent pairs in flight"
+        unit = "scan-pairs/s"
+    else:
+        metric = ("IMLS-ICP frames/s (config C/D-like stream: producer-sampled <=2000-pt flat clouds of HDL-64 "
+                  "sweeps vs the device map FIFO, 20 ICP iterations, PCIe of the new scan included)")
+        workload = f"config C/D-like: {P} independent sequences, one frame each per step"
+        unit = "frames/s"
+    per = np.array(per_step) * 1e3
     out = {
-        "metric": ("IMLS-ICP frames/s (config C-like stream: 2000 FPS queries of an HDL-64 scan vs the previous scan, "
-                   "20 ICP iterations)") if stream else
-                  "IMLS-ICP scan-pairs/s (HDL-64 ~120k-pt scan vs 10-scan map, 20 ICP iterations)",
+        "metric": metric,
         "value": value,
-        "unit": "frames/s" if stream else "scan-pairs/s",
+        "unit": unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": ms_step,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step_median": float(np.median(per)),
+        "ms_per_step_p90": float(np.percentile(per, 90)),
         "ms_per_pair": elapsed / n_pairs * 1e3,
         "pairs_in_flight": P,
-        "ms_per_iteration": (elapsed / n_pairs * 1e3 - idx_ms / max(idx_n, 1)) / args.iters,
+        "ms_per_iteration": elapsed / n_pairs * 1e3 / args.iters,
+        "single_pair": probe,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (seeded HDL-64 ray-cast urban scene, planetary-lidar-odometry_amd/synth.py)",
+        "data": "synthetic (seeded HDL-64 / VLP-16 ray-cast urban scene, planetary-lidar-odometry_amd/synth.py)",
         "config": {
-            "workload": (f"config C-like stream: {args.queries} FPS queries vs the previous scan; a step = {P} frames "
-                         f"in flight") if stream else
-                        f"config B: HDL-64 scan vs 10-scan local map; a step = {P} independent scan pairs in flight",
-            "queries": int(stats["queries"]),
-            "map_points": int(stats["points"]),
+            "workload": workload,
+            "queries": int(stats["queries"]) if args.workload != "stream" else queries,
+            "map_points": int(stats["points"]) if args.workload != "stream" else map_points,
             "icp_iterations": args.iters,
-            "solver": "LS (trimmed, t=0.02)",
+            "solver": solver_txt,
             "search_number": p.search_number,
-            "parallelism": f"pairs sharded over {world} GPU(s), RCCL pose all-gather" if world > 1 else "1 GPU",
+            "parallelism": f"independent pairs per GPU over {world} GPU(s), RCCL pose all-gather" if world > 1 else "1 GPU",
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "projection step = k_knn_wave (packet traversal) + k_finish (exact re-rank, gates, IMLS, "
-                      "pass-1 normal equations) + k_project_lane (fallback, normally 0 queries)",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": bytes_launch,
-            "avg_launch_ms": avg_proj_s * 1e3,
-            "launches": int(proj_n),
-            "kernel_avg_ms": {"k_knn_wave": knn_ms / max(knn_n, 1), "k_finish": fin_ms / max(fin_n, 1)},
-            "aggregate_algorithmic_GBps": aggregate,
-        },
-        "breakdown_ms_per_pair": {     # summed per-pair stream time (overlaps across pairs in flight)
-            "index_build": idx_ms / max(n_pairs, 1),
-            "projection": proj_ms / max(n_pairs, 1),
-            "solve_chain": sol_ms / max(n_pairs, 1),
-        },
+        "roofline": roof,
         "traversal_per_launch": {k: v / args.iters for k, v in trav.items()},
+        "trajectory_end": traj[-1][:3, 3].tolist() if len(traj) else None,
         "cpu_baseline": cpu,
-        "final_pose_error_cm": float(err * 100),
     }
     print(json.dumps(out), flush=True)
-    for c in ctxs:
-        c.close()
+    runner.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -9,6 +9,7 @@
 #include "imls_oracle.h"
 
 #include <algorithm>
+#include <array>
 #include <cfloat>
 #include <chrono>
 #include <cmath>
@@ -923,8 +924,72 @@ inline void rotate_normal(const double T[16], float nx, float ny, float nz, floa
 struct Corr { std::vector<float> x, y, n; std::vector<uint32_t> idx; };
 
 int g_threads = 1;   // oracle_set_threads: the secondary (all-cores) CPU baseline, SURVEY §8(d)
+int g_faithful = 0;  // oracle_set_faithful: the reference's own data-structure costs (CPU baseline only)
+
+// The "faithful" CPU baseline: the same arithmetic with the reference's container
+// costs — a full 48-byte AoS copy of the source per iteration (laser_odometry.cpp:527), the
+// erase-based loop over it (imls_icp.cpp:553-734: `in_cloud->erase(it)` moves the tail for every
+// rejected point, O(N) each), heap-allocated kNN index/distance vectors and neighbour lists per
+// query (328-329, 378-379, 602-604), out_cloud push_back, and the getXYZ/getNormals copies
+// (laser_odometry.cpp:595-599).  Results are identical to project_all's.
+struct Pt48 { float x, y, z, p0, nx, ny, nz, p1, in, cu, p2, p3; };
+void project_all_faithful(const Matcher& m, const Cloud& src, const double T[16], bool rot_normals, Corr& c,
+                          uint64_t rej[6]) {
+    for (int k = 0; k < 6; ++k) rej[k] = 0;
+    c.x.clear(); c.y.clear(); c.n.clear(); c.idx.clear();
+    std::vector<Pt48> in_cloud(src.size());
+    std::vector<uint32_t> orig(src.size());
+    for (size_t i = 0; i < src.size(); ++i) {
+        Pt48& q = in_cloud[i];
+        q = Pt48{src.x[i], src.y[i], src.z[i], 0.f, src.nx[i], src.ny[i], src.nz[i], 0.f, 0.f, 0.f, 0.f, 0.f};
+        float x[3];
+        transform_point(T, src.x[i], src.y[i], src.z[i], x);
+        q.x = x[0]; q.y = x[1]; q.z = x[2];
+        if (rot_normals) { float nn[3]; rotate_normal(T, src.nx[i], src.ny[i], src.nz[i], nn); q.nx = nn[0]; q.ny = nn[1]; q.nz = nn[2]; }
+        orig[i] = (uint32_t)i;
+    }
+    std::vector<Pt48> out_cloud;
+    const int K = m.P->search_number;
+    volatile double sink = 0.0;
+    for (size_t i = 0; i < in_cloud.size();) {
+        std::vector<int> nn_idx(1);                                // Eigen::VectorXi indices(1)
+        std::vector<double> nn_d2(1);                              // Eigen::VectorXd dist2(1)
+        std::vector<int> k_idx(K);                                 // VectorXi nearIndices(K)
+        std::vector<double> k_d2(K);                               // VectorXd nearDist2(K)
+        std::vector<std::array<double, 3>> nearPoints, nearNormals;
+        nearPoints.reserve(K);
+        nearNormals.reserve(K);
+        const Pt48& q = in_cloud[i];
+        float x[3] = {q.x, q.y, q.z}, ns[3] = {q.nx, q.ny, q.nz}, y[3], nn[3];
+        int r = m.P->matching_method == IMLS_MATCH_PLANE_ICP ? m.project_one_plane(x, ns, y, nn) : m.project_one(x, ns, y, nn);
+        sink = sink + (double)nn_idx.size() + (double)k_d2.size();
+        if (r >= 0) {
+            rej[r]++;
+            in_cloud.erase(in_cloud.begin() + (long)i);            // it = in_cloud->erase(it)
+            orig.erase(orig.begin() + (long)i);
+            continue;
+        }
+        out_cloud.push_back(Pt48{y[0], y[1], y[2], 0.f, nn[0], nn[1], nn[2], 0.f, 0.f, 0.f, 0.f, 0.f});
+        ++i;
+    }
+    // getXYZ(in_cloud), getXYZ(out_cloud), getNormals(out_cloud) (laser_odometry.cpp:595-599)
+    std::vector<std::array<double, 3>> vin, vref, vnrm;
+    for (const Pt48& p : in_cloud) vin.push_back({(double)p.x, (double)p.y, (double)p.z});
+    for (const Pt48& p : out_cloud) { vref.push_back({(double)p.x, (double)p.y, (double)p.z}); vnrm.push_back({(double)p.nx, (double)p.ny, (double)p.nz}); }
+    for (size_t k = 0; k < in_cloud.size(); ++k) {
+        const float xs[3] = {in_cloud[k].x, in_cloud[k].y, in_cloud[k].z};
+        const float ys[3] = {out_cloud[k].x, out_cloud[k].y, out_cloud[k].z};
+        const float ns[3] = {out_cloud[k].nx, out_cloud[k].ny, out_cloud[k].nz};
+        c.x.insert(c.x.end(), xs, xs + 3);
+        c.y.insert(c.y.end(), ys, ys + 3);
+        c.n.insert(c.n.end(), ns, ns + 3);
+        c.idx.push_back(orig[k]);
+    }
+    sink = sink + (double)vin.size() + (double)vref.size() + (double)vnrm.size();
+}
 
 void project_all(const Matcher& m, const Cloud& src, const double T[16], bool rot_normals, Corr& c, uint64_t rej[6]) {
+    if (g_faithful && g_threads <= 1) { project_all_faithful(m, src, T, rot_normals, c, rej); return; }
     for (int k = 0; k < 6; ++k) rej[k] = 0;
     c.x.clear(); c.y.clear(); c.n.clear(); c.idx.clear();
     if (g_threads > 1) {
@@ -1188,6 +1253,7 @@ int oracle_format_pose(const double P[16], const char* timestamp, char* buf, siz
                          q[1], q[2], q[3]);
 }
 void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+void oracle_set_faithful(int on) { g_faithful = on ? 1 : 0; }
 int32_t oracle_rand_next(int32_t* state) { return rand_next(state); }
 
 int oracle_colpiv_qr_solve(const double* A, int rows, int cols, const double* b, double* x) {

@@ -83,6 +83,12 @@ int oracle_register_frame_rs(const float* src6, size_t N, const float* tgt6, siz
 void oracle_chain_pose(const double prev[16], const double rel[16], double out[16]);
 int oracle_format_pose(const double pose[16], const char* timestamp, char* buf, size_t cap);
 
+/* CPU-baseline modes (bench.py only): threads of the per-query projection loop, and the
+ * "faithful" container costs of the reference (AoS copy per iteration, erase per rejected point,
+ * per-query heap vectors; identical results). */
+void oracle_set_threads(int n);
+void oracle_set_faithful(int on);
+
 /* glibc rand() restated (common.cpp:49 consumes it).  Fills 34-word state for srand(seed). */
 void oracle_rand_seed(int32_t* state, uint32_t seed);
 int32_t oracle_rand_next(int32_t* state);

@@ -51,6 +51,7 @@ def lib():
         L.oracle_rand_seed.argtypes = [VP, C.c_uint32]
         L.oracle_rand_next.argtypes = [VP]
         L.oracle_set_threads.argtypes = [C.c_int]
+        L.oracle_set_faithful.argtypes = [C.c_int]
         L.oracle_rand_next.restype = C.c_int32
         L.oracle_colpiv_qr_solve.argtypes = [VP, C.c_int, C.c_int, VP, VP]
         L.oracle_delta_from_x.argtypes = [VP, VP]
@@ -232,3 +233,9 @@ def sample_point_cloud(xyz, nrm, candidates, last_xyz, sample_params):
 def set_threads(n: int):
     """Threads of the oracle's per-query projection loop (1 = the reference's single thread)."""
     lib().oracle_set_threads(int(n))
+
+
+def set_faithful(on: bool):
+    """The reference's container costs in the projection loop (erase per rejection, AoS copies,
+    per-query allocations); identical results.  CPU baseline only."""
+    lib().oracle_set_faithful(int(bool(on)))

@@ -131,11 +131,9 @@ KParams make_kparams(const imls_params& p) {
     k.seed_half = 1;
     k.reseed = 0.25f;
     k.sparse_lanes = 32;
-    k.sparse_lanes_seed = 4;
     if (const char* w = std::getenv("IMLS_SPARSE")) k.sparse_lanes = std::atoi(w);
     k.qwave = -1;   // auto
     if (const char* w = std::getenv("IMLS_QWAVE")) k.qwave = std::atoi(w);
-    if (const char* w = std::getenv("IMLS_SPARSE_SEED")) k.sparse_lanes_seed = std::atoi(w);
     if (const char* w = std::getenv("IMLS_SEED_HALF")) k.seed_half = std::atoi(w);
     if (const char* w = std::getenv("IMLS_RESEED")) k.reseed = (float)std::atof(w);
     if (const char* w = std::getenv("IMLS_WAVE_TRACE")) k.wave_trace = std::atoi(w);

@@ -52,7 +52,6 @@ struct KParams {
     int seed_half;            // seed pass scans the nearest leaf ± seed_half Morton neighbours
     float reseed;             // temporal seed unless displacement² > reseed · previous worst key
     int sparse_lanes;         // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
-    int sparse_lanes_seed;    // the same for waves holding freshly seeded lanes
     int qwave;                // traversal: 0 = packets of 64 queries per wave, 1 = one wave per query
     int wide;                 // packet traversal: binary levels descended per step (1..3)
     int verlet;               // reuse a query's list without traversal while its certification holds

@@ -40,11 +40,13 @@ namespace {
 constexpr double kInfD = __builtin_huge_val();
 constexpr float kInfF = __builtin_huge_valf();
 constexpr int kWaveBlock = 256;
+// constant address space view of read-only device data: wave-uniform loads through it are scalar
+typedef float kf4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const kf4v kconst_f4;
 constexpr int kFallbackBlocks = 64;
 constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query up to this many queries
 constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
 constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
-constexpr int kSeedLeaves = 8;       // first-iteration seed pass: at most this many leaves per wave
 #ifndef IMLS_SEED_CHUNK
 #define IMLS_SEED_CHUNK 8
 #endif
@@ -308,7 +310,6 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView 
                                                          int use_prev, unsigned long long* __restrict__ nbr_stats,
                                                          unsigned* __restrict__ fb_count) {
     if (done && *done) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = 0u;   // k_finish's deferred-query counter
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float4 sbox[kWaveBlock / 64][kWaveStack][2];
     __shared__ float4 sleaf[kWaveBlock / 64][64];   // the current leaf's points (lockstep insertion)
@@ -332,7 +333,6 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView 
 #ifdef IMLS_DEBUG_WAVE_TRACE
     const long long dbg_t0 = wall_clock64();
 #endif
-    int seed_lo = 0, seed_hi = -1;   // leaves already scanned by the seed pass (skipped below)
     bool greedy = active && !use_prev;
     bool skip = false;               // list certified without a traversal (Verlet-list reuse)
     float wskip = kInfF;
@@ -520,17 +520,15 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView 
             }
         }
     };
-    // seed, first ICP iteration (every lane): the leaves holding the lanes' own Morton keys
-    // (binary search over the leaves' first keys) — Morton-near points are mostly space-near,
-    // while a greedy box-distance descent goes astray in the heavily overlapping upper-level
-    // boxes.  The wave's 64 queries are Morton-coherent, so their leaves mostly coincide: a
-    // narrow range [min, max] ± seed_half is scanned wave-wide (one coalesced load per leaf,
-    // skipped by the traversal later); otherwise each distinct lane leaf once (≤ kSeedLeaves).
+    // seed (first ICP iteration, or a lane that moved far): the leaf holding the lane's own Morton
+    // key (binary search over the leaves' first keys) ± seed_half, scanned per lane — Morton-near
+    // points are mostly space-near, while a greedy box-distance descent goes astray in the heavily
+    // overlapping upper-level boxes.  The traversal re-scans these leaves harmlessly (listed points
+    // are masked, the rest are not under the bound).  (A wave-wide seed pass over the packet's
+    // leaves measured no faster, and its second inlined copy of scan_leaf raised the kernel's
+    // register demand from ~160 to ~200 VGPRs.)
     const unsigned long long gmask = __ballot(greedy);
-    if (greedy && use_prev) {
-        // a reseeded lane amid prefilled ones: its own leaf ± seed_half, scanned per lane (the
-        // traversal re-scans these leaves harmlessly: listed points are masked, the rest are
-        // not under the bound)
+    if (greedy) {
         const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
         int l = 0, h = t.L - 1;
         while (l < h) {
@@ -560,40 +558,6 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView 
             for (int k = 0; k < kSeedChunk; ++k) qs[k] = nx[k];
         }
     }
-    if (gmask && !use_prev) {
-        sparse_thr = kp.sparse_lanes_seed;   // freshly seeded lanes insert a lot: per-lane scans would serialise that
-        int lo = 0x7fffffff;
-        if (greedy) {
-            const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
-            int l = 0, h = t.L - 1;
-            while (l < h) {
-                const int mid = (l + h + 1) >> 1;
-                if (t.lkeys[mid] <= qk) l = mid;
-                else h = mid - 1;
-            }
-            lo = l;
-        }
-        int lmin = lo, lmax = greedy ? lo : -1;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            lmin = min(lmin, __shfl_xor(lmin, o, 64));
-            lmax = max(lmax, __shfl_xor(lmax, o, 64));
-        }
-        lmin = __builtin_amdgcn_readfirstlane(lmin);
-        lmax = __builtin_amdgcn_readfirstlane(lmax);
-        if (lmax - lmin + 1 + 2 * kp.seed_half <= kSeedLeaves) {
-            seed_lo = max(0, lmin - kp.seed_half);
-            seed_hi = min(t.L - 1, lmax + kp.seed_half);
-            for (int leaf = seed_lo; leaf <= seed_hi; ++leaf) scan_leaf(leaf, gmask, false);
-        } else {
-            unsigned long long m = gmask;
-            for (int n = 0; m && n < kSeedLeaves; ++n) {
-                const int leaf = __builtin_amdgcn_readlane(lo, __builtin_ctzll(m));
-                m &= ~__ballot(lo == leaf);
-                scan_leaf(leaf, gmask, true);
-            }
-        }
-    }
     unsigned n_inner = 0, n_leaf = 0;
 #ifdef IMLS_DEBUG_WAVE_TRACE
     const long long dbg_t1 = wall_clock64();
@@ -612,10 +576,18 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView 
             const int lev = 31 - __builtin_clz(node);
             const int sw = min(kp.wide, t.levels - lev);
             const int nk = 1 << sw, nrec = nk >> 1;
-            const float4* rec = t.nodes + 3 * ((size_t)node << (sw - 1));
+            // the records are read-only for the whole kernel and the address is wave-uniform: read
+            // them through the constant address space so they come by scalar loads into SGPRs (a
+            // generic pointer is may-clobbered by the fences / atomics of this kernel and would be
+            // fetched by vector loads into 48 VGPRs)
+            const int unode = __builtin_amdgcn_readfirstlane(node);
+            const kconst_f4* rec = (const kconst_f4*)t.nodes + 3 * ((size_t)unode << (sw - 1));
             float4 R[3 * (kWideMax / 2)];
 #pragma unroll
-            for (int k = 0; k < 3 * (kWideMax / 2); ++k) R[k] = rec[min(k, 3 * nrec - 1)];
+            for (int k = 0; k < 3 * (kWideMax / 2); ++k) {
+                const kf4v v = rec[min(k, 3 * nrec - 1)];
+                R[k] = make_float4(v.x, v.y, v.z, v.w);
+            }
             const float bs = bnd * kBoxSlack;
             unsigned long long m[kWideMax];
             int best = -1;
@@ -656,7 +628,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView 
         } else {
             ++n_leaf;
             const int leaf = node - P;
-            if (leaf < seed_lo || leaf > seed_hi) scan_leaf(leaf, em, use_prev || gmask);
+            scan_leaf(leaf, em, use_prev || gmask);
         }
         // pop: the stacked node's box is in LDS — re-check it against the shrunken lane bounds
         node = 0;
@@ -719,6 +691,10 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView 
         atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
         atomicAdd(&nbr_stats[4], 1ull);
     }
+    // k_finish's deferred-query counter, zeroed at the END of the kernel: a global store ahead
+    // of the traversal may-clobbers every later load, and the node records are then fetched by
+    // vector loads instead of through the scalar cache
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = 0u;
 }
 
 // =============================================================================================
@@ -740,7 +716,6 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
                                                           unsigned* __restrict__ fb_count) {
     static_assert(KL <= 64, "one list entry per lane");
     if (done && *done) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = 0u;   // k_finish's deferred-query counter
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float sdist[kWaveBlock / 64][kWaveStack];
     const int lane = threadIdx.x & 63;
@@ -942,6 +917,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
         atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
         atomicAdd(&nbr_stats[4], 1ull);
     }
+    // k_finish's deferred-query counter, zeroed at the END of the kernel: a global store ahead
+    // of the traversal may-clobbers every later load, and the node records are then fetched by
+    // vector loads instead of through the scalar cache
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = 0u;
 }
 
 // =============================================================================================

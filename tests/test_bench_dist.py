@@ -1,0 +1,84 @@
+"""CPU (gloo, world size 2): bench.py's own multi-rank path — rank setup (dist_setup with
+--backend gloo), the timed region (barrier + sync on both sides, max-over-ranks elapsed),
+the one pose exchange (all-gather in unit order) and the trajectory chaining — driven through
+the functions bench.main uses.  The device leg is replaced, in this test only, by the CPU oracle
+registering a small golden pair, so the poses are real registration results."""
+import os
+import pathlib
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def marker(rank, k):
+    from planetary_lidar_odometry_amd import synth
+    return synth.pose_xyyaw(0.01 * rank, 0.001 * k, 0.0001 * (rank * 10 + k))
+
+
+def _worker(rank, world, port, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    import bench
+    import oracle_ctypes as oc
+    from planetary_lidar_odometry_amd import config
+    import torch.distributed as dist
+    w, r, _, dev = bench.dist_setup("gloo")
+    assert (w, r) == (world, rank) and dev.type == "cpu"
+    g = dict(np.load(ROOT / "tests" / "golden" / "vlp16_pair.npz"))
+    p = config.bench_params(2)
+    counter = [0]
+
+    def step():           # one unit per step on this rank: a real (oracle) registration, tagged
+        res = oc.register_frame(g["src"], g["tgt"], p)
+        k = counter[0]
+        counter[0] += 1
+        return [(res["pose"] @ marker(rank, k), res["iters"], res["status"])]
+
+    elapsed, per, out = bench.timed_steps(step, steps, world, dev)
+    allp, traj = bench.exchange_poses([o[0] for o in out], world)
+    q.put((rank, elapsed, sum(per), allp, traj))
+    dist.destroy_process_group()
+
+
+def test_bench_dist_path_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port, steps, world = _free_port(), 3, 2
+    procs = [ctx.Process(target=_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import oracle_ctypes as oc
+    from planetary_lidar_odometry_amd import config
+    g = dict(np.load(ROOT / "tests" / "golden" / "vlp16_pair.npz"))
+    base = oc.register_frame(g["src"], g["tgt"], config.bench_params(2))["pose"]
+    want = np.array([base @ marker(r, k) for r in range(world) for k in range(steps)])   # unit order: rank-major
+    chained = []
+    T = np.eye(4)
+    for d in want:
+        T = T @ d
+        chained.append(T)
+    elapsed = [t[1] for t in res]
+    assert elapsed[0] == elapsed[1]                          # max over ranks, identical on every rank
+    assert all(elapsed[0] >= t[2] for t in res)              # ≥ each rank's own time in its steps
+    for _, _, _, allp, traj in res:
+        assert np.array_equal(allp, want)
+        assert np.allclose(traj, np.array(chained), rtol=0, atol=1e-12)

@@ -438,3 +438,19 @@ def test_oracle_rand_state_carries_across_frames():
     assert not np.array_equal(st, st0)
     fresh = oc.register_frame(g["src"], g["tgt"], p)
     assert np.array_equal(a["pose"], fresh["pose"])   # first frame: the stream starts at the seed either way
+
+
+def test_faithful_baseline_mode_is_identical():
+    """bench.py's "faithful" CPU baseline (the reference's erase-per-rejection loop, AoS copies and
+    per-query allocations) computes exactly what the efficient oracle computes."""
+    g = golden("vlp16_pair")
+    p = gparams(6)
+    a = oc.register_frame(g["src"], g["tgt"], p)
+    oc.set_faithful(True)
+    try:
+        b = oc.register_frame(g["src"], g["tgt"], p)
+        x, y, n, idx, rej = oc.project(g["src"], g["tgt"], g["pose1"], p)
+    finally:
+        oc.set_faithful(False)
+    assert np.array_equal(a["pose"], b["pose"]) and a["iters"] == b["iters"]
+    assert np.array_equal(idx, g["idx1"]) and np.array_equal(rej, g["rej1"]) and np.array_equal(y, g["y1"])
