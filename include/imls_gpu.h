@@ -269,11 +269,32 @@ int imls_register_frame_async(imls_ctx* ctx);
 int imls_register_frame_result(imls_ctx* ctx, double pose_out[16], int* iters_run, int* status,
                                imls_iter_trace* trace);
 
+/* ---- many frames in one launch sequence (configs C/D: many sequences per GPU) ------------ */
+/* Registers the frames already loaded into ctxs[0..n) (each by imls_set_target / imls_map_push +
+ * imls_set_source, exactly as before imls_register_frame) in ONE launch sequence: every
+ * per-iteration kernel is launched once for all n frames (grid y = frame), each frame at its own
+ * pose, convergence flag and iteration count, so n small frames (the ≤ 2000-point flat clouds of a
+ * KITTI stream) fill the GPU together.  Each frame's result, trace and iteration count are
+ * bit-identical to imls_register_frame on its context (laser_odometry.cpp:478-660 per frame:
+ * frames are independent, 484-485).  All contexts must be on one device with equal params; the
+ * launches run on ctxs[0]'s stream after every context's pending uploads, and every context's later
+ * work is ordered after them.  RANSAC / DRPM, tensor voting, the projected-distance rule and the
+ * exact per-lane mode run one launch sequence per frame instead (same results, less overlap).
+ * poses_out[16·k], iters_out[k], status_out[k], traces[k·iterations …] (each nullable) receive
+ * frame k's result.  The _async form returns after enqueueing; imls_register_frames_result(ctxs[0],
+ * …) synchronises and fills the outputs. */
+int imls_register_frames(imls_ctx* const* ctxs, size_t n, double* poses_out, int32_t* iters_out,
+                         int32_t* status_out, imls_iter_trace* traces);
+int imls_register_frames_async(imls_ctx* const* ctxs, size_t n);
+int imls_register_frames_result(imls_ctx* lead, double* poses_out, int32_t* iters_out,
+                                int32_t* status_out, imls_iter_trace* traces);
+
 /* ---- many independent pairs (configs C/D: a KITTI stream, many sequences per GPU) -------- */
 /* Every frame's registration starts from rPose = I against the raw previous scan(s)
  * (laser_odometry.cpp:484-485, 116-136), so frames are independent: a batch keeps `streams`
- * contexts (one HIP stream each) and keeps that many registrations in flight, overlapping one
- * pair's host upload and index build with the others' ICP loops.  One batch per host thread. */
+ * contexts (1..256, one HIP stream each); pairs are taken in groups of that many, each group
+ * uploaded and indexed (one context per pair) and then registered as ONE launch sequence
+ * (imls_register_frames).  One batch per host thread. */
 typedef struct imls_batch imls_batch;
 typedef struct imls_pair_input {
     const float* src_xyz;             /* the flat (source) cloud, as imls_set_source */

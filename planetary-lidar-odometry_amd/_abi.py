@@ -182,6 +182,9 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_batch_destroy": (None, [VP]),
         "imls_batch_last_error": (C.c_char_p, [VP]),
         "imls_register_batch": (C.c_int, [VP, SZ, VP, VP, VP, VP]),
+        "imls_register_frames": (C.c_int, [VP, SZ, VP, VP, VP, VP]),
+        "imls_register_frames_async": (C.c_int, [VP, SZ]),
+        "imls_register_frames_result": (C.c_int, [VP, VP, VP, VP, VP]),
         "imls_sample_point_cloud": (C.c_int, [VP, P(ImlsSampleParams), VP, VP, SZ, SZ, VP, SZ, VP, SZ, SZ, VP, P(SZ),
                                               VP]),
         "imls_seed_rng": (C.c_int, [VP, C.c_uint32]),
@@ -210,6 +213,7 @@ ABI_SYMBOLS = (
     "imls_default_sample_params", "imls_sample_point_cloud", "imls_batch_create", "imls_batch_destroy",
     "imls_batch_last_error", "imls_register_batch", "imls_seed_rng", "imls_get_rng_state",
     "imls_set_rng_state", "imls_map_push", "imls_map_push_device", "imls_map_clear", "imls_map_size",
+    "imls_register_frames", "imls_register_frames_async", "imls_register_frames_result",
 )
 
 _LIB = None

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <deque>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "internal.h"
@@ -55,6 +56,18 @@ struct imls_ctx {
     int temporal_seed = 1;
     int N = 0;
     bool has_source = false;
+    // deferred index builds: set_target / map_push / set_source without a requested count only
+    // enqueue the upload and the NaN filter; the rest of the build (which needs the kept count on
+    // the host) runs at the first use (ensure_built), so many frames' filters overlap one wait
+    int* h_cnt = nullptr;                 // pinned [4]: kept counts of the pending target / source
+    hipEvent_t ev_tgt = nullptr, ev_src = nullptr;
+    bool tgt_pending = false, src_pending = false;
+    int tgt_slot = -1;                    // timing event slot of the pending target build
+    uint32_t* src_kept_out = nullptr;
+    // pinned staging of host uploads (0: target / map scans, 1: source), reused once its copy ran
+    float* h_stage[2] = {nullptr, nullptr};
+    size_t stage_cap[2] = {0, 0};
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
     // correspondences + solver state
     DevBuf cs, cd, cn, solve_mem, trace_mem, stats, rows_d, pose_tmp;
     DevBuf ransac_mem, rng;               // RANSAC scratch + the glibc rand() state (34 words)
@@ -69,6 +82,16 @@ struct imls_ctx {
     double* h_misc = nullptr;             // pinned: pose[16], iters, status
     int pending_iters = 0;
     bool pending = false;
+    // batched registration led by this context (imls_register_frames*): frame table, results
+    PairDev* tab_h = nullptr;             // pinned [tab_cap]
+    DevBuf tab_d, res_d;
+    double* res_h = nullptr;              // pinned [tab_cap][kResStride]
+    int tab_cap = 0;
+    std::vector<imls_ctx*> members;       // frames of the pending batch (members[0] == this)
+    std::vector<int> member_n;
+    bool batch_pending = false, batch_fused = false, batch_traces = false;
+    bool batch_member = false;            // part of a pending batch (as lead or member)
+    hipEvent_t ev_batch = nullptr;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev;
@@ -85,13 +108,17 @@ int fail(imls_ctx* c, int code, const std::string& m) {
     return code;
 }
 
+// Grow-only device buffers with 25 % headroom: per-frame sizes vary by a few percent, and every
+// reallocation is a hipFree, which waits for the whole device (it would stall the other contexts'
+// work in flight and the host).
 bool grow(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes) return true;
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
-    if (hipMalloc(&b.p, bytes) != hipSuccess) return false;
-    b.bytes = bytes;
+    const size_t want = bytes + bytes / 4 + 256;
+    if (hipMalloc(&b.p, want) != hipSuccess) return false;
+    b.bytes = want;
     return true;
 }
 
@@ -185,6 +212,7 @@ int check_params(imls_ctx* c, const imls_params* p) {
 int ensure_solve(imls_ctx* c, int N) {
     if (c->st_N >= N && c->st.trace) return IMLS_OK;
     size_t n = (size_t)std::max(N, 1);
+    n += n / 4 + 64;                      // headroom (see grow): the next frames' N differ a little
     if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, n * 4 + 256))
         return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
     if (!grow(c->prevnn, prevnn_bytes((int)n))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
@@ -382,50 +410,132 @@ void harvest_timing(imls_ctx* c) {
     c->ev_used = 0;
 }
 
-// Pack a strided host cloud into SoA6 floats and upload.
-int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, size_t n, size_t stride) {
+// Pack a strided host cloud into SoA6 floats in pinned staging and upload asynchronously (no host
+// wait: the staging buffer is reused only after its previous copy has run).
+int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, size_t n, size_t stride, int which) {
     if (!xyz || !nrm || n == 0 || stride < 3) return fail(c, IMLS_ERR_ARG, "bad cloud pointer/size/stride");
-    std::vector<float> h(6 * n);
-    for (size_t i = 0; i < n; ++i) {
-        const float* p = xyz + i * stride;
-        const float* q = nrm + i * stride;
-        h[i] = p[0]; h[n + i] = p[1]; h[2 * n + i] = p[2];
-        h[3 * n + i] = q[0]; h[4 * n + i] = q[1]; h[5 * n + i] = q[2];
+    if (!c->ev_stage[which] && hipEventCreateWithFlags(&c->ev_stage[which], hipEventDisableTiming) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "hipEventCreate (staging)");
+    if (hipEventSynchronize(c->ev_stage[which]) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "staging wait");
+    if (c->stage_cap[which] < 6 * n) {
+        if (c->h_stage[which]) (void)hipHostFree(c->h_stage[which]);
+        c->h_stage[which] = nullptr;
+        c->stage_cap[which] = 0;
+        const size_t cap = 6 * n + 6 * n / 4 + 1024;
+        if (hipHostMalloc((void**)&c->h_stage[which], cap * 4) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipHostMalloc (staging)");
+        c->stage_cap[which] = cap;
     }
-    if (!grow(dst, h.size() * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (upload)");
-    if (hipMemcpyAsync(dst.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
+    float* h = c->h_stage[which];
+    auto pack = [=](size_t i0, size_t i1) {
+        float *hx = h, *hy = h + n, *hz = h + 2 * n, *hnx = h + 3 * n, *hny = h + 4 * n, *hnz = h + 5 * n;
+        for (size_t i = i0; i < i1; ++i) {
+            const float* p = xyz + i * stride;
+            const float* q = nrm + i * stride;
+            hx[i] = p[0]; hy[i] = p[1]; hz[i] = p[2];
+            hnx[i] = q[0]; hny[i] = q[1]; hnz[i] = q[2];
+        }
+    };
+    // a scan of ~10^5 points is a strided gather of several MB: split it over host threads
+    const size_t T = std::min<size_t>(std::max<size_t>(std::thread::hardware_concurrency(), 1),
+                                      std::min<size_t>(8, n / 16384 + 1));
+    if (T <= 1) {
+        pack(0, n);
+    } else {
+        std::vector<std::thread> th;
+        const size_t chunk = (n + T - 1) / T;
+        for (size_t t = 1; t < T; ++t) th.emplace_back(pack, std::min(n, t * chunk), std::min(n, (t + 1) * chunk));
+        pack(0, std::min(n, chunk));
+        for (auto& x : th) x.join();
+    }
+    if (!grow(dst, 6 * n * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (upload)");
+    if (hipMemcpyAsync(dst.p, h, 6 * n * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipEventRecord(c->ev_stage[which], c->stream) != hipSuccess)
         return fail(c, IMLS_ERR_DEVICE, "upload failed");
     return IMLS_OK;
 }
 
+// Phase B of a pending target build (waits for its filter's kept count).
+int finish_target(imls_ctx* c) {
+    if (!c->tgt_pending) return IMLS_OK;
+    c->tgt_pending = false;
+    if (hipEventSynchronize(c->ev_tgt) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "target filter failed");
+    c->M = c->h_cnt[0];
+    int rc = build_target_tree(c->stream, c->M, c->B, c->lkeys, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch,
+                               c->treescratch, c->permbuf, &c->Pl, &c->levels, c->err);
+    timed_end(c, 1, c->tgt_slot);
+    c->tgt_slot = -1;
+    c->has_target = rc == IMLS_OK && c->M > 0;
+    return rc;
+}
+
+// Phase B of a pending source load.
+int finish_source(imls_ctx* c) {
+    if (!c->src_pending) return IMLS_OK;
+    c->src_pending = false;
+    if (hipEventSynchronize(c->ev_src) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "source filter failed");
+    c->N = c->h_cnt[1];
+    c->has_source = false;
+    if (int rc = source_order(c->stream, c->N, c->spt, c->sscratch, c->qperm, c->err)) return rc;
+    if (c->src_kept_out && c->N > 0 &&
+        (hipMemcpyAsync(c->src_kept_out, c->skept.p, (size_t)c->N * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+         hipStreamSynchronize(c->stream) != hipSuccess))
+        return fail(c, IMLS_ERR_DEVICE, "kept index download failed");
+    c->src_kept_out = nullptr;
+    c->has_source = c->N > 0;
+    return ensure_solve(c, c->N);
+}
+
+int ensure_built(imls_ctx* c) {
+    if (int rc = finish_target(c)) return rc;
+    return finish_source(c);
+}
+
 int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
+    if (n == 0 || n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "target size out of range");
     if (!grow(c->tkept, n * 4 + 16)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (kept)");
+    if (!c->ev_tgt && hipEventCreateWithFlags(&c->ev_tgt, hipEventDisableTiming) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "hipEventCreate");
     c->has_tensors = false;
-    int slot;
-    timed_begin(c, 1, slot);
-    int rc = build_target_index(c->stream, d_soa6, n, c->B, c->lkeys, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch,
-                                c->treescratch, c->permbuf, &c->M, &c->Pl, &c->levels, c->err, (unsigned*)c->tkept.p);
-    timed_end(c, 1, slot);
+    c->tgt_pending = false;
+    timed_begin(c, 1, c->tgt_slot);
+    int rc = filter_async(c->stream, d_soa6, n, c->tpt, c->tnr, c->tscratch, (unsigned*)c->tkept.p, &c->h_cnt[0], c->err);
     if (rc) return rc;
+    if (hipEventRecord(c->ev_tgt, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "event record");
     c->n_target_in = n;
-    c->has_target = c->M > 0;
+    c->tgt_pending = true;
+    c->has_target = true;                 // provisional: the build decides (an all-NaN map has none)
     c->rnr_valid = false;
     c->has_corr = false;
-    if (n_kept) *n_kept = (size_t)c->M;
+    if (n_kept) {
+        if (int rc2 = finish_target(c)) return rc2;
+        *n_kept = (size_t)c->M;
+    }
     return IMLS_OK;
 }
 
 int do_set_source(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept, uint32_t* kept_index) {
-    int rc = load_source(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, c->qperm, &c->N, c->skept, kept_index, c->err);
+    if (n == 0 || n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "source size out of range");
+    if (kept_index && !grow(c->skept, n * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (kept)");
+    if (!c->ev_src && hipEventCreateWithFlags(&c->ev_src, hipEventDisableTiming) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "hipEventCreate");
+    c->src_pending = false;
+    int rc = filter_async(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, kept_index ? (unsigned*)c->skept.p : nullptr,
+                          &c->h_cnt[1], c->err);
     if (rc) return rc;
-    c->has_source = c->N > 0;
+    if (hipEventRecord(c->ev_src, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "event record");
+    c->src_pending = true;
+    c->src_kept_out = kept_index;
+    c->has_source = true;                 // provisional, as for the target
     c->has_corr = false;
-    if (n_kept) *n_kept = (size_t)c->N;
-    return ensure_solve(c, c->N);
+    if (n_kept || kept_index) {
+        if (int rc2 = finish_source(c)) return rc2;
+        if (n_kept) *n_kept = (size_t)c->N;
+    }
+    return IMLS_OK;
 }
 
 int do_set_tensors(imls_ctx* c, const float* d_ten6, size_t n) {
+    if (int rc = ensure_built(c)) return rc;
     if (!c->has_target) return fail(c, IMLS_ERR_STATE, "set_target first");
     if (n != c->n_target_in) return fail(c, IMLS_ERR_ARG, "tensor count must equal the last set_target's point count");
     if (!grow(c->mten, (size_t)std::max(c->M, 1) * 32)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tensors)");
@@ -507,7 +617,8 @@ imls_ctx* imls_create(int device, const imls_params* p) {
         return nullptr;
     }
     c->stream = c->own;
-    if (hipHostMalloc((void**)&c->h_misc, 32 * sizeof(double)) != hipSuccess) {
+    if (hipHostMalloc((void**)&c->h_misc, 32 * sizeof(double)) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_cnt, 4 * sizeof(int)) != hipSuccess) {
         delete c;
         return nullptr;
     }
@@ -543,6 +654,18 @@ void imls_destroy(imls_ctx* c) {
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->h_trace) (void)hipHostFree(c->h_trace);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
+    if (c->tab_h) (void)hipHostFree(c->tab_h);
+    if (c->h_cnt) (void)hipHostFree(c->h_cnt);
+    for (int k = 0; k < 2; ++k) {
+        if (c->h_stage[k]) (void)hipHostFree(c->h_stage[k]);
+        if (c->ev_stage[k]) (void)hipEventDestroy(c->ev_stage[k]);
+    }
+    if (c->ev_tgt) (void)hipEventDestroy(c->ev_tgt);
+    if (c->ev_src) (void)hipEventDestroy(c->ev_src);
+    if (c->res_h) (void)hipHostFree(c->res_h);
+    if (c->tab_d.p) (void)hipFree(c->tab_d.p);
+    if (c->res_d.p) (void)hipFree(c->res_d.p);
+    if (c->ev_batch) (void)hipEventDestroy(c->ev_batch);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -607,7 +730,7 @@ int imls_synchronize(imls_ctx* c) {
 int imls_set_target(imls_ctx* c, const float* xyz, const float* nrm, size_t n, size_t stride, size_t* n_kept) {
     if (!c) return IMLS_ERR_ARG;
     if (int rc = check_device(c)) return rc;
-    if (int rc = upload_soa6(c, c->upload_t, xyz, nrm, n, stride)) return rc;
+    if (int rc = upload_soa6(c, c->upload_t, xyz, nrm, n, stride, 0)) return rc;
     return do_set_target(c, (const float*)c->upload_t.p, n, n_kept);
 }
 
@@ -635,7 +758,7 @@ static int map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, s
             if (hipMemcpyAsync(sl.buf.p, d_soa6, n * 24, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
                 rc = fail(c, IMLS_ERR_DEVICE, "map slot copy");
         } else {
-            rc = upload_soa6(c, sl.buf, xyz, nrm, n, stride);
+            rc = upload_soa6(c, sl.buf, xyz, nrm, n, stride, 0);
         }
         if (rc) { c->slot_pool.push_back(sl.buf); return rc; }
     }
@@ -648,12 +771,15 @@ static int map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, s
     }
     const size_t M = c->map_points;
     if (M == 0) {                     // empty map (max_queue_size 0 or empty scans): no target
+        c->tgt_pending = false;
         c->has_target = false;
         c->has_corr = false;
         c->M = 0;
         if (n_map) *n_map = 0;
         return IMLS_OK;
     }
+    for (const auto& e : c->fifo)     // one non-empty entry (max_queue_size 1): index it in place
+        if (e.n == M) return do_set_target(c, (const float*)e.buf.p, M, n_map);
     if (!grow(c->macc, M * 24)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (map)");
     size_t off = 0;
     for (const auto& e : c->fifo) {
@@ -743,7 +869,7 @@ int imls_set_source(imls_ctx* c, const float* xyz, const float* nrm, size_t n, s
                     uint32_t* kept_index) {
     if (!c) return IMLS_ERR_ARG;
     if (int rc = check_device(c)) return rc;
-    if (int rc = upload_soa6(c, c->upload_s, xyz, nrm, n, stride)) return rc;
+    if (int rc = upload_soa6(c, c->upload_s, xyz, nrm, n, stride, 1)) return rc;
     return do_set_source(c, (const float*)c->upload_s.p, n, n_kept, kept_index);
 }
 
@@ -756,8 +882,9 @@ int imls_set_source_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n
 int imls_project(imls_ctx* c, const double pose[16], float* x_out, float* y_out, float* n_out, uint32_t* src_index_out,
                  size_t* n_valid, uint64_t reject[IMLS_NUM_REJ]) {
     if (!c || !pose) return IMLS_ERR_ARG;
-    if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
     if (int rc = check_device(c)) return rc;
+    if (int rc = ensure_built(c)) return rc;
+    if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
     if (int rc = ensure_solve(c, c->N)) return rc;
     if (int rc = check_tv_ready(c)) return rc;
     if (int rc = ensure_map_normals(c)) return rc;
@@ -869,8 +996,10 @@ int imls_solve_correspondences(imls_ctx* c, int32_t method, const double* s, con
 
 int imls_register_frame_async(imls_ctx* c) {
     if (!c) return IMLS_ERR_ARG;
-    if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
+    if (c->batch_member) return fail(c, IMLS_ERR_STATE, "the context is part of a pending batch");
     if (int rc = check_device(c)) return rc;
+    if (int rc = ensure_built(c)) return rc;
+    if (!c->has_target || !c->has_source) return fail(c, IMLS_ERR_STATE, "set_target and set_source first");
     if (int rc = ensure_solve(c, c->N)) return rc;
     if (int rc = check_tv_ready(c)) return rc;
     const int iters = c->P.iterations;
@@ -936,6 +1065,233 @@ int imls_register_frame(imls_ctx* c, double pose_out[16], int* iters_run, int* s
 
 }  // extern "C"
 
+// ------------------------------------------------------------------------------------------------
+// Batched registration (imls_register_frames*): the frames loaded into n contexts run through ONE
+// launch sequence — every per-iteration kernel once for all frames (grid y = frame) — on the lead
+// context's stream, so n small frames fill the GPU together instead of n queues of tiny launches.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kResStride = 20;   // per frame: pose[16], iters, status
+
+// rPose = I, done / status / iters = 0, the frame's trace and counters cleared (one launch for the
+// whole batch instead of six fills per frame)
+__global__ void k_batch_init(const PairDev* __restrict__ tab, int iters) {
+    const PairDev A = tab[blockIdx.x];
+    const int t = threadIdx.x;
+    if (t < 16) A.st.pose[t] = (t % 5 == 0) ? 1.0 : 0.0;
+    if (t == 0) { *A.st.done = 0; *A.st.status = 0; *A.st.iters = 0; }
+    if (t < 16) A.stats[t] = 0ull;
+    unsigned long long* tr = reinterpret_cast<unsigned long long*>(A.trace);
+    const int words = iters * (int)(sizeof(imls_iter_trace) / 8);
+    for (int k = t; k < words; k += blockDim.x) tr[k] = 0ull;
+}
+
+__global__ void k_batch_results(const PairDev* __restrict__ tab, int n, double* __restrict__ out) {
+    for (int k = blockIdx.x; k < n; k += gridDim.x) {
+        const PairDev A = tab[k];
+        const int t = threadIdx.x;
+        if (t < 16) out[(size_t)k * kResStride + t] = A.st.pose[t];
+        if (t == 16) out[(size_t)k * kResStride + 16] = (double)*A.st.iters;
+        if (t == 17) out[(size_t)k * kResStride + 17] = (double)*A.st.status;
+    }
+}
+
+// The batched path covers the shipped matcher with the LS-family solvers on float rows; RANSAC /
+// DRPM, tensor voting, the projected-distance rule and the exact per-lane mode keep one launch
+// sequence per frame (each on its own context stream, so they still overlap).
+bool batch_fusable(const imls_ctx* c) {
+    return !c->lane_mode && !c->kp.proj && !c->kp.tv &&
+           (c->P.solve_method == IMLS_SOLVE_LS || c->P.solve_method == IMLS_SOLVE_WEIGHTED_LS);
+}
+
+PairDev pair_dev(imls_ctx* c) {
+    PairDev A{};
+    A.t = tree_view(c);
+    A.spt = (const float4*)c->spt.p;
+    A.snr = (const float4*)c->snr.p;
+    A.qperm = (const unsigned*)c->qperm.p;
+    A.N = c->N;
+    A.cs = (float4*)c->cs.p;
+    A.cd = (float4*)c->cd.p;
+    A.cn = (float4*)c->cn.p;
+    A.lists = (int*)c->prevnn.p;
+    A.st = c->st;
+    A.trace = (imls_iter_trace*)c->trace_mem.p;
+    A.stats = (unsigned long long*)c->stats.p;
+    A.fb_list = fb_list(c);
+    A.fb_count = fb_count(c);
+    return A;
+}
+
+int frames_async(imls_ctx* const* ctxs, size_t n) {
+    if (!ctxs || n == 0 || !ctxs[0]) return IMLS_ERR_ARG;
+    imls_ctx* L = ctxs[0];
+    if (L->batch_pending) return fail(L, IMLS_ERR_STATE, "a batch led by this context is pending");
+    if (int rc = check_device(L)) return rc;
+    for (size_t k = 0; k < n; ++k) {
+        imls_ctx* c = ctxs[k];
+        if (!c) return fail(L, IMLS_ERR_ARG, "null context in the batch");
+        for (size_t j = 0; j < k; ++j)
+            if (ctxs[j] == c) return fail(L, IMLS_ERR_ARG, "a context appears twice in the batch");
+        if (c->device != L->device) return fail(L, IMLS_ERR_ARG, "batch contexts must share one device");
+        if (std::memcmp(&c->P, &L->P, sizeof(imls_params)) != 0)
+            return fail(L, IMLS_ERR_ARG, "batch contexts must share their params (context " + std::to_string(k) + ")");
+        if (c->lane_mode != L->lane_mode || c->temporal_seed != L->temporal_seed || c->B != L->B)
+            return fail(L, IMLS_ERR_ARG, "batch contexts must share their traversal settings");
+        if (c->pending || c->batch_member || (k > 0 && c->batch_pending))
+            return fail(L, IMLS_ERR_STATE, "context " + std::to_string(k) + " has a frame pending");
+    }
+    // every member's deferred build: its filter count (one wait each, all filters already enqueued)
+    // then the rest of its index build on its own stream
+    for (size_t k = 0; k < n; ++k) {
+        imls_ctx* c = ctxs[k];
+        if (c != L && check_device(c)) return fail(L, IMLS_ERR_DEVICE, "hipSetDevice");
+        if (int rc = ensure_built(c)) return fail(L, rc, "context " + std::to_string(k) + ": " + c->err);
+    }
+    (void)hipSetDevice(L->device);
+    for (size_t k = 0; k < n; ++k) {
+        imls_ctx* c = ctxs[k];
+        if (!c->has_target || !c->has_source)
+            return fail(L, IMLS_ERR_STATE, "context " + std::to_string(k) + ": set_target and set_source first");
+    }
+    L->members.assign(ctxs, ctxs + n);
+    L->batch_fused = batch_fusable(L);
+    if (!L->batch_fused) {
+        // one launch sequence per frame, each on its own context stream
+        for (size_t k = 0; k < n; ++k) {
+            if (int rc = imls_register_frame_async(ctxs[k])) {
+                for (size_t j = 0; j < k; ++j) (void)imls_register_frame_result(ctxs[j], nullptr, nullptr, nullptr, nullptr);
+                if (k > 0) L->err = imls_last_error(ctxs[k]);
+                return rc;
+            }
+        }
+        for (size_t k = 0; k < n; ++k) ctxs[k]->batch_member = true;
+        L->batch_pending = true;
+        return IMLS_OK;
+    }
+    const int iters = L->P.iterations;
+    if ((size_t)L->tab_cap < n) {
+        if (L->tab_h) (void)hipHostFree(L->tab_h);
+        if (L->res_h) (void)hipHostFree(L->res_h);
+        L->tab_h = nullptr;
+        L->res_h = nullptr;
+        L->tab_cap = 0;
+        if (hipHostMalloc((void**)&L->tab_h, n * sizeof(PairDev)) != hipSuccess ||
+            hipHostMalloc((void**)&L->res_h, n * kResStride * sizeof(double)) != hipSuccess)
+            return fail(L, IMLS_ERR_DEVICE, "hipHostMalloc (batch)");
+        L->tab_cap = (int)n;
+    }
+    if (!grow(L->tab_d, n * sizeof(PairDev)) || !grow(L->res_d, n * kResStride * sizeof(double)))
+        return fail(L, IMLS_ERR_DEVICE, "hipMalloc (batch)");
+    if (!L->ev_batch && hipEventCreateWithFlags(&L->ev_batch, hipEventDisableTiming) != hipSuccess)
+        return fail(L, IMLS_ERR_DEVICE, "hipEventCreate (batch)");
+    hipStream_t s = L->stream;
+    L->member_n.assign(n, 0);
+    for (size_t k = 0; k < n; ++k) {
+        imls_ctx* c = ctxs[k];
+        if (int rc = ensure_solve(c, c->N)) return fail(L, rc, c->err);
+        if (int rc = ensure_trace(c, iters)) return fail(L, rc, c->err);
+        if (!grow(c->stats, 128)) return fail(L, IMLS_ERR_DEVICE, "hipMalloc");
+        if (int rc = ensure_map_normals(c)) return fail(L, rc, c->err);
+        L->tab_h[k] = pair_dev(c);
+        L->member_n[k] = c->N;
+        if (c != L) {
+            // the frame's uploads and index build ran on its own stream: the batch waits for them
+            if (!c->ev_batch && hipEventCreateWithFlags(&c->ev_batch, hipEventDisableTiming) != hipSuccess)
+                return fail(L, IMLS_ERR_DEVICE, "hipEventCreate (batch)");
+            if (hipEventRecord(c->ev_batch, c->stream) != hipSuccess || hipStreamWaitEvent(s, c->ev_batch, 0) != hipSuccess)
+                return fail(L, IMLS_ERR_DEVICE, "batch stream join");
+        }
+    }
+    (void)hipSetDevice(L->device);
+    const PairDev* tab = (const PairDev*)L->tab_d.p;
+    hipMemcpyAsync(L->tab_d.p, L->tab_h, n * sizeof(PairDev), hipMemcpyHostToDevice, s);
+    k_batch_init<<<(unsigned)n, 64, 0, s>>>(tab, iters);
+    const KParams kp = L->kp;
+    const int* nh = L->member_n.data();
+    for (int it = 0; it < iters; ++it) {
+        int slot;
+        timed_begin(L, 0, slot);
+        launch_project_batch(s, tab, nh, (int)n, kp, it, it > 0 && L->temporal_seed);
+        timed_end(L, 0, slot);
+        timed_begin(L, 2, slot);
+        launch_solve_batch(s, tab, nh, (int)n, kp, it);
+        timed_end(L, 2, slot);
+    }
+    k_batch_results<<<(unsigned)std::min<size_t>(n, 256), 64, 0, s>>>(tab, (int)n, (double*)L->res_d.p);
+    hipMemcpyAsync(L->res_h, L->res_d.p, n * kResStride * sizeof(double), hipMemcpyDeviceToHost, s);
+    L->batch_traces = iters > 0;
+    if (L->batch_traces)
+        for (size_t k = 0; k < n; ++k)
+            hipMemcpyAsync(ctxs[k]->h_trace, ctxs[k]->trace_mem.p, (size_t)iters * sizeof(imls_iter_trace),
+                           hipMemcpyDeviceToHost, s);
+    if (hipGetLastError() != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "batch launch failed");
+    // every member's later work (its next uploads / index build) is ordered after the batch
+    if (hipEventRecord(L->ev_batch, s) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "batch event");
+    for (size_t k = 1; k < n; ++k)
+        if (hipStreamWaitEvent(ctxs[k]->stream, L->ev_batch, 0) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "batch stream join");
+    for (size_t k = 0; k < n; ++k) { ctxs[k]->has_corr = true; ctxs[k]->batch_member = true; }
+    L->batch_pending = true;
+    return IMLS_OK;
+}
+
+int frames_result(imls_ctx* L, double* poses_out, int32_t* iters_out, int32_t* status_out, imls_iter_trace* traces) {
+    if (!L) return IMLS_ERR_ARG;
+    if (!L->batch_pending) return fail(L, IMLS_ERR_STATE, "no batch pending");
+    L->batch_pending = false;
+    const size_t n = L->members.size();
+    for (imls_ctx* m : L->members) m->batch_member = false;
+    const int iters = L->P.iterations;
+    if (!L->batch_fused) {
+        int first = IMLS_OK;
+        for (size_t k = 0; k < n; ++k) {
+            double pose[16];
+            int it = 0, st = 0;
+            const int rc = imls_register_frame_result(L->members[k], pose, &it, &st,
+                                                      traces ? traces + k * (size_t)std::max(iters, 0) : nullptr);
+            if (rc != IMLS_OK) {
+                if (first == IMLS_OK) { first = rc; L->err = "frame " + std::to_string(k) + ": " + imls_last_error(L->members[k]); }
+                continue;
+            }
+            if (poses_out) std::memcpy(poses_out + 16 * k, pose, sizeof(pose));
+            if (iters_out) iters_out[k] = it;
+            if (status_out) status_out[k] = st;
+        }
+        return first;
+    }
+    hipError_t e = hipStreamSynchronize(L->stream);
+    if (e != hipSuccess) return fail(L, IMLS_ERR_DEVICE, std::string("batch failed: ") + hipGetErrorString(e));
+    harvest_timing(L);
+    for (size_t k = 0; k < n; ++k) {
+        const double* r = L->res_h + k * kResStride;
+        if (poses_out) std::memcpy(poses_out + 16 * k, r, 16 * sizeof(double));
+        if (iters_out) iters_out[k] = (int32_t)r[16];
+        if (status_out) status_out[k] = (int32_t)r[17];
+        if (traces && iters > 0) std::memcpy(traces + k * (size_t)iters, L->members[k]->h_trace, (size_t)iters * sizeof(imls_iter_trace));
+    }
+    return IMLS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int imls_register_frames_async(imls_ctx* const* ctxs, size_t n) { return frames_async(ctxs, n); }
+
+int imls_register_frames_result(imls_ctx* lead, double* poses_out, int32_t* iters_out, int32_t* status_out,
+                                imls_iter_trace* traces) {
+    return frames_result(lead, poses_out, iters_out, status_out, traces);
+}
+
+int imls_register_frames(imls_ctx* const* ctxs, size_t n, double* poses_out, int32_t* iters_out, int32_t* status_out,
+                         imls_iter_trace* traces) {
+    if (int rc = frames_async(ctxs, n)) return rc;
+    return frames_result(ctxs[0], poses_out, iters_out, status_out, traces);
+}
+
+}  // extern "C"
+
 struct imls_batch {
     std::vector<imls_ctx*> ctx;
     std::string err;
@@ -944,7 +1300,7 @@ struct imls_batch {
 extern "C" {
 
 imls_batch* imls_batch_create(int device, const imls_params* p, int32_t streams) {
-    if (streams < 1 || streams > 16) return nullptr;
+    if (streams < 1 || streams > 256) return nullptr;
     imls_batch* b = new imls_batch();
     for (int s = 0; s < streams; ++s) {
         imls_ctx* c = imls_create(device, p);
@@ -969,45 +1325,30 @@ int imls_register_batch(imls_batch* b, size_t n_pairs, const imls_pair_input* pa
                         int32_t* iters_out, int32_t* status_out) {
     if (!b) return IMLS_ERR_ARG;
     if (n_pairs > 0 && !pairs) { b->err = "null pairs"; return IMLS_ERR_ARG; }
+    // groups of S pairs (one per context): upload + index every pair of the group, then register the
+    // group as ONE launch sequence (imls_register_frames)
     const size_t S = b->ctx.size();
-    std::vector<long long> owner(S, -1);      // pair in flight on each context
-    int first_rc = IMLS_OK;
-    auto collect = [&](size_t s) {
-        const long long i = owner[s];
-        if (i < 0) return;
-        owner[s] = -1;
-        double pose[16];
-        int it = 0, st = 0;
-        const int rc = imls_register_frame_result(b->ctx[s], pose, &it, &st, nullptr);
-        if (rc != IMLS_OK) {
-            if (first_rc == IMLS_OK) {
-                first_rc = rc;
-                b->err = "pair " + std::to_string(i) + ": " + imls_last_error(b->ctx[s]);
+    for (size_t g = 0; g < n_pairs; g += S) {
+        const size_t m = std::min(S, n_pairs - g);
+        for (size_t k = 0; k < m; ++k) {
+            imls_ctx* c = b->ctx[k];
+            const imls_pair_input& q = pairs[g + k];
+            int rc = imls_set_target(c, q.tgt_xyz, q.tgt_nrm, q.n_tgt, q.stride_floats, nullptr);
+            if (rc == IMLS_OK) rc = imls_set_source(c, q.src_xyz, q.src_nrm, q.n_src, q.stride_floats, nullptr, nullptr);
+            if (rc != IMLS_OK) {
+                b->err = "pair " + std::to_string(g + k) + ": " + imls_last_error(c);
+                return rc;
             }
-            return;
         }
-        if (poses_out) std::memcpy(poses_out + 16 * i, pose, sizeof(pose));
-        if (iters_out) iters_out[i] = it;
-        if (status_out) status_out[i] = st;
-    };
-    for (size_t i = 0; i < n_pairs && first_rc == IMLS_OK; ++i) {
-        const size_t s = i % S;
-        collect(s);                           // the context's previous pair first (its stream is then idle)
-        if (first_rc != IMLS_OK) break;
-        imls_ctx* c = b->ctx[s];
-        const imls_pair_input& q = pairs[i];
-        int rc = imls_set_target(c, q.tgt_xyz, q.tgt_nrm, q.n_tgt, q.stride_floats, nullptr);
-        if (rc == IMLS_OK) rc = imls_set_source(c, q.src_xyz, q.src_nrm, q.n_src, q.stride_floats, nullptr, nullptr);
-        if (rc == IMLS_OK) rc = imls_register_frame_async(c);
+        const int rc = imls_register_frames(b->ctx.data(), m, poses_out ? poses_out + 16 * g : nullptr,
+                                            iters_out ? iters_out + g : nullptr, status_out ? status_out + g : nullptr,
+                                            nullptr);
         if (rc != IMLS_OK) {
-            first_rc = rc;
-            b->err = "pair " + std::to_string(i) + ": " + imls_last_error(c);
-            break;
+            b->err = "pairs " + std::to_string(g) + "..: " + imls_last_error(b->ctx[0]);
+            return rc;
         }
-        owner[s] = (long long)i;
     }
-    for (size_t s = 0; s < S; ++s) collect(s);   // drain
-    return first_rc;
+    return IMLS_OK;
 }
 
 void imls_default_pca_params(imls_pca_params* p) {
@@ -1133,6 +1474,7 @@ int imls_traversal_stats(imls_ctx* c, uint64_t out[8]) {
 
 int imls_index_stats(imls_ctx* c, uint64_t out[8]) {
     if (!c || !out) return IMLS_ERR_ARG;
+    if (int rc = ensure_built(c)) return rc;
     unsigned long long st[2] = {0, 0};
     if (c->stats.p) hipMemcpy(st, c->stats.p, 16, hipMemcpyDeviceToHost);
     out[0] = (uint64_t)c->M;

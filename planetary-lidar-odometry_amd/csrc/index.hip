@@ -192,8 +192,12 @@ __global__ void k_subtree(const float* __restrict__ in, int count, int D, float4
 
 inline unsigned grid_for(size_t n, int b = kBlock) { return (unsigned)((n + b - 1) / b); }
 
-int filter_compact(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, DevBuf& nr, DevBuf& scratch,
-                   int* n_out, unsigned* d_kept, std::string& err) {
+}  // namespace
+
+// NaN filter + order-keeping compaction, asynchronous: the kept count lands in *h_count (pinned
+// host memory) by an async copy behind the compaction — valid once the stream has passed it.
+int filter_async(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, DevBuf& nr, DevBuf& scratch,
+                 unsigned* d_kept, int* h_count, std::string& err) {
     size_t cub_bytes = 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (unsigned*)nullptr, (unsigned*)nullptr, (int)n_in, s) != hipSuccess) {
         err = "hipcub scan size query failed";
@@ -209,14 +213,15 @@ int filter_compact(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, 
     k_flag_finite<<<grid_for(n_in), kBlock, 0, s>>>(d_soa6, n_in, flag);
     hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, flag, pos, (int)n_in, s);
     k_compact<<<grid_for(n_in), kBlock, 0, s>>>(d_soa6, n_in, flag, pos, (float4*)pt.p, (float4*)nr.p, d_kept, cnt);
-    int h = 0;
-    if (hipMemcpyAsync(&h, cnt, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
-        err = "filter/compact failed: " + std::string(hipGetErrorString(hipGetLastError()));
+    if (hipMemcpyAsync(h_count, cnt, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipGetLastError() != hipSuccess) {
+        err = "filter/compact launch failed";
         return IMLS_ERR_DEVICE;
     }
-    *n_out = h;
     return IMLS_OK;
 }
+
+namespace {
 
 // Permutation (sorted → input index) of n float4 points by 48-bit Morton code over their bbox.
 // With lkeys: also the first key of each B-point leaf and the quantisation (seed search).
@@ -255,21 +260,16 @@ int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf
 
 }  // namespace
 
-int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket, DevBuf& lkeys, DevBuf& tpt, DevBuf& tnr,
-                       DevBuf& mpt, DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* M_out,
-                       int* P_out, int* levels_out, std::string& err, unsigned* kept) {
-    if (n_in == 0 || n_in > (size_t)0x7fffffff) { err = "target size out of range"; return IMLS_ERR_ARG; }
-    int M = 0;
-    int rc = filter_compact(s, d_soa6, n_in, tpt, tnr, scratch, &M, kept, err);
-    if (rc) return rc;
-    *M_out = M;
-    if (M == 0) { *P_out = 0; *levels_out = 0; return IMLS_OK; }
+int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& tpt, DevBuf& tnr, DevBuf& mpt,
+                      DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* P_out, int* levels_out,
+                      std::string& err) {
+    if (M <= 0) { *P_out = 0; *levels_out = 0; return IMLS_OK; }
     const int B = bucket;
     int L = (M + B - 1) / B;
     int P = 1, levels = 0;
     while (P < L) { P <<= 1; ++levels; }
     if (levels > kStackDepth - 1) { err = "tree too deep for the traversal stack"; return IMLS_ERR_CAPACITY; }
-    rc = morton_perm(s, (const float4*)tpt.p, M, scratch, permbuf, err, &lkeys, B);
+    int rc = morton_perm(s, (const float4*)tpt.p, M, scratch, permbuf, err, &lkeys, B);
     if (rc) return rc;
     size_t need = ((size_t)P * 24 + 255) / 256 * 256 + 2 * (((size_t)P / kBlock + 1) * 24 + 256) + 1024;
     if (!ensure(treescratch, need, err) || !ensure(mpt, (size_t)M * 36 + 64, err) ||
@@ -303,24 +303,9 @@ int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int buck
     return IMLS_OK;
 }
 
-int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, DevBuf& snr, DevBuf& scratch,
-                DevBuf& qperm, int* N_out, DevBuf& keptbuf, uint32_t* kept, std::string& err) {
-    if (n_in == 0 || n_in > (size_t)0x7fffffff) { err = "source size out of range"; return IMLS_ERR_ARG; }
-    unsigned* dk = nullptr;
-    if (kept) {   // the context's persistent kept-index buffer (no allocation per call)
-        if (!ensure(keptbuf, n_in * 4, err)) return IMLS_ERR_DEVICE;
-        dk = (unsigned*)keptbuf.p;
-    }
-    int N = 0;
-    int rc = filter_compact(s, d_soa6, n_in, spt, snr, scratch, &N, dk, err);
-    if (!rc && kept && N > 0 &&
-        (hipMemcpyAsync(kept, dk, (size_t)N * 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)) {
-        err = "kept index download failed";
-        return IMLS_ERR_DEVICE;
-    }
-    *N_out = N;
-    if (!rc && N > 0) rc = morton_perm(s, (const float4*)spt.p, N, scratch, qperm, err);
-    return rc;
+int source_order(hipStream_t s, int N, DevBuf& spt, DevBuf& scratch, DevBuf& qperm, std::string& err) {
+    if (N <= 0) return IMLS_OK;
+    return morton_perm(s, (const float4*)spt.p, N, scratch, qperm, err);
 }
 
 }  // namespace imlsgpu

@@ -121,15 +121,36 @@ struct SolveState {
     int partial_cap;
 };
 
-// index.hip
-// kept (nullable, n_in entries): filtered index → input index
-int build_target_index(hipStream_t s, const float* d_soa6, size_t n_in, int bucket, DevBuf& lkeys,
-                       DevBuf& tpt, DevBuf& tnr, DevBuf& mpt, DevBuf& nodes, DevBuf& scratch,
-                       DevBuf& treescratch, DevBuf& permbuf, int* M_out, int* P_out, int* levels_out,
-                       std::string& err, unsigned* kept = nullptr);
-// also computes qperm: the source in Morton order (query order of the wave kernel)
-int load_source(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& spt, DevBuf& snr,
-                DevBuf& scratch, DevBuf& qperm, int* N_out, DevBuf& keptbuf, uint32_t* kept, std::string& err);
+// One registration of a batched launch (imls_register_frames): everything a per-iteration kernel
+// reads or writes for that frame.  The batch's table of these lives in device memory; a batched
+// kernel takes its frame from tab[blockIdx.y] (a wave-uniform, read-only load: scalar) and runs the
+// same body as the single-frame kernel, so a frame gives bit-identical results either way.
+struct PairDev {
+    TreeView t;
+    const float4* spt;
+    const float4* snr;
+    const unsigned* qperm;
+    int N;
+    float4 *cs, *cd, *cn;
+    int* lists;                        // [KL][N] + worst keys + xref/nref (prevnn_bytes)
+    SolveState st;
+    imls_iter_trace* trace;            // [iterations]
+    unsigned long long* stats;         // traversal / neighbour counters
+    unsigned* fb_list;                 // uncertified queries (exact fallback) + their count
+    unsigned* fb_count;
+};
+
+// index.hip — two phases, so many frames' uploads and filters can be enqueued before one wait:
+// (A) filter_async: NaN filter + order-keeping compaction (kept: filtered → input index, nullable),
+//     the kept count copied to pinned *h_count behind it;
+// (B) with that count known: build_target_tree (Morton sort, leaf boxes, node records) or
+//     source_order (the source's Morton order = the wave kernels' query order).
+int filter_async(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, DevBuf& nr, DevBuf& scratch,
+                 unsigned* d_kept, int* h_count, std::string& err);
+int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& tpt, DevBuf& tnr, DevBuf& mpt,
+                      DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* P_out, int* levels_out,
+                      std::string& err);
+int source_order(hipStream_t s, int N, DevBuf& spt, DevBuf& scratch, DevBuf& qperm, std::string& err);
 
 // project.hip
 // k_knn_wave → k_finish (+ the exact k_project_lane fallback for uncertified queries); lane_mode
@@ -151,6 +172,12 @@ inline float4* xref_of(int* lists, int N) {
 inline size_t prevnn_bytes(int N) { return ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256 + (size_t)N * 20; }
 constexpr int kStatSkipped = 6;   // nbr_stats slot: lanes whose list was reused without traversal
 int project_blocks(int N);
+constexpr int kPass1Block = 256;       // k_finish block size (one pass-1 slab per block)
+constexpr int kPass1Fallback = 64;     // k_project_lane fallback blocks (one slab each, after the k_finish slabs)
+// Batched projection: one launch per kernel for all `npairs` frames of tab (device), iteration
+// `it` (trace slot), every frame at its own pose / done flag.  n_host: the frames' N (grid shapes).
+void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp, int it,
+                          int use_prev);
 
 // solve.hip
 void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, const float4* cs,
@@ -160,6 +187,9 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
 // N above which the float-row LS takes the grid chain (below: one block, k_solve_small)
 constexpr int kSmallRows = 4096;
 int solve_blocks(int N);
+// Batched LS / weighted-LS solve + pose update for all frames of tab (float rows from the batched
+// projection): k_solve_small over the frames with N ≤ kSmallRows, the grid chain over the others.
+void launch_solve_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp, int it);
 
 // normals.hip — map normals recomputed from the map (get_normals=false, count mode), Morton order
 int launch_map_normals(hipStream_t s, const TreeView& t, int K, double r_normal, float4* out);

@@ -29,6 +29,7 @@
 // k_project_lane — one lane per query, exact fp64 list during the traversal (the fallback, and
 // the IMLS_TRAVERSAL=lane reference mode).
 // Compiled with -ffp-contract=off: every fp64 expression evaluates as written.
+#include <algorithm>
 #include <cfloat>
 
 #include "internal.h"
@@ -44,6 +45,7 @@ constexpr int kWaveBlock = 256;
 typedef float kf4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(4))) const kf4v kconst_f4;
 constexpr int kFallbackBlocks = 64;
+static_assert(kWaveBlock == kPass1Block && kFallbackBlocks == kPass1Fallback, "pass-1 slab layout (solve.hip)");
 constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query up to this many queries
 constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
 constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
@@ -240,8 +242,12 @@ __device__ void block_normeq(const double a[6], double b, double one, double (*r
 __device__ __forceinline__ void store_result(int i, int cat, const float xf[3], const float yf[3], const float nf[3],
                                              float4* cs, float4* cd, float4* cn) {
     cs[i] = make_float4(xf[0], xf[1], xf[2], cat == -1 ? 1.f : 0.f);
-    cd[i] = make_float4(yf[0], yf[1], yf[2], 0.f);
-    cn[i] = make_float4(nf[0], nf[1], nf[2], 0.f);
+    // y and n are read only behind the valid flag (Rows::get, the RANSAC compaction, imls_project):
+    // rejected rows skip them
+    if (cat == -1) {
+        cd[i] = make_float4(yf[0], yf[1], yf[2], 0.f);
+        cn[i] = make_float4(nf[0], nf[1], nf[2], 0.f);
+    }
 }
 
 // =============================================================================================
@@ -300,7 +306,7 @@ __device__ __forceinline__ float need_key(const float (&lk)[KL], float r2, int K
 #endif
 #define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 24 ? IMLS_KNN_WPE : 1)))
 template <int KL, bool LOCKSTEP>
-__global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView t, const float4* __restrict__ spt,
+__device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
                                                          const double* __restrict__ pose,
                                                          const int* __restrict__ done, KParams kp,
@@ -705,7 +711,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(TreeView 
 // Output contract identical to k_knn_wave (positions [KL][N], worst key W per query).
 // =============================================================================================
 template <int KL>
-__global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const float4* __restrict__ spt,
+__device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restrict__ spt,
                                                           const unsigned* __restrict__ qperm, int N,
                                                           const double* __restrict__ pose,
                                                           const int* __restrict__ done, KParams kp,
@@ -932,7 +938,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(TreeView t, const floa
 #define IMLS_FINISH_ATTR
 #endif
 template <int KL>
-__global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(TreeView t, const float4* __restrict__ spt,
+__device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict__ spt,
                                                        const float4* __restrict__ snr,
                                                        const unsigned* __restrict__ qperm, int N,
                                                        const double* __restrict__ pose,
@@ -1042,7 +1048,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(TreeView
 // Per-lane exact traversal (fallback for uncertified queries; IMLS_TRAVERSAL=lane mode)
 // =============================================================================================
 template <int KCAP>
-__global__ __launch_bounds__(kProjBlock) void k_project_lane(TreeView t, const float4* __restrict__ spt,
+__device__ __forceinline__ void project_lane_body(TreeView t, const float4* __restrict__ spt,
                                                              const float4* __restrict__ snr,
                                                              const unsigned* __restrict__ qlist,
                                                              const unsigned* __restrict__ qcount, int N,
@@ -1200,6 +1206,112 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(TreeView t, const f
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Kernels: one frame (arguments by value) and batched (frame = tab[blockIdx.y]; blocks past the
+// frame's own grid leave at once).  Both run the same bodies.
+// ---------------------------------------------------------------------------------------------
+template <int KL, bool LOCKSTEP>
+__global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(
+        TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
+        const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
+        int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
+        int use_prev, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_count) {
+    knn_wave_body<KL, LOCKSTEP>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats,
+                                fb_count);
+}
+
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(
+        TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
+        const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
+        int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
+        int use_prev, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_count) {
+    knn_qwave_body<KL>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats, fb_count);
+}
+
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(
+        TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qperm,
+        int N, const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
+        const float* __restrict__ wlist, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
+        double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats,
+        unsigned* __restrict__ fb_list, unsigned* __restrict__ fb_count) {
+    finish_body<KL>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr, nbr_stats, fb_list,
+                    fb_count);
+}
+
+template <int KCAP>
+__global__ __launch_bounds__(kProjBlock) void k_project_lane(
+        TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qlist,
+        const unsigned* __restrict__ qcount, int N, const double* __restrict__ pose, const int* __restrict__ done,
+        KParams kp, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
+        double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats) {
+    project_lane_body<KCAP>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats);
+}
+
+__device__ __forceinline__ int wave_blocks_of(int N) { return (N + kWaveBlock - 1) / kWaveBlock; }
+// traversal choice (launch_wave): one wave per query for sparse query sets, packets otherwise
+__host__ __device__ __forceinline__ bool use_qwave(const KParams& kp, int N) {
+    return kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN);
+}
+// the list block of a frame (see launch_wave): positions [KL][N], worst keys [N], xref, nref
+template <int KL>
+__device__ __forceinline__ float* wlist_of(int* lists, int N) { return reinterpret_cast<float*>(lists + (size_t)KL * N); }
+__device__ __forceinline__ float4* xref_dev(int* lists, int N) {
+    return reinterpret_cast<float4*>(reinterpret_cast<char*>(lists) + ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256);
+}
+
+template <int KL, bool LOCKSTEP>
+__global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const PairDev* __restrict__ tab, KParams kp,
+                                                                          int use_prev) {
+    const PairDev A = tab[blockIdx.y];
+    if (use_qwave(kp, A.N) || (int)blockIdx.x >= wave_blocks_of(A.N)) return;
+    float4* xref = xref_dev(A.lists, A.N);
+    knn_wave_body<KL, LOCKSTEP>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
+                                wlist_of<KL>(A.lists, A.N), xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats,
+                                A.fb_count);
+}
+
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) void k_knn_qwave_b(const PairDev* __restrict__ tab, KParams kp, int use_prev) {
+    const PairDev A = tab[blockIdx.y];
+    if (!use_qwave(kp, A.N) || (int)blockIdx.x * (kWaveBlock / 64) >= A.N) return;
+    float4* xref = xref_dev(A.lists, A.N);
+    knn_qwave_body<KL>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists, wlist_of<KL>(A.lists, A.N),
+                       xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats, A.fb_count);
+}
+
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish_b(const PairDev* __restrict__ tab, KParams kp,
+                                                                           int it) {
+    const PairDev A = tab[blockIdx.y];
+    if ((int)blockIdx.x >= wave_blocks_of(A.N)) return;
+    finish_body<KL>(A.t, A.spt, A.snr, A.qperm, A.N, A.st.pose, A.st.done, kp, A.lists, wlist_of<KL>(A.lists, A.N), A.cs,
+                    A.cd, A.cn, A.st.partial1, A.trace + it, A.stats, A.fb_list, A.fb_count);
+}
+
+template <int KCAP>
+__global__ __launch_bounds__(kProjBlock) void k_project_lane_b(const PairDev* __restrict__ tab, KParams kp, int it) {
+    const PairDev A = tab[blockIdx.y];
+    project_lane_body<KCAP>(A.t, A.spt, A.snr, A.fb_list, A.fb_count, A.N, A.st.pose, A.st.done, kp, A.cs, A.cd, A.cn,
+                            A.st.partial1 + (size_t)wave_blocks_of(A.N) * kNormEq, A.trace + it, A.stats);
+}
+
+template <int KL>
+void launch_wave_batch(hipStream_t s, const PairDev* tab, int npairs, int maxN, bool any_small, bool any_large,
+                       const KParams& kp, int it, int use_prev) {
+    const int wb = (maxN + kWaveBlock - 1) / kWaveBlock;
+    if (any_small) {
+        const int n = kp.qwave > 0 ? maxN : std::min(maxN, kQwaveAutoN);
+        k_knn_qwave_b<KL><<<dim3((n + kWaveBlock / 64 - 1) / (kWaveBlock / 64), npairs), kWaveBlock, 0, s>>>(tab, kp, use_prev);
+    }
+    if (any_large) {
+        if (kp.lockstep) k_knn_wave_b<KL, true><<<dim3(wb, npairs), kWaveBlock, 0, s>>>(tab, kp, use_prev);
+        else k_knn_wave_b<KL, false><<<dim3(wb, npairs), kWaveBlock, 0, s>>>(tab, kp, use_prev);
+    }
+    k_finish_b<KL><<<dim3(wb, npairs), kWaveBlock, 0, s>>>(tab, kp, it);
+}
+
 template <int KCAP>
 void launch_lane(hipStream_t s, int blocks, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qlist,
                  const unsigned* qcount, int N, const double* pose, const int* done, const KParams& kp, float4* cs,
@@ -1220,7 +1332,7 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
     if (marks) (void)hipEventRecord(marks[0], s);
     // sparse query sets (≤ kQwaveAutoN queries, e.g. FPS-sampled frames): one wave per query;
     // dense scans: packets of 64 Morton-coherent queries
-    if (kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN))
+    if (use_qwave(kp, N))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
                                                                                           delta, lists, wlist, xref, nref, use_prev, stats,
                                                                                           fb_count);
@@ -1237,6 +1349,35 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
 }
 
 }  // namespace
+
+void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp0, int it,
+                          int use_prev) {
+    // auto traversal choice for a batch: the wave-per-query kernel wins on one small frame (latency:
+    // few waves), packets win once the batch's queries fill the GPU (measured on the config-C-like
+    // stream, 32 frames of ~1900 queries per launch: 546 → 320 µs).  Either gives the exact answer.
+    KParams kp = kp0;
+    long long total = 0;
+    for (int k = 0; k < npairs; ++k) total += n_host[k];
+    if (kp.qwave < 0 && total > kQwaveAutoN) kp.qwave = 0;
+    int maxN = 0;
+    bool any_small = false, any_large = false;
+    for (int k = 0; k < npairs; ++k) {
+        maxN = std::max(maxN, n_host[k]);
+        (use_qwave(kp, n_host[k]) ? any_small : any_large) = true;
+    }
+    if (npairs <= 0 || maxN <= 0) return;
+    const int K = kp.K;
+    if (K <= 8) launch_wave_batch<12>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
+    else if (K <= 16) launch_wave_batch<20>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
+    else if (K <= 20) launch_wave_batch<22>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
+    else launch_wave_batch<36>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
+    // exact fallback for uncertified queries: every frame's kFallbackBlocks slabs are written
+    const dim3 g(kFallbackBlocks, npairs);
+    if (K <= 8) k_project_lane_b<8><<<g, kProjBlock, 0, s>>>(tab, kp, it);
+    else if (K <= 16) k_project_lane_b<16><<<g, kProjBlock, 0, s>>>(tab, kp, it);
+    else if (K <= 20) k_project_lane_b<20><<<g, kProjBlock, 0, s>>>(tab, kp, it);
+    else k_project_lane_b<32><<<g, kProjBlock, 0, s>>>(tab, kp, it);
+}
 
 int project_blocks(int N) { return (N + kWaveBlock - 1) / kWaveBlock + kFallbackBlocks; }
 

@@ -16,6 +16,7 @@
 // k_collect (also re-zeroes the histogram) → k_solve_final (1 block).  Every kernel returns at
 // once when the frame's `done` flag is set.  (A "last block finishes the reduction" fusion was
 // measured slower on MI355X: each block's agent-scope release fence writes back its XCD's L2.)
+#include <algorithm>
 #include <cfloat>
 
 #include "solve_common.h"
@@ -44,12 +45,16 @@ __global__ __launch_bounds__(NT) void k_rows_pass1(Rows rows, int N, double* __r
 }
 
 // Reduce pass-1 partials, first solve, set up the trim; or, for WLS, the only solve.
-__global__ __launch_bounds__(256) void k_solve_first(const double* __restrict__ partial, int blocks, SolveState st,
-                                                     imls_iter_trace* tr, KParams kp, int weighted, int update_pose) {
+__device__ __forceinline__ void solve_first_body(const double* __restrict__ partial, int blocks, const SolveState& st,
+                                                 imls_iter_trace* tr, const KParams& kp, int weighted, int update_pose) {
     if (*st.done) return;
     __shared__ double acc[kNormEq];
     __shared__ double red[(256 / 64) * kNormEq];
     solve_first_block<256>(partial, blocks, st, tr, kp, weighted, update_pose, red, acc);
+}
+__global__ __launch_bounds__(256) void k_solve_first(const double* __restrict__ partial, int blocks, SolveState st,
+                                                     imls_iter_trace* tr, KParams kp, int weighted, int update_pose) {
+    solve_first_body(partial, blocks, st, tr, kp, weighted, update_pose);
 }
 
 // 65536 bins on the top 16 bits of the float image of |r| (sign bit 0: 8 exponent + 7 mantissa
@@ -87,7 +92,7 @@ __device__ unsigned block_exscan(unsigned v, unsigned* wsum, unsigned* all) {
 // 256 coarse bins (256 fine bins each) finds the coarse bin of each rank, a scan of that coarse
 // bin's fine bins the fine one.  One block of kCoarse threads; k_collect re-zeroes both levels.
 constexpr int kCoarse = kHistBins / 256;
-__global__ __launch_bounds__(kCoarse) void k_find_bins(SolveState st) {
+__device__ __forceinline__ void find_bins_body(const SolveState& st) {
     if (*st.done) return;
     __shared__ unsigned wsum[kCoarse / 64];
     __shared__ int cb[2];
@@ -127,12 +132,12 @@ constexpr int kResidBlock = 1024;
 constexpr int kResidBlocks = 96;
 constexpr int kResidWin = 16384;                          // 128 octaves of 1/128-octave bins
 constexpr int kResidWinLo = (0x1F800000 >> 15);           // key_bin(2^-64)
-__global__ __launch_bounds__(kResidBlock) void k_resid_hist(Rows rows, int N, SolveState st, KParams kp) {
+__device__ __forceinline__ void resid_hist_body(const Rows& rows, int N, const SolveState& st, int nb) {
     if (*st.done) return;
     __shared__ unsigned h[kResidWin];
     for (int k = threadIdx.x; k < kResidWin / 4; k += kResidBlock) reinterpret_cast<uint4*>(h)[k] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    for (int i = blockIdx.x * kResidBlock + threadIdx.x; i < N; i += gridDim.x * kResidBlock) {
+    for (int i = blockIdx.x * kResidBlock + threadIdx.x; i < N; i += nb * kResidBlock) {
         double a[6], b, wt;
         double key = -1.0;
         if (rows.get(i, a, b, wt)) {
@@ -318,17 +323,18 @@ __device__ void final_block(const Rows& rows, int N, SolveState st, imls_iter_tr
 
 // Reduce rows strictly between the boundary bins; collect the boundary rows.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
+__device__ __forceinline__ void collect_body(const Rows& rows, int N, const SolveState& st, double* __restrict__ partial2,
+                                             int nb) {
     if (*st.done) return;
     __shared__ double red[(NT / 64) * kNormEq];
     // the histogram was read by k_find_bins: zero it for the next solve
-    for (int b = blockIdx.x * NT + threadIdx.x; b < kHistBins / 4; b += gridDim.x * NT)
+    for (int b = blockIdx.x * NT + threadIdx.x; b < kHistBins / 4; b += nb * NT)
         reinterpret_cast<uint4*>(st.hist)[b] = make_uint4(0u, 0u, 0u, 0u);
     if (blockIdx.x == 0) for (int b = threadIdx.x; b < kHistBins / 256; b += NT) st.coarse[b] = 0u;
     const int blo = st.sel[0], bhi = st.sel[1];
     double acc[kNormEq];
     for (int k = 0; k < kNormEq; ++k) acc[k] = 0.0;
-    for (int i = blockIdx.x * NT + threadIdx.x; i < N; i += gridDim.x * NT) {
+    for (int i = blockIdx.x * NT + threadIdx.x; i < N; i += nb * NT) {
         const double key = st.keys[i];
         if (key < 0) continue;
         const int bin = min(key_bin(key), kHistBins - 1);
@@ -366,9 +372,9 @@ __global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st,
 }
 
 constexpr int kFinalBlock = 256;
-__global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, SolveState st, imls_iter_trace* tr,
-                                                            const double* __restrict__ partial2, int nparts, KParams kp,
-                                                            int update_pose) {
+__device__ __forceinline__ void solve_final_body(const Rows& rows, int N, const SolveState& st, imls_iter_trace* tr,
+                                                 const double* __restrict__ partial2, int nparts, const KParams& kp,
+                                                 int update_pose) {
     if (*st.done) return;
     __shared__ unsigned long long ck[kCandCap];
     __shared__ unsigned cr[kCandCap];
@@ -397,9 +403,9 @@ __device__ unsigned long long g_dbg_solve[8];
 #else
 #define DBG_STAMP(k) do { } while (0)
 #endif
-__global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, const double* __restrict__ partial, int blocks,
-                                                            SolveState st, imls_iter_trace* tr, KParams kp, int weighted,
-                                                            int update_pose) {
+__device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const double* __restrict__ partial, int blocks,
+                                                 const SolveState& st, imls_iter_trace* tr, const KParams& kp,
+                                                 int weighted, int update_pose) {
     if (*st.done) return;
 #ifdef IMLS_DEBUG_WAVE_TRACE
     long long dbg_t = wall_clock64();
@@ -560,6 +566,80 @@ __global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, c
     DBG_STAMP(7);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Kernels: one frame (arguments by value) and batched (frame = tab[blockIdx.y], float rows from the
+// batched projection; blocks past the frame's own grid leave at once).  Both run the same bodies.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kCoarse) void k_find_bins(SolveState st) { find_bins_body(st); }
+__global__ __launch_bounds__(kResidBlock) void k_resid_hist(Rows rows, int N, SolveState st) {
+    resid_hist_body(rows, N, st, (int)gridDim.x);
+}
+template <int NT>
+__global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
+    collect_body<NT>(rows, N, st, partial2, (int)gridDim.x);
+}
+__global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, SolveState st, imls_iter_trace* tr,
+                                                            const double* __restrict__ partial2, int nparts, KParams kp,
+                                                            int update_pose) {
+    solve_final_body(rows, N, st, tr, partial2, nparts, kp, update_pose);
+}
+__global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, const double* __restrict__ partial, int blocks,
+                                                            SolveState st, imls_iter_trace* tr, KParams kp, int weighted,
+                                                            int update_pose) {
+    solve_small_body(rows, N, partial, blocks, st, tr, kp, weighted, update_pose);
+}
+
+// grid shapes of the chain, per frame (shared by the one-frame and the batched launches)
+__host__ __device__ __forceinline__ int resid_blocks_of(int N) {
+    const int b = (N + kResidBlock - 1) / kResidBlock;
+    return b < kResidBlocks ? b : kResidBlocks;
+}
+__host__ __device__ __forceinline__ int collect_blocks_of(int N) {
+    const int b = (N + kBlock * 4 - 1) / (kBlock * 4);
+    return b < 1 ? 1 : (b < kCollectBlocks ? b : kCollectBlocks);
+}
+__host__ __device__ __forceinline__ int pass1_blocks_of(int N) {   // project_blocks(N): wave slabs + fallback slabs
+    return (N + kPass1Block - 1) / kPass1Block + kPass1Fallback;
+}
+__device__ __forceinline__ Rows float_rows(const PairDev& A) {
+    return Rows{A.cs, A.cd, A.cn, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr};
+}
+
+__global__ __launch_bounds__(kSmallBlock) void k_solve_small_b(const PairDev* __restrict__ tab, KParams kp, int weighted,
+                                                              int it) {
+    const PairDev A = tab[blockIdx.y];
+    if (A.N > kSmallRows) return;
+    solve_small_body(float_rows(A), A.N, A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, weighted, 1);
+}
+__global__ __launch_bounds__(256) void k_solve_first_b(const PairDev* __restrict__ tab, KParams kp, int weighted, int it) {
+    const PairDev A = tab[blockIdx.y];
+    if (A.N <= kSmallRows) return;
+    solve_first_body(A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, weighted, 1);
+}
+__global__ __launch_bounds__(kResidBlock) void k_resid_hist_b(const PairDev* __restrict__ tab) {
+    const PairDev A = tab[blockIdx.y];
+    const int nb = resid_blocks_of(A.N);
+    if (A.N <= kSmallRows || (int)blockIdx.x >= nb) return;
+    resid_hist_body(float_rows(A), A.N, A.st, nb);
+}
+__global__ __launch_bounds__(kCoarse) void k_find_bins_b(const PairDev* __restrict__ tab) {
+    const PairDev A = tab[blockIdx.y];
+    if (A.N <= kSmallRows) return;
+    find_bins_body(A.st);
+}
+__global__ __launch_bounds__(kBlock) void k_collect_b(const PairDev* __restrict__ tab) {
+    const PairDev A = tab[blockIdx.y];
+    const int nb = collect_blocks_of(A.N);
+    if (A.N <= kSmallRows || (int)blockIdx.x >= nb) return;
+    collect_body<kBlock>(float_rows(A), A.N, A.st, A.st.partial2, nb);
+}
+__global__ __launch_bounds__(kFinalBlock) void k_solve_final_b(const PairDev* __restrict__ tab, KParams kp, int it) {
+    const PairDev A = tab[blockIdx.y];
+    if (A.N <= kSmallRows) return;
+    solve_final_body(float_rows(A), A.N, A.st, A.trace + it, A.st.partial2, collect_blocks_of(A.N), kp, 1);
+}
+
 }  // namespace
 
 int solve_blocks(int N) { return (N + kBlock - 1) / kBlock; }
@@ -586,8 +666,8 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
     }
     k_solve_first<<<1, 256, 0, s>>>(st.partial1, blocks1, st, tr, kp, weighted, update_pose);
     if (weighted) return;
-    k_resid_hist<<<std::min(kResidBlocks, (N + kResidBlock - 1) / kResidBlock), kResidBlock, 0, s>>>(rows, N, st, kp);
-    const int cb = std::max(1, std::min(kCollectBlocks, (N + kBlock * 4 - 1) / (kBlock * 4)));
+    k_resid_hist<<<resid_blocks_of(N), kResidBlock, 0, s>>>(rows, N, st);
+    const int cb = collect_blocks_of(N);
     k_find_bins<<<1, kCoarse, 0, s>>>(st);
     k_collect<kBlock><<<cb, kBlock, 0, s>>>(rows, N, st, st.partial2);
     k_solve_final<<<1, kFinalBlock, 0, s>>>(rows, N, st, tr, st.partial2, cb, kp, update_pose);
@@ -600,3 +680,24 @@ extern "C" int imls_debug_solve(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(imlsgpu::g_dbg_solve), 64) == hipSuccess ? 0 : -1;
 }
 #endif
+
+namespace imlsgpu {
+void launch_solve_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp, int it) {
+    if (npairs <= 0) return;
+    int maxN = 0;
+    bool any_small = false, any_large = false;
+    for (int k = 0; k < npairs; ++k) {
+        maxN = std::max(maxN, n_host[k]);
+        (n_host[k] <= kSmallRows ? any_small : any_large) = true;
+    }
+    const int weighted = kp.solve_method == IMLS_SOLVE_WEIGHTED_LS;
+    if (any_small) k_solve_small_b<<<dim3(1, npairs), kSmallBlock, 0, s>>>(tab, kp, weighted, it);
+    if (!any_large) return;
+    k_solve_first_b<<<dim3(1, npairs), 256, 0, s>>>(tab, kp, weighted, it);
+    if (weighted) return;
+    k_resid_hist_b<<<dim3(resid_blocks_of(maxN), npairs), kResidBlock, 0, s>>>(tab);
+    k_find_bins_b<<<dim3(1, npairs), kCoarse, 0, s>>>(tab);
+    k_collect_b<<<dim3(collect_blocks_of(maxN), npairs), kBlock, 0, s>>>(tab);
+    k_solve_final_b<<<dim3(1, npairs), kFinalBlock, 0, s>>>(tab, kp, it);
+}
+}  // namespace imlsgpu

@@ -47,6 +47,21 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
+_XYZ_OFF = POINT_DTYPE.fields["x"][1]
+_NRM_OFF = POINT_DTYPE.fields["normal_x"][1]
+
+
+def _cloud_args(cloud):
+    """(keep-alive array, xyz pointer, normal pointer, n, stride in floats) for the C ABI's strided
+    clouds: a contiguous PointXYZINormal array is passed in place (the reference's 48-byte PCL
+    record, stride 12: no host copy); anything else as a packed (N, 6) float32 array."""
+    if isinstance(cloud, np.ndarray) and cloud.dtype == POINT_DTYPE and cloud.flags.c_contiguous and cloud.ndim == 1:
+        base = cloud.ctypes.data
+        return cloud, C.c_void_p(base + _XYZ_OFF), C.c_void_p(base + _NRM_OFF), cloud.size, POINT_DTYPE.itemsize // 4
+    a = _as_xyzn(cloud)
+    return a, C.c_void_p(a.ctypes.data), C.c_void_p(a.ctypes.data + 12), a.shape[0], 6
+
+
 class ImlsContext:
     """RAII wrapper of one `imls_ctx` (one per host thread; not thread-safe, like the reference)."""
 
@@ -94,12 +109,14 @@ class ImlsContext:
         self._check(self.lib.imls_synchronize(self.ctx))
 
     # -- clouds ---------------------------------------------------------------------------------
-    def set_target(self, cloud) -> int:
-        a = _as_xyzn(cloud)
+    # count=False: the C call returns without waiting for the NaN-filtered count (the rest of the
+    # index build is deferred to the first use), so many contexts' uploads overlap; returns None.
+    def set_target(self, cloud, count: bool = True):
+        _keep, px, pn, m, stride = _cloud_args(cloud)
         n = C.c_size_t()
-        self._check(self.lib.imls_set_target(self.ctx, _ptr(a), C.c_void_p(a.ctypes.data + 12), a.shape[0], 6, C.byref(n)))
-        self.n_target = n.value
-        return n.value
+        self._check(self.lib.imls_set_target(self.ctx, px, pn, m, stride, C.byref(n) if count else None))
+        self.n_target = n.value if count else None
+        return self.n_target
 
     def set_target_tensors(self, tensors):
         """Tensor-voting input tensors of the last set_target's points: (n, 6) float32
@@ -112,47 +129,51 @@ class ImlsContext:
     def set_target_tensors_device(self, ten6_ptr: int, n: int):
         self._check(self.lib.imls_set_target_tensors_device(self.ctx, C.c_void_p(ten6_ptr), n))
 
-    def set_source(self, cloud):
-        a = _as_xyzn(cloud)
+    def set_source(self, cloud, count: bool = True):
+        """Returns the input index of every kept point (count=True) or None (deferred, see set_target)."""
+        _keep, px, pn, m, stride = _cloud_args(cloud)
+        if not count:
+            self._check(self.lib.imls_set_source(self.ctx, px, pn, m, stride, None, None))
+            self.n_source = None
+            return None
         n = C.c_size_t()
-        kept = np.zeros(a.shape[0], np.uint32)
-        self._check(self.lib.imls_set_source(self.ctx, _ptr(a), C.c_void_p(a.ctypes.data + 12), a.shape[0], 6,
-                                             C.byref(n), _ptr(kept)))
+        kept = np.zeros(m, np.uint32)
+        self._check(self.lib.imls_set_source(self.ctx, px, pn, m, stride, C.byref(n), _ptr(kept)))
         self.n_source = n.value
         return kept[: n.value]
 
-    def set_target_device(self, soa6_ptr: int, n: int) -> int:
+    def set_target_device(self, soa6_ptr: int, n: int, count: bool = True):
         k = C.c_size_t()
-        self._check(self.lib.imls_set_target_device(self.ctx, C.c_void_p(soa6_ptr), n, C.byref(k)))
-        self.n_target = k.value
-        return k.value
+        self._check(self.lib.imls_set_target_device(self.ctx, C.c_void_p(soa6_ptr), n, C.byref(k) if count else None))
+        self.n_target = k.value if count else None
+        return self.n_target
 
-    def set_source_device(self, soa6_ptr: int, n: int) -> int:
+    def set_source_device(self, soa6_ptr: int, n: int, count: bool = True):
         k = C.c_size_t()
-        self._check(self.lib.imls_set_source_device(self.ctx, C.c_void_p(soa6_ptr), n, C.byref(k)))
-        self.n_source = k.value
-        return k.value
+        self._check(self.lib.imls_set_source_device(self.ctx, C.c_void_p(soa6_ptr), n, C.byref(k) if count else None))
+        self.n_source = k.value if count else None
+        return self.n_source
 
     # -- map FIFO (accumulateTargetCloud, laser_odometry.cpp:116-136) ---------------------------
-    def map_push(self, cloud) -> int:
+    def map_push(self, cloud, count: bool = True):
         """accumulateTargetCloud(cloud, max_queue_size) + setTargetPointCloud(accumulatedTargetCloud):
         the scan joins the device-resident FIFO (only it crosses PCIe) and the index is rebuilt over
-        the FIFO's scans, oldest first.  Returns the map size after the NaN filter."""
-        a = _as_xyzn(cloud)
+        the FIFO's scans, oldest first.  Returns the map size after the NaN filter (count=True)."""
+        _keep, px, pn, m, stride = _cloud_args(cloud)
         n = C.c_size_t()
-        if a.shape[0] == 0:
-            self._check(self.lib.imls_map_push(self.ctx, None, None, 0, 6, C.byref(n)))
+        np_ = C.byref(n) if count else None
+        if m == 0:
+            self._check(self.lib.imls_map_push(self.ctx, None, None, 0, 6, np_))
         else:
-            self._check(self.lib.imls_map_push(self.ctx, _ptr(a), C.c_void_p(a.ctypes.data + 12), a.shape[0], 6,
-                                               C.byref(n)))
-        self.n_target = n.value
-        return n.value
+            self._check(self.lib.imls_map_push(self.ctx, px, pn, m, stride, np_))
+        self.n_target = n.value if count else None
+        return self.n_target
 
-    def map_push_device(self, soa6_ptr: int, n: int) -> int:
+    def map_push_device(self, soa6_ptr: int, n: int, count: bool = True):
         k = C.c_size_t()
-        self._check(self.lib.imls_map_push_device(self.ctx, C.c_void_p(soa6_ptr), n, C.byref(k)))
-        self.n_target = k.value
-        return k.value
+        self._check(self.lib.imls_map_push_device(self.ctx, C.c_void_p(soa6_ptr), n, C.byref(k) if count else None))
+        self.n_target = k.value if count else None
+        return self.n_target
 
     def map_clear(self):
         self._check(self.lib.imls_map_clear(self.ctx))
@@ -179,7 +200,7 @@ class ImlsContext:
 
     # -- matching / solving -------------------------------------------------------------------
     def project(self, pose=None):
-        N = max(self.n_source, 1)
+        N = max(self.n_source if self.n_source is not None else self.index_stats()["queries"], 1)
         pose = np.ascontiguousarray(np.eye(4) if pose is None else pose, dtype=np.float64).reshape(16)
         x = np.zeros((N, 3), np.float32); y = np.zeros((N, 3), np.float32); n = np.zeros((N, 3), np.float32)
         idx = np.zeros(N, np.uint32); rej = np.zeros(6, np.uint64); nv = C.c_size_t()
@@ -287,6 +308,42 @@ class ImlsContext:
         self._check(self.lib.imls_traversal_stats(self.ctx, _ptr(out)))
         keys = ("sum_kq", "nn_found", "leaves_visited", "inner_visited", "waves", "uncertified", "verlet_reused")
         return {k: int(v) for k, v in zip(keys, out)}
+
+
+def _ctx_array(contexts):
+    arr = (C.c_void_p * max(len(contexts), 1))()
+    for k, c in enumerate(contexts):
+        arr[k] = c.ctx
+    return arr
+
+
+def register_frames_async(contexts):
+    """Enqueue the frames loaded into `contexts` (set_target / map_push + set_source on each) as ONE
+    launch sequence (imls_register_frames_async): every per-iteration kernel runs once for all
+    frames.  Collect with register_frames_result(contexts)."""
+    if not contexts:
+        raise ValueError("no contexts")
+    lead = contexts[0]
+    lead._check(lead.lib.imls_register_frames_async(_ctx_array(contexts), len(contexts)))
+
+
+def register_frames_result(contexts):
+    """(poses (n,4,4), iterations (n,), statuses (n,), traces [n lists of ImlsIterTrace])."""
+    lead, n = contexts[0], len(contexts)
+    it = max(lead.params.iterations, 1)
+    poses = np.zeros((n, 16)); iters = np.zeros(n, np.int32); st = np.zeros(n, np.int32)
+    tr = (_abi.ImlsIterTrace * (it * n))()
+    lead._check(lead.lib.imls_register_frames_result(lead.ctx, _ptr(poses), _ptr(iters), _ptr(st), tr))
+    traces = [[tr[k * it + j] for j in range(int(iters[k]))] for k in range(n)]
+    for c, t in zip(contexts, traces):
+        c.last_trace = t
+    return poses.reshape(n, 4, 4), iters, st, traces
+
+
+def register_frames(contexts):
+    """imls_register_frames: register_frames_async + register_frames_result."""
+    register_frames_async(contexts)
+    return register_frames_result(contexts)
 
 
 # ================================================================================================

@@ -1,0 +1,199 @@
+"""GPU: imls_register_frames — the frames loaded into n contexts registered as ONE launch sequence
+(every per-iteration kernel once for all frames, grid y = frame; SURVEY §8(b) "many independent
+pairs per launch").  Frames are independent in the reference (rPose = I per frame against the raw
+previous scan(s), laser_odometry.cpp:484-485, 116-136), so the contract is strict: every frame's
+pose, iteration count, status and per-iteration trace must equal — bit for bit — what
+imls_register_frame gives on that frame alone, whatever else shares the launch (other sizes, other
+traversal / solver paths, frames that stop early)."""
+import numpy as np
+import pytest
+
+from planetary_lidar_odometry_amd import _abi, config, imls_icp, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(iters=8, shipped_convergence=True):
+    p = config.bench_params(iters)
+    if shipped_convergence:
+        p.delta_dist_threshold, p.delta_angle_threshold = 0.001, 0.0001745353
+    return p
+
+
+@pytest.fixture(scope="module")
+def vlp_pairs():
+    pairs = synth.make_pairs(4, "vlp16", map_scans=1, scene_seed=5, traj_seed=2005, noise_seed=1005)
+    return pairs
+
+
+@pytest.fixture(scope="module")
+def hdl_pair():
+    return synth.make_pairs(1, "hdl64", map_scans=1, scene_seed=6, traj_seed=2006, noise_seed=1006)[0]
+
+
+def _single(p, frames):
+    out = []
+    with imls_icp.ImlsContext(p) as c:
+        for src, tgt in frames:
+            c.set_target(tgt)
+            c.set_source(src)
+            out.append(c.register_frame())
+    return out
+
+
+def _batched(p, frames, repeat=1):
+    ctxs = [imls_icp.ImlsContext(p) for _ in frames]
+    try:
+        res = None
+        for _ in range(repeat):
+            for c, (src, tgt) in zip(ctxs, frames):
+                c.set_target(tgt)
+                c.set_source(src)
+            res = imls_icp.register_frames(ctxs)
+        return res
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def _trace_equal(a, b):
+    return (list(a.delta) == list(b.delta) and list(a.pose) == list(b.pose) and list(a.reject) == list(b.reject)
+            and a.n_valid == b.n_valid and a.n_kept == b.n_kept)
+
+
+def _check(p, frames, repeat=1):
+    ref = _single(p, frames)
+    poses, iters, status, traces = _batched(p, frames, repeat)
+    for k, r in enumerate(ref):
+        assert np.array_equal(r["pose"], poses[k]), (k, np.abs(r["pose"] - poses[k]).max())
+        assert (r["iters"], r["status"]) == (iters[k], status[k]), k
+        assert len(r["trace"]) == len(traces[k])
+        assert all(_trace_equal(a, b) for a, b in zip(r["trace"], traces[k])), k
+    return ref
+
+
+def test_small_frames_one_launch(vlp_pairs):
+    """≤ 2000-query frames (the config-C shape): wave-per-query traversal + one-block LS solve."""
+    frames = [(synth.fps_subsample(q.source, 1500 + 100 * k, seed=k), q.target) for k, q in enumerate(vlp_pairs)]
+    ref = _check(_params(), frames, repeat=2)
+    assert any(r["status"] == _abi.IMLS_FRAME_CONVERGED for r in ref)     # frames stop at their own iteration
+
+
+def test_mixed_paths_in_one_batch(vlp_pairs, hdl_pair):
+    """Every per-frame path shares the launch: packets (> 16384 queries) and wave-per-query
+    traversal, the grid LS chain (> 4096 rows) and the one-block solve."""
+    frames = [
+        (hdl_pair.source, hdl_pair.target),                                        # packets + chain
+        (synth.fps_subsample(vlp_pairs[0].source, 1200, seed=1), vlp_pairs[0].target),   # qwave + small
+        (vlp_pairs[1].source, vlp_pairs[1].target),                                # qwave + chain
+        (synth.fps_subsample(hdl_pair.source, 30000, seed=2), hdl_pair.target),    # packets + chain
+    ]
+    _check(_params(6), frames)
+
+
+def test_too_few_and_weighted_ls(vlp_pairs):
+    """A frame that stops at the correspondence gate (TOO_FEW) next to running frames; weighted LS."""
+    p = _params(5)
+    frames = [(synth.fps_subsample(vlp_pairs[2].source, 1500, seed=3), vlp_pairs[2].target),
+              (vlp_pairs[3].source[:12], vlp_pairs[3].target),
+              (synth.fps_subsample(vlp_pairs[3].source, 1800, seed=4), vlp_pairs[3].target)]
+    ref = _check(p, frames)
+    assert ref[1]["status"] == _abi.IMLS_FRAME_TOO_FEW
+    p.solve_method = _abi.IMLS_SOLVE_WEIGHTED_LS
+    _check(p, frames)
+
+
+def test_unfused_solver_runs_per_frame(vlp_pairs):
+    """The shipped RANSAC → DRPM solver keeps one launch sequence per frame inside the call (each
+    context continues its own rand() stream): results equal fresh single contexts'."""
+    p = config.params_from_config(config.load())
+    p.iterations = 3
+    frames = [(synth.fps_subsample(q.source, 1500, seed=k), q.target) for k, q in enumerate(vlp_pairs[:2])]
+    ref = []
+    for src, tgt in frames:           # a fresh context per frame = a fresh seeded rand() stream
+        ref += _single(p, [(src, tgt)])
+    poses, iters, status, _ = _batched(p, frames)
+    for k, r in enumerate(ref):
+        assert np.array_equal(r["pose"], poses[k]) and r["iters"] == iters[k] and r["status"] == status[k]
+
+
+def test_errors(vlp_pairs):
+    src, tgt = vlp_pairs[0].source, vlp_pairs[0].target
+    p, q = _params(3), _params(4)
+    with imls_icp.ImlsContext(p) as a, imls_icp.ImlsContext(q) as b, imls_icp.ImlsContext(p) as c:
+        for x in (a, b):
+            x.set_target(tgt)
+            x.set_source(src)
+        with pytest.raises(_abi.ImlsError, match="params"):
+            imls_icp.register_frames([a, b])
+        c.set_target(tgt)
+        with pytest.raises(_abi.ImlsError, match="set_source"):
+            imls_icp.register_frames([a, c])
+        with pytest.raises(_abi.ImlsError, match="twice"):
+            imls_icp.register_frames([a, a])
+        imls_icp.register_frames_async([a])
+        with pytest.raises(_abi.ImlsError, match="pending"):
+            a.register_frame_async()
+        poses, _, _, _ = imls_icp.register_frames_result([a])
+        assert np.all(np.isfinite(poses))
+        assert np.array_equal(poses[0], a.register_frame()["pose"])     # usable afterwards, same answer
+
+
+def test_plane_icp_frames(vlp_pairs):
+    """The plane_ICP matcher (NN-1 tangent plane, angle gate on) through the batched launch."""
+    p = _params(5)
+    p.matching_method = _abi.IMLS_MATCH_PLANE_ICP
+    p.picp_normal_angle_constraint = 1
+    frames = [(synth.fps_subsample(q.source, 1500, seed=k), q.target) for k, q in enumerate(vlp_pairs[:3])]
+    _check(p, frames)
+
+
+def test_deferred_builds_match_counted(vlp_pairs):
+    """set_target / set_source / map_push without a requested count return before the NaN filter's
+    count is known (the rest of the build runs at first use): same registration as the counted calls;
+    an all-NaN deferred target surfaces as the missing-target state error at first use."""
+    p = _params(6)
+    q = vlp_pairs[1]
+    src = synth.fps_subsample(q.source, 1600, seed=9)
+    with imls_icp.ImlsContext(p) as a, imls_icp.ImlsContext(p) as b:
+        a.set_target(q.target)
+        a.set_source(src)
+        ra = a.register_frame()
+        assert b.set_target(q.target, count=False) is None and b.set_source(src, count=False) is None
+        rb = b.register_frame()
+        assert np.array_equal(ra["pose"], rb["pose"]) and ra["iters"] == rb["iters"]
+        b.map_push(q.target, count=False)
+        b.set_source(src, count=False)
+        assert np.array_equal(b.register_frame()["pose"], ra["pose"])
+        x, y, n, idx, rej = b.project(np.eye(4))      # query count found without a counted set_source
+        assert len(idx) > 0
+        bad = np.array(q.target, copy=True)
+        bad["x"] = np.nan
+        b.set_target(bad, count=False)
+        with pytest.raises(_abi.ImlsError, match="set_target"):
+            b.register_frame()
+
+
+def test_two_batches_in_flight(vlp_pairs):
+    """Two disjoint batches in flight at once (the bench's double buffering): each equals its frames
+    registered alone."""
+    p = _params(6)
+    frames = [(synth.fps_subsample(q.source, 1400, seed=20 + k), q.target) for k, q in enumerate(vlp_pairs)]
+    ref = _single(p, frames)
+    ctxs = [imls_icp.ImlsContext(p) for _ in frames]
+    try:
+        for c, (src, tgt) in zip(ctxs[:2], frames[:2]):
+            c.set_target(tgt, count=False)
+            c.set_source(src, count=False)
+        imls_icp.register_frames_async(ctxs[:2])
+        for c, (src, tgt) in zip(ctxs[2:], frames[2:]):
+            c.set_target(tgt, count=False)
+            c.set_source(src, count=False)
+        imls_icp.register_frames_async(ctxs[2:])
+        p1 = imls_icp.register_frames_result(ctxs[:2])[0]
+        p2 = imls_icp.register_frames_result(ctxs[2:])[0]
+        for k, pose in enumerate(list(p1) + list(p2)):
+            assert np.array_equal(pose, ref[k]["pose"]), k
+    finally:
+        for c in ctxs:
+            c.close()
