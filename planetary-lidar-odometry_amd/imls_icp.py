@@ -27,6 +27,7 @@ import numpy as np
 
 from . import _abi
 from . import config as _config
+from . import wire as _wire
 from .synth import POINT_DTYPE
 
 
@@ -53,8 +54,16 @@ _NRM_OFF = POINT_DTYPE.fields["normal_x"][1]
 
 def _cloud_args(cloud):
     """(keep-alive array, xyz pointer, normal pointer, n, stride in floats) for the C ABI's strided
-    clouds: a contiguous PointXYZINormal array is passed in place (the reference's 48-byte PCL
-    record, stride 12: no host copy); anything else as a packed (N, 6) float32 array."""
+    clouds: a contiguous PointXYZINormal array — or a PointCloud2 message of one (wire.py: the
+    /laser_cloud_filtered, /laser_cloud_flat wire format) — is passed in place (the reference's
+    48-byte PCL record, stride 12: no host copy); anything else as a packed (N, 6) float32 array."""
+    if isinstance(cloud, _wire.PointCloud2):
+        sv = _wire.strided_view(cloud)
+        if sv is None:
+            cloud = _wire.xyzinormal_from_msg(cloud)
+        else:
+            buf, xo, no, n, stride = sv
+            return buf, C.c_void_p(buf.ctypes.data + xo), C.c_void_p(buf.ctypes.data + no), n, stride
     if isinstance(cloud, np.ndarray) and cloud.dtype == POINT_DTYPE and cloud.flags.c_contiguous and cloud.ndim == 1:
         base = cloud.ctypes.data
         return cloud, C.c_void_p(base + _XYZ_OFF), C.c_void_p(base + _NRM_OFF), cloud.size, POINT_DTYPE.itemsize // 4
