@@ -315,6 +315,30 @@ const char* imls_batch_last_error(const imls_batch* b);
 int imls_register_batch(imls_batch* b, size_t n_pairs, const imls_pair_input* pairs, double* poses_out,
                         int32_t* iters_out, int32_t* status_out);
 
+/* ---- upstream producer: front end (scan_registration.cpp:laserCloudHandler 809-1069) ---- */
+/* Node parameters (scan_registration.cpp:1575-1581; the shipped launch file
+ * planetary_slam_VLP_32.launch sets scan_line 64, minimum_range 2, maximum_range 150). */
+typedef struct imls_front_params {
+    int32_t n_scans;                /* scan_line: 16, 32 or 64 */
+    float minimum_range;            /* removeClosedPointCloud thresholds (m) */
+    float maximum_range;
+    float scan_period;              /* scanPeriod = 0.1 (55) */
+    int32_t is_dense;               /* the message's is_dense: pcl::removeNaNFromPointCloud copies a dense
+                                       cloud unchanged (NaN points then meet the range test) */
+} imls_front_params;
+void imls_default_front_params(imls_front_params* p);    /* the launch file's values, is_dense 0 */
+/* The raw sweep (pcl::PointXYZ records of the /velodyne_points message, in the driver's order:
+ * x, y, z at xyz + i·stride_floats) → laserCloud: the NaN filter (862), the range filter
+ * removeClosedPointCloud (87-115, 863), the ring assignment and relative time (898-1058), the
+ * rings concatenated in ring order, each in input order (1064-1069).  out_xyzi: [n][4] = x, y, z,
+ * intensity (= ring + scanPeriod·relTime, 1048); out_index (nullable): the input index of each
+ * output point; ring_sizes: [n_scans] points per ring (the ring_sizes imls_ring_normals_pca takes;
+ * scanStartInd / scanEndInd = prefix + 5 / prefix + size − 6, 1066-1068); *n_out = Σ ring sizes.
+ * Capacity of the outputs: n points.  A sweep with no surviving point gives n_out = 0 (the
+ * reference would index an empty cloud). */
+int imls_scan_front_end(imls_ctx* ctx, const imls_front_params* p, const float* xyz, size_t stride_floats,
+                        size_t n, float* out_xyzi, uint32_t* out_index, int32_t* ring_sizes, size_t* n_out);
+
 /* ---- upstream producer: ring-neighbourhood PCA normals (scan_registration) ------------- */
 /* scan_registration.compute_normal_method.pca + presample_method.geometric_features
  * (config.json; read at scan_registration.cpp:1140-1145, 1451, 1133).  imls_default_pca_params()
@@ -404,7 +428,8 @@ int imls_sample_point_cloud(imls_ctx* ctx, const imls_sample_params* p, const fl
  * launched on); imls_kernel_timing returns the accumulated milliseconds and launch count since
  * the last reset.  kernel: 0 = projection (all its kernels), 1 = index build (all its kernels),
  * 2 = solve chain, 3 = k_knn_wave (packet traversal) alone, 4 = k_finish (exact stage) alone,
- * 5 = k_ring_pca (imls_ring_normals_pca), 6 = k_major_avg (imls_sample_point_cloud, major_axis). */
+ * 5 = k_ring_pca (imls_ring_normals_pca), 6 = k_major_avg (imls_sample_point_cloud, major_axis),
+ * 7 = imls_scan_front_end (all its kernels). */
 int imls_enable_timing(imls_ctx* ctx, int enable);
 int imls_kernel_timing(imls_ctx* ctx, int kernel, double* total_ms, uint64_t* launches);
 int imls_reset_timing(imls_ctx* ctx);

@@ -58,6 +58,7 @@ def lib():
         L.oracle_sym_eig6.argtypes = [VP, VP, VP]
         L.oracle_sample_point_cloud.argtypes = [P(abi.ImlsSampleParams), VP, VP, SZ, SZ, VP, SZ, VP, SZ, SZ, VP,
                                                 P(SZ), VP]
+        L.oracle_scan_front_end.argtypes = [P(abi.ImlsFrontParams), VP, SZ, SZ, VP, VP, VP, P(SZ)]
         L.oracle_ring_pca.argtypes = [VP, SZ, VP, C.c_int32, P(abi.ImlsPcaParams), VP, VP, VP, VP, VP, VP, VP,
                                       P(SZ), VP]
         _lib = L
@@ -196,6 +197,19 @@ def delta_from_x(x):
     x = np.ascontiguousarray(x, dtype=np.float64); D = np.zeros(16)
     lib().oracle_delta_from_x(_ptr(x), _ptr(D))
     return D.reshape(4, 4)
+
+
+def scan_front_end(xyz, front_params):
+    """scan_registration.cpp front end (scanreg_oracle.cpp): (xyzi (m, 4), input index (m,), ring sizes)."""
+    a = np.ascontiguousarray(xyz, dtype=np.float32)
+    n = a.shape[0]
+    out = np.zeros((max(n, 1), 4), np.float32); idx = np.zeros(max(n, 1), np.uint32)
+    rs = np.zeros(64, np.int32); m = C.c_size_t()
+    rc = lib().oracle_scan_front_end(C.byref(front_params), _ptr(a), a.shape[1] if a.ndim == 2 else 3, n, _ptr(out),
+                                     _ptr(idx), _ptr(rs), C.byref(m))
+    assert rc == 0
+    k = m.value
+    return out[:k], idx[:k], rs[:front_params.n_scans]
 
 
 def ring_pca(xyz, ring_sizes, pca_params):

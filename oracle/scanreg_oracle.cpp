@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstddef>
 #include <cstdint>
+#include <limits>
 #include <random>
 #include <vector>
 
@@ -257,9 +258,106 @@ void sample_bin(const SampleCloud& c, const std::vector<int>& bin, int k, int st
     }
 }
 
+// static_cast<int>(double) as the reference's x86-64 build evaluates it (cvttsd2si): truncation,
+// INT_MIN for NaN / out of range (spelled out: the C++ cast is undefined there)
+inline int x86_d2i(double v) {
+    if (!(v > -2147483649.0 && v < 2147483648.0)) return INT32_MIN;
+    return (int)v;
+}
+
 }  // namespace
 
 extern "C" {
+
+// scan_registration.cpp:laserCloudHandler front end, line by line: pcl::removeNaNFromPointCloud
+// (862; a dense cloud is copied unchanged), removeClosedPointCloud (87-115, 863), startOri / endOri
+// (899-912), the per-point ring + azimuth loop with the sequential halfPassed switch (940-1058; the
+// std:: float overloads of sqrt / atan / atan2 = glibc sqrtf / atanf / atan2f), and laserCloud = the
+// rings concatenated (1064-1069).  Outputs as imls_scan_front_end.
+int oracle_scan_front_end(const imls_front_params* p, const float* xyz, size_t stride, size_t n, float* out_xyzi,
+                          uint32_t* out_index, int32_t* ring_sizes, size_t* n_out) {
+    const int NS = p->n_scans;
+    *n_out = 0;
+    if (NS != 16 && NS != 32 && NS != 64) return -1;
+    for (int r = 0; r < NS; ++r) ring_sizes[r] = 0;
+    struct Pt { float x, y, z; uint32_t i; };
+    std::vector<Pt> in;
+    for (size_t i = 0; i < n; ++i) {
+        const float* q = xyz + i * stride;
+        if (!p->is_dense && (!std::isfinite(q[0]) || !std::isfinite(q[1]) || !std::isfinite(q[2]))) continue;
+        in.push_back({q[0], q[1], q[2], (uint32_t)i});
+    }
+    std::vector<Pt> kept;
+    const float mn = p->minimum_range, mx = p->maximum_range;
+    for (const Pt& q : in) {
+        if (q.x * q.x + q.y * q.y + q.z * q.z < mn * mn || q.x * q.x + q.y * q.y + q.z * q.z > mx * mx) continue;
+        kept.push_back(q);
+    }
+    const int cloudSize = (int)kept.size();
+    if (cloudSize == 0) return 0;
+    float startOri = -std::atan2(kept[0].y, kept[0].x);
+    float endOri = -std::atan2(kept[cloudSize - 1].y, kept[cloudSize - 1].x) + 2 * M_PI;
+    if (endOri - startOri > 3 * M_PI) endOri -= 2 * M_PI;
+    else if (endOri - startOri < M_PI) endOri += 2 * M_PI;
+    bool halfPassed = false;
+    float upperBound = 0.f, lowerBound = 0.f;
+    if (NS == 32) { upperBound = 15.0f; lowerBound = -25.0f; }
+    else if (NS == 64) { upperBound = 2.0f; lowerBound = -24.33f; }
+    static const std::vector<float> scanAngles = {-25.000, -15.639, -11.310, -8.843, -7.254, -6.148, -5.333,
+                                                  -4.667,  -4.000,  -3.667,  -3.333, -3.000, -2.667, -2.333,
+                                                  -2.000,  -1.667,  -1.333,  -1.000, -0.667, -0.333, 0.000,
+                                                  0.333,   0.667,   1.000,   1.333,  1.667,  2.333};
+    const float scanPeriod = p->scan_period;
+    std::vector<std::vector<std::pair<Pt, float>>> scans(NS);
+    for (int i = 0; i < cloudSize; i++) {
+        Pt point = kept[i];
+        float range = std::sqrt(point.x * point.x + point.y * point.y);
+        float vertical_angle = std::atan(point.z / range);
+        float angle = vertical_angle * 180 / M_PI;
+        int scanID = 0;
+        if (NS == 16) {
+            scanID = x86_d2i((angle + 15) / 2 + 0.5);
+            if (scanID > (NS - 1) || scanID < 0) continue;
+        } else if (NS == 32) {
+            float min_diff = std::numeric_limits<float>::max();
+            for (size_t j = 0; j < scanAngles.size(); j++) {
+                float diff = std::abs(angle - scanAngles[j]);
+                if (diff < min_diff) { min_diff = diff; scanID = (int)j; }
+            }
+            if (scanID > (NS - 1) || scanID < 0) continue;
+        } else {
+            if (angle >= -8.83) scanID = x86_d2i((upperBound - angle) * 3.0 + 0.5);
+            else scanID = (int)((unsigned)(NS / 2) + (unsigned)x86_d2i((-8.83 - angle) * 2.0 + 0.5));
+            if (angle > upperBound || angle < lowerBound || scanID > 50 || scanID < 0) continue;
+        }
+        float ori = -std::atan2(point.y, point.x);
+        if (!halfPassed) {
+            if (ori < startOri - M_PI / 2) ori += 2 * M_PI;
+            else if (ori > startOri + M_PI * 3 / 2) ori -= 2 * M_PI;
+            if (ori - startOri > M_PI) halfPassed = true;
+        } else {
+            ori += 2 * M_PI;
+            if (ori < endOri - M_PI * 3 / 2) ori += 2 * M_PI;
+            else if (ori > endOri + M_PI / 2) ori -= 2 * M_PI;
+        }
+        float relTime = (ori - startOri) / (endOri - startOri);
+        float intensity = scanID + scanPeriod * relTime;
+        scans[scanID].push_back({point, intensity});
+    }
+    size_t k = 0;
+    for (int r = 0; r < NS; ++r) {
+        ring_sizes[r] = (int32_t)scans[r].size();
+        for (const auto& e : scans[r]) {
+            out_xyzi[4 * k] = e.first.x; out_xyzi[4 * k + 1] = e.first.y; out_xyzi[4 * k + 2] = e.first.z;
+            out_xyzi[4 * k + 3] = e.second;
+            if (out_index) out_index[k] = e.first.i;
+            ++k;
+        }
+    }
+    *n_out = k;
+    return 0;
+}
+
 
 // The "pca" branch of scan_registration.cpp:1136-1229 + computeGeometricFeatures (279-327) + the
 // invalid-index erase (1481-1489).  Same outputs as imls_ring_normals_pca (include/imls_gpu.h), plus

@@ -24,7 +24,7 @@ IMLS_NUM_REJ = 6
 STATUS_NAMES = {0: "IMLS_OK", -1: "IMLS_ERR_ARG", -2: "IMLS_ERR_DEVICE", -3: "IMLS_ERR_STATE",
                 -4: "IMLS_ERR_UNSUPPORTED", -5: "IMLS_ERR_CAPACITY"}
 
-_i32, _u32, _f64 = C.c_int32, C.c_uint32, C.c_double
+_i32, _u32, _f64, _f32 = C.c_int32, C.c_uint32, C.c_double, C.c_float
 
 
 class ImlsParams(C.Structure):
@@ -86,6 +86,19 @@ def default_params() -> ImlsParams:
     p.drpm_threshold, p.drpm_stdev_points, p.drpm_stdev_normals = 0.05, 0.02, 0.05
     p.ransac_seed = 1
     p.transform_normal, p.max_queue_size = 0, 1
+    return p
+
+
+class ImlsFrontParams(C.Structure):
+    _fields_ = [("n_scans", _i32), ("minimum_range", _f32), ("maximum_range", _f32), ("scan_period", _f32),
+                ("is_dense", _i32)]
+
+
+def default_front_params(n_scans: int | None = None) -> "ImlsFrontParams":
+    p = ImlsFrontParams()
+    load_library().imls_default_front_params(C.byref(p))
+    if n_scans is not None:
+        p.n_scans = n_scans
     return p
 
 
@@ -175,6 +188,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_index_stats": (C.c_int, [VP, VP]),
         "imls_traversal_stats": (C.c_int, [VP, VP]),
         "imls_default_pca_params": (None, [P(ImlsPcaParams)]),
+        "imls_default_front_params": (None, [P(ImlsFrontParams)]),
+        "imls_scan_front_end": (C.c_int, [VP, P(ImlsFrontParams), VP, SZ, SZ, VP, VP, VP, P(SZ)]),
         "imls_ring_normals_pca": (C.c_int, [VP, P(ImlsPcaParams), VP, SZ, VP, C.c_int32, VP, VP, VP, VP, VP, VP,
                                             P(SZ), VP]),
         "imls_default_sample_params": (None, [P(ImlsSampleParams), C.c_int32]),
@@ -214,6 +229,7 @@ ABI_SYMBOLS = (
     "imls_batch_last_error", "imls_register_batch", "imls_seed_rng", "imls_get_rng_state",
     "imls_set_rng_state", "imls_map_push", "imls_map_push_device", "imls_map_clear", "imls_map_size",
     "imls_register_frames", "imls_register_frames_async", "imls_register_frames_result",
+    "imls_default_front_params", "imls_scan_front_end",
 )
 
 _LIB = None

@@ -16,7 +16,7 @@
 
 using namespace imlsgpu;
 
-constexpr int kTimingKinds = 7;   // projection, index, solve chain, k_knn_wave, k_finish, k_ring_pca, k_major_avg
+constexpr int kTimingKinds = 8;   // projection, index, solve chain, k_knn_wave, k_finish, k_ring_pca, k_major_avg, front end
 
 struct imls_ctx {
     int device = 0;
@@ -50,6 +50,7 @@ struct imls_ctx {
     DevBuf tvn;                           // tensor voting: per-source voted normal + found flag (double4)
     DevBuf pca_mem;                       // imls_ring_normals_pca scratch (upstream producer)
     DevBuf sample_mem;                    // imls_sample_point_cloud scratch
+    DevBuf front_mem;                     // imls_scan_front_end scratch
     size_t n_target_in = 0;               // input size of the last set_target (tensor arrays match it)
     bool has_tensors = false;
     int lane_mode = 0;
@@ -642,7 +643,7 @@ void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->sample_mem, &c->pca_mem, &c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
+    DevBuf* bufs[] = {&c->front_mem, &c->sample_mem, &c->pca_mem, &c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
                       &c->upload_t, &c->spt, &c->snr, &c->sscratch,
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
@@ -1349,6 +1350,28 @@ int imls_register_batch(imls_batch* b, size_t n_pairs, const imls_pair_input* pa
         }
     }
     return IMLS_OK;
+}
+
+void imls_default_front_params(imls_front_params* p) {
+    if (!p) return;
+    p->n_scans = 64;            // planetary_slam_VLP_32.launch: scan_line 64, minimum_range 2, maximum_range 150
+    p->minimum_range = 2.0f;
+    p->maximum_range = 150.0f;
+    p->scan_period = 0.1f;      // scan_registration.cpp:55
+    p->is_dense = 0;
+}
+
+int imls_scan_front_end(imls_ctx* c, const imls_front_params* p, const float* xyz, size_t stride_floats, size_t n,
+                        float* out_xyzi, uint32_t* out_index, int32_t* ring_sizes, size_t* n_out) {
+    if (!c || !p || !out_xyzi || !ring_sizes || !n_out || (n > 0 && !xyz)) return IMLS_ERR_ARG;
+    if (int rc = check_device(c)) return rc;
+    int slot;
+    timed_begin(c, 7, slot);
+    const int rc = front_end_run(c->stream, *p, xyz, stride_floats, n, c->front_mem, out_xyzi, out_index, ring_sizes,
+                                 n_out, c->err);
+    timed_end(c, 7, slot);
+    harvest_timing(c);
+    return rc;
 }
 
 void imls_default_pca_params(imls_pca_params* p) {

@@ -234,6 +234,11 @@ int ring_pca_run(hipStream_t s, const imls_pca_params& p, const float* xyz, size
                  float* evals_out, float* evecs_out, float* features_out, uint8_t* flags_out, size_t* n_out,
                  uint64_t counters[2], std::string& err);
 
+// front.hip — scan front end: NaN + range filter, ring assignment, relative time (imls_scan_front_end)
+int front_end_run(hipStream_t s, const imls_front_params& p, const float* xyz_host, size_t stride, size_t n_in,
+                  DevBuf& mem, float* out_xyzi, uint32_t* out_index, int32_t* ring_sizes, size_t* n_out,
+                  std::string& err);
+
 // sample.hip — samplePointCloud "normal" / "major_axis" (imls_sample_point_cloud)
 int sample_run(hipStream_t s, const imls_sample_params& p, const float* xyz, const float* nrm, size_t stride, size_t n,
                const int32_t* cand, size_t n_cand, const float* last_xyz, size_t last_stride, size_t m, DevBuf& mem,

@@ -250,6 +250,22 @@ class ImlsContext:
         return pose.reshape(4, 4), iters.value, status.value
 
     # -- instrumentation ------------------------------------------------------------------------
+    def scan_front_end(self, xyz, front_params: Optional[_abi.ImlsFrontParams] = None):
+        """laserCloudHandler's front end (scan_registration.cpp:862-1069) on a raw sweep (n, 3+)
+        float32 in the driver's order: NaN + range filter, ring assignment, relative time.  Returns
+        (xyz (m, 3), intensity (m,), input index (m,), ring sizes) — laserCloud, ring-concatenated."""
+        a = np.ascontiguousarray(xyz, dtype=np.float32)
+        if a.ndim != 2 or a.shape[1] < 3:
+            raise ValueError("xyz must be (n, >=3)")
+        p = front_params if front_params is not None else _abi.default_front_params()
+        n = a.shape[0]
+        out = np.zeros((max(n, 1), 4), np.float32); idx = np.zeros(max(n, 1), np.uint32)
+        rs = np.zeros(max(p.n_scans, 1), np.int32); m = C.c_size_t()
+        self._check(self.lib.imls_scan_front_end(self.ctx, C.byref(p), _ptr(a), a.shape[1], n, _ptr(out), _ptr(idx),
+                                                 _ptr(rs), C.byref(m)))
+        k = m.value
+        return out[:k, :3], out[:k, 3], idx[:k], rs[:p.n_scans]
+
     def ring_normals_pca(self, xyz, ring_sizes, pca_params: Optional[_abi.ImlsPcaParams] = None) -> dict:
         """scan_registration.cpp's "pca" normal estimation + geometric-features presample (1136-1229,
         279-327, 1481-1489) on the ring-concatenated cloud `laserCloud` (1064-1069).

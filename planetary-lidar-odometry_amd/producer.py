@@ -2,6 +2,8 @@
 shipped config (config.json scan_registration: compute_normal_method "pca" → presample_method
 "geometric_features" → sample_method "major_axis"), on the GPU through the C ABI.
 
+  ScanRegistration.process_raw(raw) the whole handler: scan_front_end (NaN / range filter, ring
+                                    assignment and relative time, 862-1069) → process
   ScanRegistration.process(sweep)   laserCloudHandler's tail (scan_registration.cpp:1136-1229 normals,
                                     1448-1461 + 1481-1489 presample, 1494-1503 sampling) → the two
                                     clouds laser_odometry consumes: pcl_cloud (/laser_cloud_filtered,
@@ -49,6 +51,12 @@ class ScanRegistration:
         sp.shuffle_seed = (self.shuffle_seed + 7919 * self.frame) & 0xFFFFFFFF
         sp.rand_seed = (self.rand_seed + self.frame - 1) & 0xFFFFFFFF
         return sp
+
+    def process_raw(self, raw_xyz, front_params: Optional[_abi.ImlsFrontParams] = None):
+        """The whole laserCloudHandler on a raw sweep (driver order, (n, 3+) float32): the front end
+        (NaN / range filter, ring assignment, relative time; 862-1069) then process()."""
+        xyz, inten, _, sizes = self.ctx.scan_front_end(raw_xyz, front_params)
+        return self.process(xyz, sizes, inten)
 
     def process(self, xyz, ring_sizes, intensity=None):
         """One sweep → (pcl_cloud, pcl_surface_cloud) as POINT_DTYPE arrays (48-byte

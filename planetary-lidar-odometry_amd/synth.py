@@ -273,9 +273,29 @@ def trajectory(n: int, seed: int = 2000, step: float = 1.0, yaw_step_deg: float 
 # --------------------------------------------------------------------------------------------
 # Scans
 # --------------------------------------------------------------------------------------------
-def scan(scene: Scene, model: ScanModel, pose: np.ndarray, seed: int) -> np.ndarray:
+def raw_sweep(scene: Scene, model: ScanModel, pose: np.ndarray, seed: int, start_deg: float = 0.0,
+              n_nan: int = 0, n_close: int = 0) -> np.ndarray:
+    """The same sweep as a lidar driver emits it (what scan_registration's front end receives):
+    (n, 3) float32 x y z in firing order — azimuth-major (clockwise), every ring at each step — starting at
+    azimuth `start_deg`; optionally `n_nan` NaN returns and `n_close` returns inside 0.3 m spread in."""
+    cloud, flat = scan(scene, model, pose, seed, return_index=True)
+    n_az = len(np.arange(0.0, 360.0, model.azimuth_step_deg))
+    ring, az = flat // n_az, flat % n_az
+    az0 = int(round(start_deg / model.azimuth_step_deg)) % n_az
+    order = np.lexsort((ring, (az0 - az) % n_az))      # clockwise (Velodyne): −atan2(y, x) increases
+    xyz = np.stack([cloud["x"], cloud["y"], cloud["z"]], 1)[order].astype(np.float32)
+    rng = np.random.default_rng(seed + 17)
+    for k in range(n_nan + n_close):
+        at = int(rng.integers(0, len(xyz) + 1))
+        pt = np.full((1, 3), np.nan, np.float32) if k < n_nan else (rng.normal(0, 0.1, (1, 3))).astype(np.float32)
+        xyz = np.concatenate([xyz[:at], pt, xyz[at:]])
+    return xyz
+
+
+def scan(scene: Scene, model: ScanModel, pose: np.ndarray, seed: int, return_index: bool = False):
     """One sweep from sensor pose (4×4 world←sensor), returned in the SENSOR frame as a
-    POINT_DTYPE array in ring-major order (like the reference's scan-ring ordering)."""
+    POINT_DTYPE array in ring-major order (like the reference's scan-ring ordering).  return_index:
+    also the flat (ring·n_azimuth + azimuth) index of every returned point."""
     rng = np.random.default_rng(seed)
     el = np.radians(model.rings)
     az = np.radians(np.arange(0.0, 360.0, model.azimuth_step_deg))
@@ -299,6 +319,8 @@ def scan(scene: Scene, model: ScanModel, pose: np.ndarray, seed: int) -> np.ndar
     out["x"], out["y"], out["z"] = p[:, 0], p[:, 1], p[:, 2]
     out["normal_x"], out["normal_y"], out["normal_z"] = nl[:, 0], nl[:, 1], nl[:, 2]
     out["intensity"] = ring[ok] + 0.1 * rel_t[ok]   # scanID + 0.1·relTime (scan_registration.cpp:1042)
+    if return_index:
+        return out, np.nonzero(ok)[0]
     return out
 
 
