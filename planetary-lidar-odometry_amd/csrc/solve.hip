@@ -12,9 +12,12 @@
 // bits of its float image (monotone), the two boundary bins are collected and sorted by
 // (|r| bits, row) in LDS, everything strictly between them is reduced directly.
 //
-// Launch chain per LS solve: k_solve_first (1 block) → k_resid_hist → k_find_bins (1 block) →
-// k_collect (also re-zeroes the histogram) → k_solve_final (1 block).  Every kernel returns at
-// once when the frame's `done` flag is set.  (A "last block finishes the reduction" fusion was
+// Launch chain per LS solve: k_resid_fused (every block reduces the pass-1 slabs and solves the
+// first 6×6 itself — deterministic, so all agree — then |r| keys + histogram) → k_collect (every
+// block locates the two boundary bins itself, then reduces the interior rows and collects the
+// boundary ones) → k_solve_final (1 block; re-zeroes the histogram).  Three launches instead of
+// five; weighted LS is k_solve_first alone.  Every kernel returns at once when the frame's `done`
+// flag is set.  (A "last block finishes the reduction" fusion was
 // measured slower on MI355X: each block's agent-scope release fence writes back its XCD's L2.)
 #include <algorithm>
 #include <cfloat>
@@ -90,10 +93,10 @@ __device__ unsigned block_exscan(unsigned v, unsigned* wsum, unsigned* all) {
 
 // Locate the bins holding ranks `lower` and `upper` (st.sel[4..5]) → st.sel[0..3]: a scan of the
 // 256 coarse bins (256 fine bins each) finds the coarse bin of each rank, a scan of that coarse
-// bin's fine bins the fine one.  One block of kCoarse threads; k_collect re-zeroes both levels.
+// bin's fine bins the fine one.  One block of kCoarse threads (every k_collect block runs it).
 constexpr int kCoarse = kHistBins / 256;
-__device__ __forceinline__ void find_bins_body(const SolveState& st) {
-    if (*st.done) return;
+// sel_out (LDS, nullable): the four values also land there, for the block that found them
+__device__ __forceinline__ void find_bins_core(const SolveState& st, int* sel_out) {
     __shared__ unsigned wsum[kCoarse / 64];
     __shared__ int cb[2];
     __shared__ unsigned cbase[2];
@@ -106,8 +109,8 @@ __device__ __forceinline__ void find_bins_body(const SolveState& st) {
     for (int w = 0; w < 2; ++w)
         if (rank[w] >= (long long)ex && rank[w] < (long long)ex + c) { cb[w] = t; cbase[w] = ex; }
     if (t == 0) {
-        if (rank[0] >= (long long)all) { st.sel[0] = -1; st.sel[2] = 0; cb[0] = -1; }   // N = 0
-        if (rank[1] >= (long long)all) { st.sel[1] = -1; st.sel[3] = 0; cb[1] = -1; }
+        if (rank[0] >= (long long)all) { st.sel[0] = -1; st.sel[2] = 0; cb[0] = -1; if (sel_out) { sel_out[0] = -1; sel_out[2] = 0; } }   // N = 0
+        if (rank[1] >= (long long)all) { st.sel[1] = -1; st.sel[3] = 0; cb[1] = -1; if (sel_out) { sel_out[1] = -1; sel_out[3] = 0; } }
     }
     __syncthreads();
 #pragma unroll
@@ -120,8 +123,10 @@ __device__ __forceinline__ void find_bins_body(const SolveState& st) {
         if (rank[w] >= (long long)fex && rank[w] < (long long)fex + f) {
             st.sel[w] = cw * 256 + t;
             st.sel[2 + w] = (int)fex;
+            if (sel_out) { sel_out[w] = cw * 256 + t; sel_out[2 + w] = (int)fex; }
         }
     }
+    __syncthreads();
 }
 
 // |r| under the first solution (solver.cpp:110) and its histogram.  Each block privatises the
@@ -132,8 +137,7 @@ constexpr int kResidBlock = 1024;
 constexpr int kResidBlocks = 96;
 constexpr int kResidWin = 16384;                          // 128 octaves of 1/128-octave bins
 constexpr int kResidWinLo = (0x1F800000 >> 15);           // key_bin(2^-64)
-__device__ __forceinline__ void resid_hist_body(const Rows& rows, int N, const SolveState& st, int nb) {
-    if (*st.done) return;
+__device__ __forceinline__ void resid_hist_core(const Rows& rows, int N, const SolveState& st, int nb, const double* x0) {
     __shared__ unsigned h[kResidWin];
     for (int k = threadIdx.x; k < kResidWin / 4; k += kResidBlock) reinterpret_cast<uint4*>(h)[k] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
@@ -141,8 +145,8 @@ __device__ __forceinline__ void resid_hist_body(const Rows& rows, int N, const S
         double a[6], b, wt;
         double key = -1.0;
         if (rows.get(i, a, b, wt)) {
-            double v = a[0] * st.x0[0];
-            for (int k = 1; k < 6; ++k) v = v + a[k] * st.x0[k];
+            double v = a[0] * x0[0];
+            for (int k = 1; k < 6; ++k) v = v + a[k] * x0[k];
             key = fabs(v - b);
             const int bin = min(key_bin(key), kHistBins - 1);
             const unsigned w = (unsigned)(bin - kResidWinLo);
@@ -172,6 +176,67 @@ __device__ __forceinline__ void resid_hist_body(const Rows& rows, int N, const S
     }
     __syncthreads();
     if (threadIdx.x < kResidWin / 256 && csh[threadIdx.x]) atomicAdd(&st.coarse[(kResidWinLo >> 8) + threadIdx.x], csh[threadIdx.x]);
+}
+
+// The first LS solve, by EVERY block of the residual pass (deterministic: all blocks get the same
+// x0, so k_solve_first's launch and its round trip disappear): reduce the pass-1 slabs, the
+// too-few / no-row gates (laser_odometry.cpp:570-576; solver.cpp:118-134, Q11), solve6, the trim
+// ranks.  Thread 0 of every block writes the same global results (x0, sel[4..6], status / done,
+// the trace count, the candidate counters); xs / *go (LDS) give the block x0 and whether to go on.
+template <int NT>
+__device__ void first_solve_shared(const double* __restrict__ partial, int blocks, const SolveState& st,
+                                   imls_iter_trace* tr, const KParams& kp, int update_pose, double* red, double* acc,
+                                   double* xs, int* go) {
+    const int t = threadIdx.x;
+    double loc[kNormEq];
+#pragma unroll
+    for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
+    for (int b = t; b < blocks; b += NT)
+#pragma unroll
+        for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
+    block_sum28<NT>(loc, red, acc);
+    if (t == 0) {
+        *go = 0;
+        st.cand_count[0] = 0u;
+        st.cand_count[1] = 0u;
+        const double nvalid = acc[27];
+        if (update_pose && nvalid < (double)kp.correspond_number) {
+            *st.status = IMLS_FRAME_TOO_FEW;
+            *st.done = 1;
+            if (tr) tr->n_valid = (unsigned long long)nvalid;
+        } else {
+            double x[6];
+            solve6(acc, x);
+            const long long Nv = (long long)nvalid;
+            const long long lo = (long long)(kp.ls_threshold * (double)Nv);
+            long long hi = (long long)((1 - kp.ls_threshold) * (double)Nv);
+            if (hi > Nv - 1) hi = Nv - 1;
+            if (Nv == 0 || lo > hi) {
+                *st.status = IMLS_FRAME_SOLVE_FAILED;
+                *st.done = 1;
+            } else {
+                for (int k = 0; k < 6; ++k) { st.x0[k] = x[k]; xs[k] = x[k]; }
+                st.sel[4] = (int)lo;
+                st.sel[5] = (int)hi;
+                st.sel[6] = (int)Nv;
+                *go = 1;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void resid_fused_body(const Rows& rows, int N, const double* __restrict__ partial, int blocks,
+                                                 const SolveState& st, imls_iter_trace* tr, const KParams& kp,
+                                                 int update_pose, int nb) {
+    if (*st.done) return;
+    __shared__ double red[(kResidBlock / 64) * kNormEq];
+    __shared__ double acc[kNormEq];
+    __shared__ double xs[8];
+    __shared__ int go;
+    first_solve_shared<kResidBlock>(partial, blocks, st, tr, kp, update_pose, red, acc, xs, &go);
+    if (!go) return;                      // block-uniform
+    resid_hist_core(rows, N, st, nb, xs);
 }
 
 // bitonic sort of n (power of two ≤ kCandCap) (key, row) pairs in LDS, ascending
@@ -322,16 +387,17 @@ __device__ void final_block(const Rows& rows, int N, SolveState st, imls_iter_tr
 }
 
 // Reduce rows strictly between the boundary bins; collect the boundary rows.
+// The boundary bins, found by EVERY block (k_find_bins' scans, redundantly: no launch between the
+// histogram and the collection); the histogram is re-zeroed by k_solve_final.
 template <int NT>
 __device__ __forceinline__ void collect_body(const Rows& rows, int N, const SolveState& st, double* __restrict__ partial2,
                                              int nb) {
+    static_assert(NT == kCoarse, "one thread per coarse bin");
     if (*st.done) return;
     __shared__ double red[(NT / 64) * kNormEq];
-    // the histogram was read by k_find_bins: zero it for the next solve
-    for (int b = blockIdx.x * NT + threadIdx.x; b < kHistBins / 4; b += nb * NT)
-        reinterpret_cast<uint4*>(st.hist)[b] = make_uint4(0u, 0u, 0u, 0u);
-    if (blockIdx.x == 0) for (int b = threadIdx.x; b < kHistBins / 256; b += NT) st.coarse[b] = 0u;
-    const int blo = st.sel[0], bhi = st.sel[1];
+    __shared__ int sel[4];
+    find_bins_core(st, sel);
+    const int blo = sel[0], bhi = sel[1];
     double acc[kNormEq];
     for (int k = 0; k < kNormEq; ++k) acc[k] = 0.0;
     for (int i = blockIdx.x * NT + threadIdx.x; i < N; i += nb * NT) {
@@ -376,6 +442,9 @@ __device__ __forceinline__ void solve_final_body(const Rows& rows, int N, const 
                                                  const double* __restrict__ partial2, int nparts, const KParams& kp,
                                                  int update_pose) {
     if (*st.done) return;
+    // the histogram was read by k_collect: zero it for the next solve
+    for (int b = threadIdx.x; b < kHistBins / 4; b += kFinalBlock) reinterpret_cast<uint4*>(st.hist)[b] = make_uint4(0u, 0u, 0u, 0u);
+    for (int b = threadIdx.x; b < kHistBins / 256; b += kFinalBlock) st.coarse[b] = 0u;
     __shared__ unsigned long long ck[kCandCap];
     __shared__ unsigned cr[kCandCap];
     __shared__ double red[(kFinalBlock / 64) * kNormEq];
@@ -571,9 +640,10 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
 // Kernels: one frame (arguments by value) and batched (frame = tab[blockIdx.y], float rows from the
 // batched projection; blocks past the frame's own grid leave at once).  Both run the same bodies.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kCoarse) void k_find_bins(SolveState st) { find_bins_body(st); }
-__global__ __launch_bounds__(kResidBlock) void k_resid_hist(Rows rows, int N, SolveState st) {
-    resid_hist_body(rows, N, st, (int)gridDim.x);
+__global__ __launch_bounds__(kResidBlock) void k_resid_fused(Rows rows, int N, const double* __restrict__ partial,
+                                                             int blocks, SolveState st, imls_iter_trace* tr, KParams kp,
+                                                             int update_pose) {
+    resid_fused_body(rows, N, partial, blocks, st, tr, kp, update_pose, (int)gridDim.x);
 }
 template <int NT>
 __global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
@@ -617,16 +687,11 @@ __global__ __launch_bounds__(256) void k_solve_first_b(const PairDev* __restrict
     if (A.N <= kSmallRows) return;
     solve_first_body(A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, weighted, 1);
 }
-__global__ __launch_bounds__(kResidBlock) void k_resid_hist_b(const PairDev* __restrict__ tab) {
+__global__ __launch_bounds__(kResidBlock) void k_resid_fused_b(const PairDev* __restrict__ tab, KParams kp, int it) {
     const PairDev A = tab[blockIdx.y];
     const int nb = resid_blocks_of(A.N);
     if (A.N <= kSmallRows || (int)blockIdx.x >= nb) return;
-    resid_hist_body(float_rows(A), A.N, A.st, nb);
-}
-__global__ __launch_bounds__(kCoarse) void k_find_bins_b(const PairDev* __restrict__ tab) {
-    const PairDev A = tab[blockIdx.y];
-    if (A.N <= kSmallRows) return;
-    find_bins_body(A.st);
+    resid_fused_body(float_rows(A), A.N, A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, 1, nb);
 }
 __global__ __launch_bounds__(kBlock) void k_collect_b(const PairDev* __restrict__ tab) {
     const PairDev A = tab[blockIdx.y];
@@ -664,11 +729,12 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
         k_solve_small<<<1, kSmallBlock, 0, s>>>(rows, N, st.partial1, blocks1, st, tr, kp, weighted, update_pose);
         return;
     }
-    k_solve_first<<<1, 256, 0, s>>>(st.partial1, blocks1, st, tr, kp, weighted, update_pose);
-    if (weighted) return;
-    k_resid_hist<<<resid_blocks_of(N), kResidBlock, 0, s>>>(rows, N, st);
+    if (weighted) {
+        k_solve_first<<<1, 256, 0, s>>>(st.partial1, blocks1, st, tr, kp, weighted, update_pose);
+        return;
+    }
+    k_resid_fused<<<resid_blocks_of(N), kResidBlock, 0, s>>>(rows, N, st.partial1, blocks1, st, tr, kp, update_pose);
     const int cb = collect_blocks_of(N);
-    k_find_bins<<<1, kCoarse, 0, s>>>(st);
     k_collect<kBlock><<<cb, kBlock, 0, s>>>(rows, N, st, st.partial2);
     k_solve_final<<<1, kFinalBlock, 0, s>>>(rows, N, st, tr, st.partial2, cb, kp, update_pose);
 }
@@ -693,10 +759,11 @@ void launch_solve_batch(hipStream_t s, const PairDev* tab, const int* n_host, in
     const int weighted = kp.solve_method == IMLS_SOLVE_WEIGHTED_LS;
     if (any_small) k_solve_small_b<<<dim3(1, npairs), kSmallBlock, 0, s>>>(tab, kp, weighted, it);
     if (!any_large) return;
-    k_solve_first_b<<<dim3(1, npairs), 256, 0, s>>>(tab, kp, weighted, it);
-    if (weighted) return;
-    k_resid_hist_b<<<dim3(resid_blocks_of(maxN), npairs), kResidBlock, 0, s>>>(tab);
-    k_find_bins_b<<<dim3(1, npairs), kCoarse, 0, s>>>(tab);
+    if (weighted) {
+        k_solve_first_b<<<dim3(1, npairs), 256, 0, s>>>(tab, kp, weighted, it);
+        return;
+    }
+    k_resid_fused_b<<<dim3(resid_blocks_of(maxN), npairs), kResidBlock, 0, s>>>(tab, kp, it);
     k_collect_b<<<dim3(collect_blocks_of(maxN), npairs), kBlock, 0, s>>>(tab);
     k_solve_final_b<<<dim3(1, npairs), kFinalBlock, 0, s>>>(tab, kp, it);
 }
