@@ -538,10 +538,12 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     // the seed search's leaf: its first ~10 bisection steps run in a coarse table of every S-th
     // leaf key staged in LDS (one coalesced block load), the last ⌈log2 S⌉ in HBM/L2 — instead of
     // ~15 dependent global loads per lane (measured: the seed pass was ~half of iterations 0-2)
+    // (first ICP iteration only, where every lane seeds: later iterations reseed a few lanes, which
+    // would not repay the block barrier)
     __shared__ unsigned long long skey[kSeedTab];
-    const int S = (t.L + kSeedTab - 1) / kSeedTab;
+    const int S = use_prev ? t.L : (t.L + kSeedTab - 1) / kSeedTab;
     const int ntab = S > 0 ? (t.L + S - 1) / S : 0;
-    if (__syncthreads_or(greedy)) {
+    if (!use_prev) {
         for (int k = threadIdx.x; k < ntab; k += kWaveBlock) skey[k] = t.lkeys[(size_t)k * S];
         __syncthreads();
     }

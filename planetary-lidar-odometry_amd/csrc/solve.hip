@@ -12,12 +12,12 @@
 // bits of its float image (monotone), the two boundary bins are collected and sorted by
 // (|r| bits, row) in LDS, everything strictly between them is reduced directly.
 //
-// Launch chain per LS solve: k_resid_fused (every block reduces the pass-1 slabs and solves the
-// first 6×6 itself — deterministic, so all agree — then |r| keys + histogram) → k_collect (every
-// block locates the two boundary bins itself, then reduces the interior rows and collects the
-// boundary ones) → k_solve_final (1 block; re-zeroes the histogram).  Three launches instead of
-// five; weighted LS is k_solve_first alone.  Every kernel returns at once when the frame's `done`
-// flag is set.  (A "last block finishes the reduction" fusion was
+// Launch chain per LS solve: k_solve_first (1 block) → k_resid_hist → k_collect (every block
+// locates the two boundary bins itself — k_find_bins' scans, redundantly, no launch of its own —
+// then reduces the interior rows and collects the boundary ones) → k_solve_final (1 block; re-zeroes
+// the histogram's touched groups).  (Solving the first 6×6 redundantly in every k_resid_hist block
+// too was measured slower: 30.4 µs vs 14.8 + 11.2.)  Weighted LS is k_solve_first alone.  Every
+// kernel returns at once when the frame's `done` flag is set.  (A "last block finishes the reduction" fusion was
 // measured slower on MI355X: each block's agent-scope release fence writes back its XCD's L2.)
 #include <algorithm>
 #include <cfloat>
@@ -176,67 +176,6 @@ __device__ __forceinline__ void resid_hist_core(const Rows& rows, int N, const S
     }
     __syncthreads();
     if (threadIdx.x < kResidWin / 256 && csh[threadIdx.x]) atomicAdd(&st.coarse[(kResidWinLo >> 8) + threadIdx.x], csh[threadIdx.x]);
-}
-
-// The first LS solve, by EVERY block of the residual pass (deterministic: all blocks get the same
-// x0, so k_solve_first's launch and its round trip disappear): reduce the pass-1 slabs, the
-// too-few / no-row gates (laser_odometry.cpp:570-576; solver.cpp:118-134, Q11), solve6, the trim
-// ranks.  Thread 0 of every block writes the same global results (x0, sel[4..6], status / done,
-// the trace count, the candidate counters); xs / *go (LDS) give the block x0 and whether to go on.
-template <int NT>
-__device__ void first_solve_shared(const double* __restrict__ partial, int blocks, const SolveState& st,
-                                   imls_iter_trace* tr, const KParams& kp, int update_pose, double* red, double* acc,
-                                   double* xs, int* go) {
-    const int t = threadIdx.x;
-    double loc[kNormEq];
-#pragma unroll
-    for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
-    for (int b = t; b < blocks; b += NT)
-#pragma unroll
-        for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
-    block_sum28<NT>(loc, red, acc);
-    if (t == 0) {
-        *go = 0;
-        st.cand_count[0] = 0u;
-        st.cand_count[1] = 0u;
-        const double nvalid = acc[27];
-        if (update_pose && nvalid < (double)kp.correspond_number) {
-            *st.status = IMLS_FRAME_TOO_FEW;
-            *st.done = 1;
-            if (tr) tr->n_valid = (unsigned long long)nvalid;
-        } else {
-            double x[6];
-            solve6(acc, x);
-            const long long Nv = (long long)nvalid;
-            const long long lo = (long long)(kp.ls_threshold * (double)Nv);
-            long long hi = (long long)((1 - kp.ls_threshold) * (double)Nv);
-            if (hi > Nv - 1) hi = Nv - 1;
-            if (Nv == 0 || lo > hi) {
-                *st.status = IMLS_FRAME_SOLVE_FAILED;
-                *st.done = 1;
-            } else {
-                for (int k = 0; k < 6; ++k) { st.x0[k] = x[k]; xs[k] = x[k]; }
-                st.sel[4] = (int)lo;
-                st.sel[5] = (int)hi;
-                st.sel[6] = (int)Nv;
-                *go = 1;
-            }
-        }
-    }
-    __syncthreads();
-}
-
-__device__ __forceinline__ void resid_fused_body(const Rows& rows, int N, const double* __restrict__ partial, int blocks,
-                                                 const SolveState& st, imls_iter_trace* tr, const KParams& kp,
-                                                 int update_pose, int nb) {
-    if (*st.done) return;
-    __shared__ double red[(kResidBlock / 64) * kNormEq];
-    __shared__ double acc[kNormEq];
-    __shared__ double xs[8];
-    __shared__ int go;
-    first_solve_shared<kResidBlock>(partial, blocks, st, tr, kp, update_pose, red, acc, xs, &go);
-    if (!go) return;                      // block-uniform
-    resid_hist_core(rows, N, st, nb, xs);
 }
 
 // bitonic sort of n (power of two ≤ kCandCap) (key, row) pairs in LDS, ascending
@@ -442,9 +381,17 @@ __device__ __forceinline__ void solve_final_body(const Rows& rows, int N, const 
                                                  const double* __restrict__ partial2, int nparts, const KParams& kp,
                                                  int update_pose) {
     if (*st.done) return;
-    // the histogram was read by k_collect: zero it for the next solve
-    for (int b = threadIdx.x; b < kHistBins / 4; b += kFinalBlock) reinterpret_cast<uint4*>(st.hist)[b] = make_uint4(0u, 0u, 0u, 0u);
-    for (int b = threadIdx.x; b < kHistBins / 256; b += kFinalBlock) st.coarse[b] = 0u;
+    // the histogram was read by k_collect: zero it for the next solve — only the 256-bin groups
+    // whose coarse count is non-zero (residuals occupy a few octaves of the 65536 bins)
+    static_assert(kFinalBlock == kHistBins / 256, "one thread per coarse bin");
+    {
+        if (st.coarse[threadIdx.x] != 0u) {
+            uint4* h = reinterpret_cast<uint4*>(st.hist + (size_t)threadIdx.x * 256);
+#pragma unroll 4
+            for (int b = 0; b < 64; ++b) h[b] = make_uint4(0u, 0u, 0u, 0u);
+            st.coarse[threadIdx.x] = 0u;
+        }
+    }
     __shared__ unsigned long long ck[kCandCap];
     __shared__ unsigned cr[kCandCap];
     __shared__ double red[(kFinalBlock / 64) * kNormEq];
@@ -640,10 +587,9 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
 // Kernels: one frame (arguments by value) and batched (frame = tab[blockIdx.y], float rows from the
 // batched projection; blocks past the frame's own grid leave at once).  Both run the same bodies.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kResidBlock) void k_resid_fused(Rows rows, int N, const double* __restrict__ partial,
-                                                             int blocks, SolveState st, imls_iter_trace* tr, KParams kp,
-                                                             int update_pose) {
-    resid_fused_body(rows, N, partial, blocks, st, tr, kp, update_pose, (int)gridDim.x);
+__global__ __launch_bounds__(kResidBlock) void k_resid_hist(Rows rows, int N, SolveState st) {
+    if (*st.done) return;
+    resid_hist_core(rows, N, st, (int)gridDim.x, st.x0);
 }
 template <int NT>
 __global__ __launch_bounds__(NT) void k_collect(Rows rows, int N, SolveState st, double* __restrict__ partial2) {
@@ -687,11 +633,11 @@ __global__ __launch_bounds__(256) void k_solve_first_b(const PairDev* __restrict
     if (A.N <= kSmallRows) return;
     solve_first_body(A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, weighted, 1);
 }
-__global__ __launch_bounds__(kResidBlock) void k_resid_fused_b(const PairDev* __restrict__ tab, KParams kp, int it) {
+__global__ __launch_bounds__(kResidBlock) void k_resid_hist_b(const PairDev* __restrict__ tab) {
     const PairDev A = tab[blockIdx.y];
     const int nb = resid_blocks_of(A.N);
-    if (A.N <= kSmallRows || (int)blockIdx.x >= nb) return;
-    resid_fused_body(float_rows(A), A.N, A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, 1, nb);
+    if (A.N <= kSmallRows || (int)blockIdx.x >= nb || *A.st.done) return;
+    resid_hist_core(float_rows(A), A.N, A.st, nb, A.st.x0);
 }
 __global__ __launch_bounds__(kBlock) void k_collect_b(const PairDev* __restrict__ tab) {
     const PairDev A = tab[blockIdx.y];
@@ -729,11 +675,9 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
         k_solve_small<<<1, kSmallBlock, 0, s>>>(rows, N, st.partial1, blocks1, st, tr, kp, weighted, update_pose);
         return;
     }
-    if (weighted) {
-        k_solve_first<<<1, 256, 0, s>>>(st.partial1, blocks1, st, tr, kp, weighted, update_pose);
-        return;
-    }
-    k_resid_fused<<<resid_blocks_of(N), kResidBlock, 0, s>>>(rows, N, st.partial1, blocks1, st, tr, kp, update_pose);
+    k_solve_first<<<1, 256, 0, s>>>(st.partial1, blocks1, st, tr, kp, weighted, update_pose);
+    if (weighted) return;
+    k_resid_hist<<<resid_blocks_of(N), kResidBlock, 0, s>>>(rows, N, st);
     const int cb = collect_blocks_of(N);
     k_collect<kBlock><<<cb, kBlock, 0, s>>>(rows, N, st, st.partial2);
     k_solve_final<<<1, kFinalBlock, 0, s>>>(rows, N, st, tr, st.partial2, cb, kp, update_pose);
@@ -759,11 +703,9 @@ void launch_solve_batch(hipStream_t s, const PairDev* tab, const int* n_host, in
     const int weighted = kp.solve_method == IMLS_SOLVE_WEIGHTED_LS;
     if (any_small) k_solve_small_b<<<dim3(1, npairs), kSmallBlock, 0, s>>>(tab, kp, weighted, it);
     if (!any_large) return;
-    if (weighted) {
-        k_solve_first_b<<<dim3(1, npairs), 256, 0, s>>>(tab, kp, weighted, it);
-        return;
-    }
-    k_resid_fused_b<<<dim3(resid_blocks_of(maxN), npairs), kResidBlock, 0, s>>>(tab, kp, it);
+    k_solve_first_b<<<dim3(1, npairs), 256, 0, s>>>(tab, kp, weighted, it);
+    if (weighted) return;
+    k_resid_hist_b<<<dim3(resid_blocks_of(maxN), npairs), kResidBlock, 0, s>>>(tab);
     k_collect_b<<<dim3(collect_blocks_of(maxN), npairs), kBlock, 0, s>>>(tab);
     k_solve_final_b<<<dim3(1, npairs), kFinalBlock, 0, s>>>(tab, kp, it);
 }
