@@ -228,11 +228,12 @@ class Pipeline:
     launched last stay in flight into the next step (the timed region's device-wide synchronize on
     both sides covers them)."""
 
-    def __init__(self, ctxs, prep):
-        h = max(1, len(ctxs) // 2)
-        self.halves = [ctxs[:h], ctxs[h:]] if len(ctxs) > 1 else [ctxs]
+    def __init__(self, ctxs, prep, groups=2):
+        g = max(1, min(groups, len(ctxs)))
+        bounds = [round(k * len(ctxs) / g) for k in range(g + 1)]
+        self.halves = [ctxs[bounds[k]:bounds[k + 1]] for k in range(g)]
         self.prep = prep                  # prep(list of context indices)
-        self.offs = [0, h]
+        self.offs = bounds[:g]
         self.inflight = [False] * len(self.halves)
 
     def _collect(self, h):
@@ -263,13 +264,13 @@ class PairRunner:
     step's pairs are registered as ONE launch sequence (imls_register_frames); else one launch
     sequence per pair, each on its context's stream."""
 
-    def __init__(self, pairs, p, dev, local, fuse=True):
+    def __init__(self, pairs, p, dev, local, fuse=True, groups=2):
         self.fuse = fuse
         self.pairs = pairs
         self.s_dev = [soa_tensor(q.source, dev) for q in pairs]
         self.t_dev = [soa_tensor(q.target, dev) for q in pairs]
         self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in pairs]
-        self.pipe = Pipeline(self.ctxs, self._prep) if fuse else None
+        self.pipe = Pipeline(self.ctxs, self._prep, groups) if fuse else None
 
     def _prep(self, idx):
         for k in idx:
@@ -307,7 +308,7 @@ class StreamRunner:
     scan, set_source of the flat cloud, register), host buffers in.  A sequence ping-pongs over its
     F produced frames (0 … F−1 … 0 …) so every step registers two adjacent frames."""
 
-    def __init__(self, n_seq, p, local, rank, frames_per_seq=5, fuse=True, unique=8, dev=None, resident=True):
+    def __init__(self, n_seq, p, local, rank, frames_per_seq=5, fuse=True, unique=8, dev=None, resident=True, groups=2):
         from planetary_lidar_odometry_amd import producer
         self.fuse = fuse
         sm = synth.hdl64()
@@ -342,7 +343,7 @@ class StreamRunner:
         self.pending = [fr[self.pos[q]][0] for q, fr in enumerate(self.seqs)]
         self.pending_k = list(self.pos)
         self.t_prep = self.t_reg = 0.0        # host time in the per-frame uploads / in registration
-        self.pipe = Pipeline(self.ctxs, self._prep) if fuse else None
+        self.pipe = Pipeline(self.ctxs, self._prep, groups) if fuse else None
 
     def _prep(self, idx):
         """One frame of each sequence in idx, as LaserOdometry.process orders it: the previous
@@ -434,6 +435,9 @@ def main():
     ap.add_argument("--no-fuse", action="store_true",
                     help="one launch sequence per pair on its own stream instead of one for the whole step")
     ap.add_argument("--unique-seqs", type=int, default=8, help="stream: distinct produced sequences")
+    ap.add_argument("--groups", type=int, default=0,
+                    help="fused: launch sequences the step's pairs are split into, kept in flight together "
+                         "(0 = workload default: B 4, A 2, stream 2)")
     ap.add_argument("--host-inputs", action="store_true",
                     help="stream: frames handed over in host memory (PCIe inside the timed region)")
     ap.add_argument("--latency-pairs", type=int, default=50, help="single-pair latency / roofline probe size")
@@ -447,16 +451,19 @@ def main():
     import torch
     import torch.distributed as dist
     world, rank, local, dev = dist_setup(args.backend)
-    # config B: 2 pairs per launch sequence (two sequences overlapping) measured best — 4: 251,
-    # 8: 231, 16: 205 pairs/s (each pair already fills the GPU; more per launch only adds cache
-    # pressure); the ~1900-query stream frames need many per launch: 64: 1925, 128: 2819 frames/s
+    # config B: each pair already fills the GPU; 4 in flight as 4 one-pair launch sequences measured
+    # best (pairs per sequence × sequences: 1×4 264.7, 2×2 252.4, 2×4 255.7, 3×2 237.2, 4×2 231,
+    # 8×2 205 pairs/s: more per launch only adds cache pressure).  The ~1900-query stream frames
+    # need many per launch: 64 per sequence × 2 → 2819 frames/s (32 × 4: 1841)
     P = args.inflight if args.inflight > 0 else {"B": 4, "A": 16, "stream": 128}[args.workload]
+    if args.groups <= 0:
+        args.groups = {"B": 4, "A": 2, "stream": 2}[args.workload]
     fuse = not args.no_fuse
     p = solver_params(args.solver, args.iters)
     t0 = time.time()
     if args.workload == "stream":
         runner = StreamRunner(P, p, local, rank, fuse=fuse, unique=args.unique_seqs, dev=dev,
-                              resident=not args.host_inputs)
+                              resident=not args.host_inputs, groups=args.groups)
         probe_ctx = runner.ctxs[0]
         queries, map_points = runner.queries, runner.map_points
         single = None
@@ -467,7 +474,7 @@ def main():
         if args.queries > 0:
             pairs = [synth.Pair(synth.fps_subsample(q.source, args.queries, seed=rank), q.target, q.true_pose, q.meta)
                      for q in pairs]
-        runner = PairRunner(pairs, p, dev, local, fuse=fuse)
+        runner = PairRunner(pairs, p, dev, local, fuse=fuse, groups=args.groups)
         probe_ctx = runner.ctxs[0]
         queries, map_points = pairs[0].source.size, pairs[0].target.size
         # the probe runs the one-frame launch sequence: its events separate k_knn_wave and k_finish
@@ -589,6 +596,7 @@ def main():
             "solver": solver_txt,
             "search_number": p.search_number,
             "fused_launch": fuse,
+            "launch_groups": args.groups if fuse else P,
             "parallelism": f"independent pairs per GPU over {world} GPU(s), RCCL pose all-gather" if world > 1 else "1 GPU",
         },
         "roofline": roof,
