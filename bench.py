@@ -414,6 +414,11 @@ def latency_probe(run_one, ctx, n_pairs: int, iters: int):
         run_one()
         lat.append(time.perf_counter() - t)
     ctx.enable_timing(False)
+    # one more pair with the traversal / neighbour counters on (Σk_q, NN found: the algorithmic
+    # bytes) — counted apart from the timed pairs, whose kernels then carry no counter atomics
+    ctx.enable_stats(True)
+    run_one()
+    ctx.enable_stats(False)
     k = {name: ctx.kernel_timing(i) for i, name in enumerate(("projection", "index", "solve", "k_knn_wave", "k_finish"))}
     lat = np.array(lat) * 1e3
     idx_ms = k["index"][0] / max(k["index"][1], 1)

@@ -431,6 +431,10 @@ int imls_sample_point_cloud(imls_ctx* ctx, const imls_sample_params* p, const fl
  * 5 = k_ring_pca (imls_ring_normals_pca), 6 = k_major_avg (imls_sample_point_cloud, major_axis),
  * 7 = imls_scan_front_end (all its kernels). */
 int imls_enable_timing(imls_ctx* ctx, int enable);
+/* Traversal / neighbour counters (imls_traversal_stats, and the sum_kq / nn_found fields of
+ * imls_index_stats) are collected only while enabled (default off: they are device-scope atomics
+ * onto a few shared words from every wave, ~60 µs per projection at config B). */
+int imls_enable_stats(imls_ctx* ctx, int enable);
 int imls_kernel_timing(imls_ctx* ctx, int kernel, double* total_ms, uint64_t* launches);
 int imls_reset_timing(imls_ctx* ctx);
 /* Sizes of the last built index (for roofline accounting): points, leaves, tree levels,

@@ -183,6 +183,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_register_frame_async": (C.c_int, [VP]),
         "imls_register_frame_result": (C.c_int, [VP, VP, P(C.c_int), P(C.c_int), VP]),
         "imls_enable_timing": (C.c_int, [VP, C.c_int]),
+        "imls_enable_stats": (C.c_int, [VP, C.c_int]),
         "imls_kernel_timing": (C.c_int, [VP, C.c_int, P(C.c_double), P(C.c_uint64)]),
         "imls_reset_timing": (C.c_int, [VP]),
         "imls_index_stats": (C.c_int, [VP, VP]),
@@ -229,7 +230,7 @@ ABI_SYMBOLS = (
     "imls_batch_last_error", "imls_register_batch", "imls_seed_rng", "imls_get_rng_state",
     "imls_set_rng_state", "imls_map_push", "imls_map_push_device", "imls_map_clear", "imls_map_size",
     "imls_register_frames", "imls_register_frames_async", "imls_register_frames_result",
-    "imls_default_front_params", "imls_scan_front_end",
+    "imls_default_front_params", "imls_scan_front_end", "imls_enable_stats",
 )
 
 _LIB = None

@@ -93,6 +93,9 @@ struct imls_ctx {
     bool batch_pending = false, batch_fused = false, batch_traces = false;
     bool batch_member = false;            // part of a pending batch (as lead or member)
     hipEvent_t ev_batch = nullptr;
+    // traversal / neighbour counters (imls_traversal_stats): off by default — their per-wave
+    // device-scope atomics onto a few shared words cost ~60 µs per projection at config B
+    bool collect_stats = false;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev;
@@ -337,6 +340,7 @@ int ensure_trace(imls_ctx* c, int iters) {
 }
 
 unsigned* fb_count(imls_ctx* c) { return (unsigned*)c->fb.p; }
+unsigned long long* stats_ptr(imls_ctx* c) { return c->collect_stats ? (unsigned long long*)c->stats.p : nullptr; }
 unsigned* fb_list(imls_ctx* c) { return (unsigned*)c->fb.p + 64; }
 
 TreeView tree_view(imls_ctx* c) {
@@ -901,7 +905,7 @@ int imls_project(imls_ctx* c, const double pose[16], float* x_out, float* y_out,
     timed_begin(c, 0, slot);
     launch_project(c->stream, tree_view(c), (const float4*)c->spt.p, (const float4*)c->snr.p, (const unsigned*)c->qperm.p,
                    c->N, dpose, dzero, c->kp, (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p, c->st.partial1,
-                   c->st.trace, (unsigned long long*)c->stats.p, fb_list(c), fb_count(c), c->lane_mode,
+                   c->st.trace, stats_ptr(c), fb_list(c), fb_count(c), c->lane_mode,
                    nullptr, (int*)c->prevnn.p, 0, project_marks(c, marks));
     timed_end(c, 0, slot);
     std::vector<float> hs((size_t)c->N * 4), hd((size_t)c->N * 4), hn((size_t)c->N * 4);
@@ -1023,7 +1027,7 @@ int imls_register_frame_async(imls_ctx* c) {
         timed_begin(c, 0, slot);
         launch_project(c->stream, tv, (const float4*)c->spt.p, (const float4*)c->snr.p, (const unsigned*)c->qperm.p, c->N,
                        c->st.pose, c->st.done, c->kp, (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p,
-                       c->st.partial1, tr + it, (unsigned long long*)c->stats.p, fb_list(c), fb_count(c), c->lane_mode,
+                       c->st.partial1, tr + it, stats_ptr(c), fb_list(c), fb_count(c), c->lane_mode,
                        c->st.delta, (int*)c->prevnn.p, it > 0 && c->temporal_seed, project_marks(c, marks));
         timed_end(c, 0, slot);
         timed_begin(c, 2, slot);
@@ -1082,7 +1086,7 @@ __global__ void k_batch_init(const PairDev* __restrict__ tab, int iters) {
     const int t = threadIdx.x;
     if (t < 16) A.st.pose[t] = (t % 5 == 0) ? 1.0 : 0.0;
     if (t == 0) { *A.st.done = 0; *A.st.status = 0; *A.st.iters = 0; }
-    if (t < 16) A.stats[t] = 0ull;
+    if (A.stats && t < 16) A.stats[t] = 0ull;
     unsigned long long* tr = reinterpret_cast<unsigned long long*>(A.trace);
     const int words = iters * (int)(sizeof(imls_iter_trace) / 8);
     for (int k = t; k < words; k += blockDim.x) tr[k] = 0ull;
@@ -1119,7 +1123,7 @@ PairDev pair_dev(imls_ctx* c) {
     A.lists = (int*)c->prevnn.p;
     A.st = c->st;
     A.trace = (imls_iter_trace*)c->trace_mem.p;
-    A.stats = (unsigned long long*)c->stats.p;
+    A.stats = stats_ptr(c);
     A.fb_list = fb_list(c);
     A.fb_count = fb_count(c);
     return A;
@@ -1460,6 +1464,12 @@ int imls_sample_point_cloud(imls_ctx* c, const imls_sample_params* p, const floa
     if (mk && rc == IMLS_OK && p->method != IMLS_SAMPLE_MAJOR_AXIS) c->ev_pairs[6].pop_back();   // no kernel recorded
     if (c->timing) harvest_timing(c);
     return rc;
+}
+
+int imls_enable_stats(imls_ctx* c, int enable) {
+    if (!c) return IMLS_ERR_ARG;
+    c->collect_stats = enable != 0;
+    return IMLS_OK;
 }
 
 int imls_enable_timing(imls_ctx* c, int enable) {

@@ -311,6 +311,10 @@ class ImlsContext:
                                                      _ptr(out), C.byref(k), _ptr(w)))
         return out[:k.value], w
 
+    def enable_stats(self, on=True):
+        """Collect the traversal / neighbour counters (traversal_stats, index_stats' sum_kq / nn_found)."""
+        self._check(self.lib.imls_enable_stats(self.ctx, int(on)))
+
     def enable_timing(self, on=True):
         self._check(self.lib.imls_enable_timing(self.ctx, int(on)))
 

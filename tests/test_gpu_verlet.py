@@ -34,6 +34,7 @@ def _params(iters=20, shipped_thresholds=True):
 def _frame(ctx, p, verlet, monkeypatch):
     monkeypatch.setenv("IMLS_VERLET", "1" if verlet else "0")
     ctx.set_params(p)          # KParams (incl. the reuse switch) are read when params are set
+    ctx.enable_stats(True)
     r = ctx.register_frame()
     r["stats"] = ctx.traversal_stats()
     return r

@@ -11,6 +11,6 @@ with imls_icp.ImlsBatch(p, streams=3) as b:
 with imls_icp.ImlsContext(p) as c:
     out = []
     for src, tgt in pairs:
-        c.set_target(tgt); c.set_source(src); out.append(c.register_frame()["pose"])
+        c.enable_stats(True); c.set_target(tgt); c.set_source(src); out.append(c.register_frame()["pose"])
         st = c.traversal_stats()
 print("bit-identical:", all(np.array_equal(x, y) for x, y in zip(a, out)), "max diff", max(np.abs(x - y).max() for x, y in zip(a, out)), st)
