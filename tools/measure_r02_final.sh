@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round-2 measurement set (outputs under gpurun_out/${OUT:-final}/): full GPU suite + smoke, the
+# headline bench (driver command, CPU baselines), the stream / A / shipped-solver legs, a kernel
+# trace of the driver command and of a one-pair-in-flight run (the roofline probe's regime), and
+# the PMC traffic passes (FETCH_SIZE, WRITE_SIZE: separate runs, --kernel-trace only).
+set -u
+O=gpurun_out/${OUT:-final}
+mkdir -p $O
+export TMPDIR=/tmp
+step() {  # name, timeout, command...
+  local name=$1 to=$2; shift 2
+  timeout -k 10 $to "$@" > $O/$name.out 2> $O/$name.err
+  local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/$name.err; exit $rc; }
+}
+[ "${SKIP_TESTS:-0}" = 1 ] || step gpu_tests 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+[ "${SKIP_TESTS:-0}" = 1 ] || step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+step bench_B 600 python3 bench.py
+step bench_stream 300 python3 bench.py --workload stream --no-cpu
+step bench_stream_host 300 python3 bench.py --workload stream --no-cpu --host-inputs
+step bench_stream_ransac 400 python3 bench.py --workload stream --no-cpu --solver RANSAC_DRPM
+step bench_A_ransac 400 python3 bench.py --workload A --solver RANSAC_DRPM
+step kt_driver 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_driver -o run -- python3 bench.py --no-cpu
+step kt_single 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_single -o run -- python3 bench.py --no-cpu --inflight 1 --no-fuse --steps 5 --warmup 1
+for c in FETCH_SIZE WRITE_SIZE; do
+  step pmc_$c 300 rocprofv3 --kernel-trace --kernel-include-regex 'k_knn_wave|k_finish' --output-format csv \
+      --pmc $c -d $O/pmc_$c -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --inflight 1 --no-fuse --latency-pairs 3
+done
+echo done

@@ -19,7 +19,9 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
         k = "k_knn_wave" if "k_knn_wave" in row["Kernel_Name"] else "k_finish"
         acc[k].append(float(row["Counter_Value"]) * 1024.0)
     per[c] = {k: sum(v) / len(v) for k, v in acc.items()}
-bench = json.loads((src / "pmc_FETCH_SIZE.json").read_text().strip().splitlines()[-1])
+jf = src / "pmc_FETCH_SIZE.json"
+jf = jf if jf.exists() else src / "pmc_FETCH_SIZE.out"
+bench = json.loads(jf.read_text().strip().splitlines()[-1])
 kern = {k: 2 * per["FETCH_SIZE"].get(k, 0.0) + per["WRITE_SIZE"].get(k, 0.0) for k in ("k_knn_wave", "k_finish")}
 out = {
     "queries": bench["config"]["queries"],
