@@ -183,6 +183,7 @@ KParams make_kparams(const imls_params& p) {
     k.tv_k = p.tensor_k;
     k.tv_sigma = p.tensor_sigma;
     k.tv_thr = p.tensor_distance_threshold;
+    k.cos_thr = std::cos(k.angle_thr_deg * M_PI / 180.0);
     return k;
 }
 

@@ -36,7 +36,7 @@ struct DevBuf {
 
 // Parameters the kernels need, in a flat POD copied by value into launches.
 struct KParams {
-    double h2, r2, cos_unused;
+    double h2, r2, cos_thr;   // cos_thr = cos(angle_thr_deg · π/180): the angle gates' fast path
     double angle_thr_deg;
     int K;                    // search_number
     int angle_on;

@@ -62,7 +62,11 @@ __device__ __forceinline__ bool lessp(double da, int ia, double db, int ib) {
 }
 
 // imls_icp.cpp:442-451 / 681-692: acos(ns·n/(|ns||n|))·180/π > threshold; NaN passes (Q8).
-__device__ __forceinline__ bool angle_reject(const double ns[3], double n0, double n1, double n2, double thr) {
+// cthr = cos(threshold): away from it (|ca − cthr| > 1e-9, where the evaluated angle is ≥ 5e-8°
+// from the threshold — ~6 orders above its rounding error) the comparison is decided without the
+// fp64 acos; inside that band, and for NaN or ca < −1 (acos → NaN → passes), as the reference.
+__device__ __forceinline__ bool angle_reject(const double ns[3], double n0, double n1, double n2, double thr,
+                                             double cthr) {
     double dot = ns[0] * n0;
     dot = dot + ns[1] * n1;
     dot = dot + ns[2] * n2;
@@ -73,6 +77,8 @@ __device__ __forceinline__ bool angle_reject(const double ns[3], double n0, doub
     b = b + n1 * n1;
     b = b + n2 * n2;
     const double ca = dot / (sqrt(a) * sqrt(b));
+    if (ca > cthr + 1e-9) return false;
+    if (ca < cthr - 1e-9 && ca >= -1.0) return true;
     const double angle = acos(ca) * 180.0 / M_PI;
     return angle > thr;
 }
@@ -119,7 +125,7 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
         nn[0] = n4.x; nn[1] = n4.y; nn[2] = n4.z;
     }
     if (!(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) return IMLS_REJ_INVALID_NORMAL;
-    if (kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg)) return IMLS_REJ_NORMAL_CONSTRAINT;
+    if (kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg, kp.cos_thr)) return IMLS_REJ_NORMAL_CONSTRAINT;
     const double xd[3] = {xf[0], xf[1], xf[2]};
     unsigned long long acc = 0ull;
     int nacc = 0;
@@ -131,7 +137,7 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
             ++kq;
             // get_normals=false without count mode (TV's IMLS neighbours): every normal is ∞ (Q1)
             bool ok = kp.get_normals && isfinite(qn.x) && isfinite(qn.y) && isfinite(qn.z);
-            if (ok && kp.angle_on) ok = !angle_reject(ns, qn.x, qn.y, qn.z, kp.angle_thr_deg);
+            if (ok && kp.angle_on) ok = !angle_reject(ns, qn.x, qn.y, qn.z, kp.angle_thr_deg, kp.cos_thr);
             if (ok) { acc |= 1ull << j; ++nacc; }
         }
     }
@@ -179,7 +185,7 @@ __device__ int finish_plane(const float xf[3], const double ns[3], int p1, const
     const float4 n4 = t.mnr[p1];
     const double nn[3] = {n4.x, n4.y, n4.z};
     if (!(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) return IMLS_REJ_INVALID_NORMAL;
-    if (kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg)) return IMLS_REJ_NORMAL_CONSTRAINT;
+    if (kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg, kp.cos_thr)) return IMLS_REJ_NORMAL_CONSTRAINT;
     const float4 q = t.mpt[p1];
     const double xd[3] = {xf[0], xf[1], xf[2]};
     const double v0 = xd[0] - (double)q.x, v1 = xd[1] - (double)q.y, v2 = xd[2] - (double)q.z;
