@@ -380,16 +380,24 @@ bool solve_wls(const double* s, const double* d, const double* n, const double* 
     return true;
 }
 
+constexpr double kDrpmEigRelTol = 1e-30;
+
 // Symmetric 6×6 eigendecomposition (Eigen::SelfAdjointEigenSolver semantics: ascending
 // eigenvalues, unit eigenvectors as columns).  Cyclic Jacobi; every DRPM quantity that uses the
 // eigenvectors is invariant to their sign (degeneracy.h:14-131), so the sign is unpinned-safe.
-void sym_eig(int n, const double* Hin, double* ev, double* U /* col-major: U[c*n+r] */) {
+// Stops when the off-diagonal mass is below max(1e-300, rel_tol·‖H‖_F²): rel_tol = 1e-30 (DRPM) is
+// the usual Jacobi criterion off(A) ≤ 1e-15·‖A‖ (4 sweeps where the absolute one needs ~12);
+// rel_tol = 0 sweeps on until the off-diagonal terms underflow.
+void sym_eig(int n, const double* Hin, double* ev, double* U /* col-major: U[c*n+r] */, double rel_tol = 0.0) {
     std::vector<double> a(Hin, Hin + n * n), v(n * n, 0.0);
     for (int i = 0; i < n; ++i) v[i * n + i] = 1;
+    double fro = 0;
+    for (int i = 0; i < n * n; ++i) fro += a[i] * a[i];
+    const double stop = std::max(1e-300, rel_tol * fro);
     for (int sweep = 0; sweep < 100; ++sweep) {
         double off = 0;
         for (int p = 0; p < n; ++p) for (int q = p + 1; q < n; ++q) off += a[p * n + q] * a[p * n + q];
-        if (off < 1e-300) break;
+        if (off < stop) break;
         for (int p = 0; p < n; ++p)
             for (int q = p + 1; q < n; ++q) {
                 double apq = a[p * n + q];
@@ -454,7 +462,7 @@ bool solve_drpm(const double* s, const double* d, const double* n, const double*
             g[r] += Aw[6 * i + r] * bw[i];
         }
     double ev[6], U[36];
-    sym_eig(6, H, ev, U);
+    sym_eig(6, H, ev, U, kDrpmEigRelTol);
     // noise estimate
     double mean[36] = {0}, var[6] = {0};
     const double sp2 = sp * sp, sn2 = sn * sn;
@@ -1261,6 +1269,6 @@ int oracle_colpiv_qr_solve(const double* A, int rows, int cols, const double* b,
     return colpiv_qr_solve(a, rows, cols, bb, x);
 }
 void oracle_delta_from_x(const double x[6], double delta[16]) { delta_from_x(x, delta); }
-int oracle_sym_eig6(const double* H, double* evals, double* evecs) { sym_eig(6, H, evals, evecs); return 0; }
+int oracle_sym_eig6(const double* H, double* evals, double* evecs) { sym_eig(6, H, evals, evecs, kDrpmEigRelTol); return 0; }
 
 }  // extern "C"

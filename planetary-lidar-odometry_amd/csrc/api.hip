@@ -294,6 +294,7 @@ int sync_rng(imls_ctx* c) {
 int prepare_ransac(imls_ctx* c, int rows) {
     if (c->P.solve_method != IMLS_SOLVE_RANSAC) return IMLS_OK;
     if (!grow(c->ransac_mem, ransac_bytes(rows))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (RANSAC)");
+    if (ransac_init_tables(c->device)) return fail(c, IMLS_ERR_DEVICE, "RANSAC rand() table upload");
     return sync_rng(c);
 }
 
@@ -1103,12 +1104,13 @@ __global__ void k_batch_results(const PairDev* __restrict__ tab, int n, double* 
     }
 }
 
-// The batched path covers the shipped matcher with the LS-family solvers on float rows; RANSAC /
-// DRPM, tensor voting, the projected-distance rule and the exact per-lane mode keep one launch
-// sequence per frame (each on its own context stream, so they still overlap).
+// The batched path covers both matchers with the LS-family solvers and RANSAC (+ its LS / weighted
+// LS / DRPM final solve); tensor voting, the projected-distance rule and the exact per-lane mode
+// keep one launch sequence per frame (each on its own context stream, so they still overlap).
 bool batch_fusable(const imls_ctx* c) {
     return !c->lane_mode && !c->kp.proj && !c->kp.tv &&
-           (c->P.solve_method == IMLS_SOLVE_LS || c->P.solve_method == IMLS_SOLVE_WEIGHTED_LS);
+           (c->P.solve_method == IMLS_SOLVE_LS || c->P.solve_method == IMLS_SOLVE_WEIGHTED_LS ||
+            c->P.solve_method == IMLS_SOLVE_RANSAC);
 }
 
 PairDev pair_dev(imls_ctx* c) {
@@ -1127,6 +1129,7 @@ PairDev pair_dev(imls_ctx* c) {
     A.stats = stats_ptr(c);
     A.fb_list = fb_list(c);
     A.fb_count = fb_count(c);
+    if (c->P.solve_method == IMLS_SOLVE_RANSAC) A.rf = ransac_frame(c->ransac_mem.p, c->N, (int*)c->rng.p);
     return A;
 }
 
@@ -1162,7 +1165,7 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
             return fail(L, IMLS_ERR_STATE, "context " + std::to_string(k) + ": set_target and set_source first");
     }
     L->members.assign(ctxs, ctxs + n);
-    L->batch_fused = batch_fusable(L);
+    L->batch_fused = batch_fusable(L) && (L->P.solve_method != IMLS_SOLVE_RANSAC || n <= (size_t)kMaxRansacBatch);
     if (!L->batch_fused) {
         // one launch sequence per frame, each on its own context stream
         for (size_t k = 0; k < n; ++k) {
@@ -1200,6 +1203,7 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         if (int rc = ensure_trace(c, iters)) return fail(L, rc, c->err);
         if (!grow(c->stats, 128)) return fail(L, IMLS_ERR_DEVICE, "hipMalloc");
         if (int rc = ensure_map_normals(c)) return fail(L, rc, c->err);
+        if (int rc = prepare_ransac(c, c->N)) return fail(L, rc, c->err);
         L->tab_h[k] = pair_dev(c);
         L->member_n[k] = c->N;
         if (c != L) {
@@ -1215,6 +1219,7 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
     hipMemcpyAsync(L->tab_d.p, L->tab_h, n * sizeof(PairDev), hipMemcpyHostToDevice, s);
     k_batch_init<<<(unsigned)n, 64, 0, s>>>(tab, iters);
     const KParams kp = L->kp;
+    const RansacParams rp = ransac_params(L->P);
     const int* nh = L->member_n.data();
     for (int it = 0; it < iters; ++it) {
         int slot;
@@ -1222,7 +1227,10 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         launch_project_batch(s, tab, nh, (int)n, kp, it, it > 0 && L->temporal_seed);
         timed_end(L, 0, slot);
         timed_begin(L, 2, slot);
-        launch_solve_batch(s, tab, nh, (int)n, kp, it);
+        if (kp.solve_method == IMLS_SOLVE_RANSAC)
+            launch_ransac_batch(s, tab, nh, (int)n, kp, rp, it);
+        else
+            launch_solve_batch(s, tab, nh, (int)n, kp, it);
         timed_end(L, 2, slot);
     }
     k_batch_results<<<(unsigned)std::min<size_t>(n, 256), 64, 0, s>>>(tab, (int)n, (double*)L->res_d.p);

@@ -121,6 +121,36 @@ struct SolveState {
     int partial_cap;
 };
 
+// RANSAC state of one context (ransac.hip), carved from its RANSAC scratch by ransac_frame().
+struct RansacDev {
+    int* rng;          // [34] glibc state (persistent)
+    int* counts;       // [kHypMax]
+    double* T;         // [kHypMax × 16]
+    int* best;         // [1]
+    int* evaluated;    // [1]
+    int* rdone;        // [1] RANSAC finished (early exit or max iterations)
+    double* bestT;     // [16]
+    int* active;       // [1] the frame was still running when this solve began
+};
+struct DrpmDev {
+    double* H;         // [36] row-major
+    double* g;         // [6]
+    double* U;         // [36] eigenvectors as columns: U[k·6 + r] = component r of vector k
+    double* ev;        // [6] ascending
+    double* slabs;     // [blocks × kDrpmSlab]
+};
+struct RansacFrame {
+    double* all;       // [10·cap] the compacted valid correspondences (fp64 Rows layout)
+    double* inl;       // [10·cap] the inliers of the best Δ with their weights
+    int* blkcnt;       // [nb + 1] compaction block counts → offsets
+    double* blkw;      // [nb + 1] compaction block Σw
+    int *cnt_all, *cnt_in;
+    double* wsum;      // Σw of the inliers
+    RansacDev R;
+    DrpmDev Dv;
+    int cap;           // max(N, 1)
+};
+
 // One registration of a batched launch (imls_register_frames): everything a per-iteration kernel
 // reads or writes for that frame.  The batch's table of these lives in device memory; a batched
 // kernel takes its frame from tab[blockIdx.y] (a wave-uniform, read-only load: scalar) and runs the
@@ -138,6 +168,7 @@ struct PairDev {
     unsigned long long* stats;         // traversal / neighbour counters
     unsigned* fb_list;                 // uncertified queries (exact fallback) + their count
     unsigned* fb_count;
+    RansacFrame rf;                    // RANSAC scratch (solve_method RANSAC), else zero
 };
 
 // index.hip — two phases, so many frames' uploads and filters can be enqueued before one wait:
@@ -189,7 +220,12 @@ constexpr int kSmallRows = 4096;
 int solve_blocks(int N);
 // Batched LS / weighted-LS solve + pose update for all frames of tab (float rows from the batched
 // projection): k_solve_small over the frames with N ≤ kSmallRows, the grid chain over the others.
-void launch_solve_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp, int it);
+// src 0: float rows of the batched projection; src 1: every frame's RANSAC inlier rows (fp64, the
+// grid chain always; n_host = the frames' RANSAC caps), pass 1 included.
+void launch_solve_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp, int it,
+                        int src = 0);
+// pass 1 over every frame's RANSAC inlier rows (weighted: w / Σw)
+void launch_rows_pass1_batch(hipStream_t s, const PairDev* tab, const int* cap_host, int npairs, int weighted);
 
 // normals.hip — map normals recomputed from the map (get_normals=false, count mode), Morton order
 int launch_map_normals(hipStream_t s, const TreeView& t, int K, double r_normal, float4* out);
@@ -226,6 +262,13 @@ struct SolveLaunch {
 };
 void launch_solve(hipStream_t s, const SolveLaunch& L);
 size_t ransac_bytes(int cap);
+RansacFrame ransac_frame(void* scratch, int cap, int* rng);   // the carve of ransac_bytes(cap)
+int ransac_init_tables(int device);    // the rand() jump table on `device` (current), once per device
+constexpr int kMaxRansacBatch = 1024;  // frames per batched RANSAC launch
+// Batched RANSAC (+ final LS / weighted LS / DRPM) for all frames of tab, ICP iteration `it`:
+// one launch per step for the whole batch, every frame at its own count / rand() stream / done flag.
+void launch_ransac_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp,
+                         const RansacParams& rp, int it);
 void ransac_seed_host(uint32_t seed, int st[34]);
 
 // scanreg.hip — ring-neighbourhood PCA normals + geometric-features presample (imls_ring_normals_pca)

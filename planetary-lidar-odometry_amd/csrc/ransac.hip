@@ -6,9 +6,9 @@
 //   1. the valid correspondences (float rows, source order) are compacted, order kept, into fp64
 //      rows S/D/N — the reference's std::vector<Vector3d> inputs; the TOO_FEW gate
 //      (laser_odometry.cpp:570-576) runs on their count;
-//   2. hypotheses in growing chunks (16, 64, 256, 1024, 4096): k_ransac_draws replays glibc rand()
-//      (one draw per hypothesis: the FPS start index), k_ransac_hyp runs one hypothesis per block —
-//      FPS (two arg-max passes, first index wins ties as the sequential `>` does), the 3×6
+//   2. hypotheses in growing chunks (16, 64, 256, 1024, 4096): k_ransac_begin / k_ransac_select
+//      replay glibc rand() (one draw per hypothesis of the next chunk: the FPS start index),
+//      k_ransac_hyp runs one hypothesis per block at a time — FPS (two arg-max passes, first index wins ties as the sequential `>` does), the 3×6
 //      column-pivoted Householder QR basic solution (Eigen ColPivHouseholderQR, not normal
 //      equations: a rank-3 system squared would misjudge the rank), Δ, and the inlier count;
 //      k_ransac_select scans the chunk in order with the reference's strict `>` and early exit
@@ -21,25 +21,65 @@
 //      Jacobi eigendecomposition (SelfAdjointEigenSolver order: ascending), the per-point noise
 //      mean/variance along the eigenvectors, normal-CDF probabilities with SNR factor 10, and
 //      x = U·diag(p/λ)·Uᵀ g when min p < threshold, else the weighted solve.
+// Batched frames (imls_register_frames, launch_ransac_batch): every step above is one launch for
+// all frames (grid y = frame, the same bodies; each frame keeps its own count, rand() stream, chunk
+// progress and done flag).
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
 #include "solve_common.h"
 
 namespace imlsgpu {
 namespace {
 
 constexpr int kHypBlock = 256;
+constexpr int kHypGrid = 2048;        // batched hypothesis grid (blocks stride over the running frames' items)
 constexpr int kDrpmSlab = 42;         // 36 noise-mean terms + 6 variance terms per block
 
 // ---------------------------------------------------------------------------------------------
-// glibc random() TYPE_3 (what rand() returns), state = 31 words + front/rear indices
+// glibc random() TYPE_3 (what rand() returns): state = a ring of 31 words + front / rear indices
+// (st[31], st[32]; rear = front − 3 mod 31).  rand() adds ring[rear] into ring[front], returns that
+// word >> 1 and advances both: the word sequence is x_i = x_{i−31} + x_{i−3} (mod 2^32), and with
+// s_j = ring[(front + j) % 31] = x_{i−31+j} the k-th next word is x_{i+k} = Σ_j C[k][j]·s_j (mod 2^32)
+// for fixed integer rows C[k] (C[m−31] = e_m for m < 31, C[k] = C[k−31] + C[k−3]).  So the draw of
+// every hypothesis of a chunk is an independent 31-term dot product with the committed state (no
+// serial replay), and committing `used` draws rebuilds the ring in one parallel step.  Integer
+// arithmetic mod 2^32: exact in any summation order.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int rand_next(int* st) {
-    unsigned* ring = reinterpret_cast<unsigned*>(st);
+__device__ unsigned g_rand_jump[kHypMax * 31];   // C[k][j], k < kHypMax (host-built, ransac_init_tables)
+
+// x_{i+k} from the committed state; called by a whole wave (lanes < 31 hold one term each)
+__device__ __forceinline__ unsigned rand_word_ahead(const int* __restrict__ st, int k) {
+    const int lane = threadIdx.x & 63;
+    unsigned term = 0u;
+    if (lane < 31) {
+        const int f = st[31];
+        term = g_rand_jump[(size_t)k * 31 + lane] * (unsigned)st[(f + lane) % 31];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) term += (unsigned)__shfl_xor((int)term, o, 64);
+    return term;
+}
+
+// commit `used` draws: ring'[(front + used + j) % 31] = x_{i+used−31+j}; called by one whole wave
+__device__ __forceinline__ void rand_commit(int* __restrict__ st, int used) {
+    const int lane = threadIdx.x & 63;
     const int f = st[31], r = st[32];
-    ring[f] += ring[r];
-    const int out = (int)(ring[f] >> 1);
-    st[31] = (f + 1) % 31;
-    st[32] = (r + 1) % 31;
-    return out;
+    const unsigned sj = lane < 31 ? (unsigned)st[(f + lane) % 31] : 0u;   // s_j in lane j
+    unsigned sv[31];                                                      // … and in every lane
+#pragma unroll
+    for (int j = 0; j < 31; ++j) sv[j] = (unsigned)__builtin_amdgcn_readlane((int)sj, j);
+    const unsigned kept = (unsigned)__shfl((int)sj, used + lane, 64);     // x_{i+used−31+j} = s_{used+j}
+    const int idx = used - 31 + lane;
+    unsigned acc = 0u;
+    if (lane < 31 && idx >= 0) {
+#pragma unroll
+        for (int j = 0; j < 31; ++j) acc += g_rand_jump[(size_t)idx * 31 + j] * sv[j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 31) st[(f + used + lane) % 31] = (int)(idx < 0 ? kept : acc);
+    if (lane == 0) { st[31] = (f + used) % 31; st[32] = (r + used) % 31; }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -92,9 +132,8 @@ struct Source {
     }
 };
 
-__global__ __launch_bounds__(kBlock) void k_compact_count(Source src, int n, int* __restrict__ blkcnt,
-                                                          double* __restrict__ blkw, const int* __restrict__ done) {
-    if (done && *done) return;
+__device__ __forceinline__ void compact_count_body(const Source& src, int n, int* __restrict__ blkcnt,
+                                                   double* __restrict__ blkw) {
     __shared__ int wc[kBlock / 64];
     __shared__ double ws[kBlock / 64];
     const int i = blockIdx.x * kBlock + threadIdx.x;
@@ -114,9 +153,8 @@ __global__ __launch_bounds__(kBlock) void k_compact_count(Source src, int n, int
 }
 
 // One block: exclusive scan of the block counts (in place), total count and Σw in fixed order.
-__global__ __launch_bounds__(1024) void k_compact_scan(int* __restrict__ blkcnt, const double* __restrict__ blkw, int nb,
-                                                       CompactOut out, const int* __restrict__ done) {
-    if (done && *done) return;
+__device__ __forceinline__ void compact_scan_body(int* __restrict__ blkcnt, const double* __restrict__ blkw, int nb,
+                                                  const CompactOut& out) {
     __shared__ int sc[1024];
     __shared__ double sw[1024];
     int carry = 0;
@@ -150,9 +188,8 @@ __global__ __launch_bounds__(1024) void k_compact_scan(int* __restrict__ blkcnt,
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_compact_scatter(Source src, int n, const int* __restrict__ blkoff, CompactOut out,
-                                                            const int* __restrict__ done) {
-    if (done && *done) return;
+__device__ __forceinline__ void compact_scatter_body(const Source& src, int n, const int* __restrict__ blkoff,
+                                                     const CompactOut& out) {
     __shared__ int wc[kBlock / 64];
     const int i = blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -176,20 +213,64 @@ __global__ __launch_bounds__(kBlock) void k_compact_scatter(Source src, int n, c
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// RANSAC state (device, one per context)
-// ---------------------------------------------------------------------------------------------
-struct RansacDev {
-    int* rng;          // [34] glibc state (persistent)
-    int* first;        // [kHypMax] FPS start index per hypothesis of the current chunk
-    int* counts;       // [kHypMax]
-    double* T;         // [kHypMax × 16]
-    int* best;         // [1]
-    int* evaluated;    // [1]
-    int* rdone;        // [1] RANSAC finished (early exit or max iterations)
-    double* bestT;     // [16]
-    int* active;       // [1] the frame was still running when this solve began
-};
+__global__ __launch_bounds__(kBlock) void k_compact_count(Source src, int n, int* __restrict__ blkcnt,
+                                                          double* __restrict__ blkw, const int* __restrict__ done) {
+    if (done && *done) return;
+    compact_count_body(src, n, blkcnt, blkw);
+}
+__global__ __launch_bounds__(1024) void k_compact_scan(int* __restrict__ blkcnt, const double* __restrict__ blkw, int nb,
+                                                       CompactOut out, const int* __restrict__ done) {
+    if (done && *done) return;
+    compact_scan_body(blkcnt, blkw, nb, out);
+}
+__global__ __launch_bounds__(kBlock) void k_compact_scatter(Source src, int n, const int* __restrict__ blkoff, CompactOut out,
+                                                            const int* __restrict__ done) {
+    if (done && *done) return;
+    compact_scatter_body(src, n, blkoff, out);
+}
+
+// The two compactions of a batched frame: mode 0 = its valid float rows (the projection's output)
+// → F.all; mode 1 = the inliers of its best Δ, weighted → F.inl (+ Σw).
+__device__ __forceinline__ int frame_compact(const PairDev& A, int mode, double dist_thr, double h2, Source& src,
+                                             CompactOut& out) {
+    const RansacFrame& F = A.rf;
+    src = Source{};
+    if (mode == 0) {
+        src.cs = A.cs; src.cd = A.cd; src.cn = A.cn;
+        out = CompactOut{F.all, F.cnt_all, nullptr, F.cap};
+        return A.N;
+    }
+    src.rows = F.all; src.count = F.cnt_all; src.cap = F.cap; src.T = F.R.bestT;
+    src.dist_thr = dist_thr; src.h2 = h2;
+    out = CompactOut{F.inl, F.cnt_in, F.wsum, F.cap};
+    return F.cap;
+}
+__global__ __launch_bounds__(kBlock) void k_compact_count_b(const PairDev* __restrict__ tab, int mode, double dist_thr,
+                                                            double h2) {
+    const PairDev A = tab[blockIdx.y];
+    Source src;
+    CompactOut out;
+    const int n = frame_compact(A, mode, dist_thr, h2, src, out);
+    if ((int)blockIdx.x >= (n + kBlock - 1) / kBlock || *A.st.done) return;
+    compact_count_body(src, n, A.rf.blkcnt, A.rf.blkw);
+}
+__global__ __launch_bounds__(1024) void k_compact_scan_b(const PairDev* __restrict__ tab, int mode) {
+    const PairDev A = tab[blockIdx.y];
+    if (*A.st.done) return;
+    Source src;
+    CompactOut out;
+    const int n = frame_compact(A, mode, 0.0, 0.0, src, out);
+    compact_scan_body(A.rf.blkcnt, A.rf.blkw, (n + kBlock - 1) / kBlock, out);
+}
+__global__ __launch_bounds__(kBlock) void k_compact_scatter_b(const PairDev* __restrict__ tab, int mode, double dist_thr,
+                                                              double h2) {
+    const PairDev A = tab[blockIdx.y];
+    Source src;
+    CompactOut out;
+    const int n = frame_compact(A, mode, dist_thr, h2, src, out);
+    if ((int)blockIdx.x >= (n + kBlock - 1) / kBlock || *A.st.done) return;
+    compact_scatter_body(src, n, A.rf.blkcnt, out);
+}
 
 // stand-alone DRPM with no rows fails like the oracle's solve_drpm (N == 0 → false)
 __global__ void k_drpm_guard(const int* __restrict__ c, SolveState st) {
@@ -201,8 +282,8 @@ __global__ void k_set_count(int* __restrict__ c, int v) {
 }
 
 // gate on the compacted count, reset the RANSAC selection state
-__global__ void k_ransac_begin(const int* __restrict__ count, int correspond_number, int update_pose, SolveState st,
-                               imls_iter_trace* tr, RansacDev R) {
+__device__ __forceinline__ void ransac_begin_body(const int* __restrict__ count, int correspond_number, int update_pose,
+                                                  const SolveState& st, imls_iter_trace* tr, const RansacDev& R) {
     if (threadIdx.x) return;
     *R.active = *st.done ? 0 : 1;
     if (*st.done) return;
@@ -219,13 +300,9 @@ __global__ void k_ransac_begin(const int* __restrict__ count, int correspond_num
 #pragma unroll
     for (int k = 0; k < 16; ++k) R.bestT[k] = (k % 5 == 0) ? 1.0 : 0.0;
 }
-
-__global__ void k_ransac_draws(const int* __restrict__ count, RansacDev R, int chunk, const int* __restrict__ done) {
-    if (threadIdx.x || *done || *R.rdone) return;
-    __shared__ int st[34];   // LDS: the ring is indexed dynamically
-    for (int k = 0; k < 34; ++k) st[k] = R.rng[k];
-    const int n = *count;
-    for (int h = 0; h < chunk; ++h) R.first[h] = rand_next(st) % n;
+__global__ void k_ransac_begin(const int* __restrict__ count, int correspond_number, int update_pose, SolveState st,
+                               imls_iter_trace* tr, RansacDev R) {
+    ransac_begin_body(count, correspond_number, update_pose, st, tr, R);
 }
 
 // block arg-max of (value, index): larger value, then smaller index
@@ -391,20 +468,16 @@ __device__ void colpiv_qr_small(double A[RR][6], double b[RR], double x[6]) {
     }
 }
 
-// One hypothesis per block: FPS(3) from the drawn start, 3×6 QR, Δ, inlier count.
-__global__ __launch_bounds__(kHypBlock) void k_ransac_hyp(const double* __restrict__ rows, const int* __restrict__ count,
-                                                          int cap, RansacDev R, double dist_thr, const int* __restrict__ done) {
-    if (*done || *R.rdone) return;
+// Hypothesis h of the current chunk, by one block: its draw (the FPS start) from the committed
+// rand() state, FPS(3), the 3×6 QR, Δ, its inlier count.
+__device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, const double* __restrict__ Dp,
+                                               const double* __restrict__ Np, int n, const RansacDev& R,
+                                               double dist_thr, int h) {
     __shared__ double sv[kHypBlock / 64];
     __shared__ int si[kHypBlock / 64];
     __shared__ double T[16];
     __shared__ int cnt_s[kHypBlock / 64];
-    const int h = blockIdx.x, n = *count;
-    const size_t c3 = 3 * (size_t)cap;
-    const double* S = rows;
-    const double* Dp = rows + c3;
-    const double* Np = rows + 2 * c3;
-    const int f0 = R.first[h];
+    const int f0 = (int)(rand_word_ahead(R.rng, h) >> 1) % n;   // rand() % n (solver.cpp / common.cpp:49)
     // pass 1: farthest from f0 (common.cpp:48-66: strict `>` from −1, taken points skipped)
     double bv = -1.0;
     int bi = 0x7fffffff;
@@ -470,30 +543,53 @@ __global__ __launch_bounds__(kHypBlock) void k_ransac_hyp(const double* __restri
     }
     if (threadIdx.x < 16) R.T[(size_t)h * 16 + threadIdx.x] = T[threadIdx.x];
 }
+// one frame: hypotheses blockIdx.x, blockIdx.x + gridDim.x, … of the chunk
+__global__ __launch_bounds__(kHypBlock) void k_ransac_hyp(const double* __restrict__ rows, const int* __restrict__ count,
+                                                          int cap, RansacDev R, double dist_thr, int chunk,
+                                                          const int* __restrict__ done) {
+    if (*done || *R.rdone) return;
+    const int n = *count;
+    const size_t c3 = 3 * (size_t)cap;
+    for (int h = blockIdx.x; h < chunk; h += gridDim.x) ransac_hyp_one(rows, rows + c3, rows + 2 * c3, n, R, dist_thr, h);
+}
 
-// Sequential semantics of the hypothesis loop (solver.cpp:244-326) over one chunk.
-__global__ void k_ransac_select(const int* __restrict__ count, RansacDev R, int chunk, int max_iterations, double min_pct,
-                                const int* __restrict__ done) {
-    if (threadIdx.x || *done || *R.rdone) return;
+// Sequential semantics of the hypothesis loop (solver.cpp:244-326) over one chunk, by one wave: the
+// loop stops at the first hypothesis whose count exceeds ⌊pct·N⌋ (best > min_inliers first holds
+// there, since best ≤ min_inliers on entry); best / bestT follow the strict `>` (first maximum
+// wins); exactly the draws consumed are committed.
+__device__ __forceinline__ void ransac_select_body(const int* __restrict__ count, const RansacDev& R, int chunk,
+                                                   int max_iterations, double min_pct) {
+    const int lane = threadIdx.x & 63;
     const int n = *count;
     const int min_inliers = (int)(min_pct * (double)n);
-    int best = *R.best, used = 0;
-    bool stop = false;
-    for (int h = 0; h < chunk && !stop; ++h) {
-        ++used;
-        if (R.counts[h] > best) {
-            best = R.counts[h];
-            for (int k = 0; k < 16; ++k) R.bestT[k] = R.T[(size_t)h * 16 + k];
+    int best = *R.best, bi = -1, used = chunk;
+    for (int base = 0; base < chunk; base += 64) {
+        const int h = base + lane;
+        const int c = h < chunk ? R.counts[h] : INT_MIN;
+        const unsigned long long sm = __ballot(h < chunk && c > min_inliers);
+        const int lim = sm ? (int)__builtin_ctzll(sm) : 63;
+        int v = lane <= lim ? c : INT_MIN, vi = h;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int ov = __shfl_xor(v, o, 64), oi = __shfl_xor(vi, o, 64);
+            if (ov > v || (ov == v && oi < vi)) { v = ov; vi = oi; }
         }
-        if (best > min_inliers) stop = true;
+        if (v > best) { best = v; bi = vi; }
+        if (sm) { used = base + lim + 1; break; }
     }
-    __shared__ int st[34];
-    for (int k = 0; k < 34; ++k) st[k] = R.rng[k];
-    for (int k = 0; k < used; ++k) (void)rand_next(st);       // commit exactly the draws consumed
-    for (int k = 0; k < 34; ++k) R.rng[k] = st[k];
-    *R.best = best;
-    *R.evaluated += used;
-    if (stop || *R.evaluated >= max_iterations) *R.rdone = 1;
+    if (bi >= 0 && lane < 16) R.bestT[lane] = R.T[(size_t)bi * 16 + lane];
+    rand_commit(R.rng, used);                 // commit exactly the draws consumed
+    if (lane == 0) {
+        *R.best = best;
+        const int evaluated = *R.evaluated + used;
+        *R.evaluated = evaluated;
+        if (used < chunk || best > min_inliers || evaluated >= max_iterations) *R.rdone = 1;
+    }
+}
+__global__ __launch_bounds__(64) void k_ransac_select(const int* __restrict__ count, RansacDev R, int chunk,
+                                                     int max_iterations, double min_pct, const int* __restrict__ done) {
+    if (*done || *R.rdone) return;
+    ransac_select_body(count, R, chunk, max_iterations, min_pct);
 }
 
 // trace of a RANSAC iteration as the oracle records it: n_valid = correspondences, n_kept = 0
@@ -514,16 +610,9 @@ __global__ void k_ransac_check_inliers(const int* __restrict__ count_in, SolveSt
 // ---------------------------------------------------------------------------------------------
 // DRPM (solver.cpp:499-603, degeneracy.h:14-131)
 // ---------------------------------------------------------------------------------------------
-struct DrpmDev {
-    double* H;        // [36] row-major
-    double* g;        // [6]
-    double* U;        // [36] eigenvectors as columns: U[k·6 + r] = component r of vector k
-    double* ev;       // [6] ascending
-    double* slabs;    // [blocks × kDrpmSlab]
-};
-
 // reduce the weighted normal equations (pass-1 slabs), eigendecompose H
-__global__ __launch_bounds__(256) void k_drpm_eig(const double* __restrict__ partial, int blocks, SolveState st, DrpmDev Dv) {
+__device__ __forceinline__ void drpm_eig_body(const double* __restrict__ partial, int blocks, const SolveState& st,
+                                              const DrpmDev& Dv) {
     if (*st.done) return;
     __shared__ double red[(256 / 64) * kNormEq];
     __shared__ double acc[kNormEq];
@@ -534,21 +623,27 @@ __global__ __launch_bounds__(256) void k_drpm_eig(const double* __restrict__ par
 #pragma unroll
         for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
     block_sum28<256>(loc, red, acc);
-    if (threadIdx.x) return;
-    double H[36];
-    int k = 0;
-    for (int r = 0; r < 6; ++r)
-        for (int c = r; c < 6; ++c) { H[r * 6 + c] = acc[k]; H[c * 6 + r] = acc[k]; ++k; }
-    for (int q = 0; q < 36; ++q) Dv.H[q] = H[q];
-    for (int r = 0; r < 6; ++r) Dv.g[r] = acc[21 + r];
-    double ev[6], U[36];
-    sym_eig<6>(H, ev, U);
-    for (int q = 0; q < 36; ++q) Dv.U[q] = U[q];
-    for (int r = 0; r < 6; ++r) Dv.ev[r] = ev[r];
+    if (threadIdx.x >= 64) return;
+    // H (row-major, from the upper-triangle terms) and g; the eigendecomposition by wave 0, lane k
+    // holding row k (sym_eig6_wave: the oracle's Jacobi, operation for operation)
+    const int lane = threadIdx.x, k = lane < 6 ? lane : 0;
+    double row[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        const int r0 = k < c ? k : c, c0 = k < c ? c : k;
+        row[c] = acc[6 * r0 - r0 * (r0 - 1) / 2 + (c0 - r0)];
+    }
+    if (lane < 6) {
+#pragma unroll
+        for (int c = 0; c < 6; ++c) Dv.H[lane * 6 + c] = row[c];
+        Dv.g[lane] = acc[21 + lane];
+    }
+    sym_eig6_wave(row, Dv.ev, Dv.U);
 }
 
 // per-point noise mean (36) and variance along the eigenvectors (6), degeneracy.h:14-72
-__global__ __launch_bounds__(kBlock) void k_drpm_noise(Rows rows, int N, SolveState st, DrpmDev Dv, double sp, double sn) {
+__device__ __forceinline__ void drpm_noise_body(const Rows& rows, int N, const SolveState& st, const DrpmDev& Dv, double sp,
+                                                double sn) {
     if (*st.done) return;
     __shared__ double red[(kBlock / 64) * kDrpmSlab];
     const int i = blockIdx.x * kBlock + threadIdx.x;
@@ -633,9 +728,9 @@ __device__ __forceinline__ double normal_cdf(double mean, double sd, double x) {
     return 0.5 * erfc(-(x - mean) / (sd * sqrt(2.0)));   // Boost.Math cdf(normal(mean, sd), x)
 }
 
-__global__ __launch_bounds__(256) void k_drpm_final(int blocks, SolveState st, DrpmDev Dv, imls_iter_trace* tr, KParams kp,
-                                                    double threshold, const int* __restrict__ count_all,
-                                                    const int* __restrict__ count_in, int update_pose) {
+__device__ __forceinline__ void drpm_final_body(int blocks, const SolveState& st, const DrpmDev& Dv, imls_iter_trace* tr,
+                                                const KParams& kp, double threshold, const int* __restrict__ count_all,
+                                                const int* __restrict__ count_in, int update_pose) {
     if (*st.done) return;
     __shared__ double red[(256 / 64) * kDrpmSlab];
     __shared__ double tot[kDrpmSlab];
@@ -703,13 +798,112 @@ __global__ __launch_bounds__(256) void k_drpm_final(int blocks, SolveState st, D
     finish_iteration(st, tr, D, (double)*count_all, (double)*count_in, update_pose, kp);
 }
 
+__global__ __launch_bounds__(256) void k_drpm_eig(const double* __restrict__ partial, int blocks, SolveState st, DrpmDev Dv) {
+    drpm_eig_body(partial, blocks, st, Dv);
+}
+__global__ __launch_bounds__(kBlock) void k_drpm_noise(Rows rows, int N, SolveState st, DrpmDev Dv, double sp, double sn) {
+    drpm_noise_body(rows, N, st, Dv, sp, sn);
+}
+__global__ __launch_bounds__(256) void k_drpm_final(int blocks, SolveState st, DrpmDev Dv, imls_iter_trace* tr, KParams kp,
+                                                    double threshold, const int* __restrict__ count_all,
+                                                    const int* __restrict__ count_in, int update_pose) {
+    drpm_final_body(blocks, st, Dv, tr, kp, threshold, count_all, count_in, update_pose);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Batched RANSAC / DRPM kernels (launch_ransac_batch): frame = tab[blockIdx.y], the same bodies as
+// the one-frame kernels above; the frame's RANSAC scratch is A.rf, its pose update always on.
+// ---------------------------------------------------------------------------------------------
+__global__ void k_ransac_begin_b(const PairDev* __restrict__ tab, int correspond_number, int it) {
+    const PairDev A = tab[blockIdx.y];
+    ransac_begin_body(A.rf.cnt_all, correspond_number, 1, A.st, A.trace + it, A.rf.R);
+}
+// The chunk's hypotheses of the frames still running, spread evenly over the grid: each block first
+// lists the running frames (done / RANSAC-finished ones drop out), then strides over
+// (frame, hypothesis) items — one frame without an early exit gets the whole grid, not a slice.
+__global__ __launch_bounds__(kHypBlock) void k_ransac_hyp_b(const PairDev* __restrict__ tab, int npairs, int chunk,
+                                                            double dist_thr) {
+    __shared__ int sact[kMaxRansacBatch];
+    __shared__ int swc[kHypBlock / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    int na = 0;
+    for (int base = 0; base < npairs; base += kHypBlock) {
+        bool act = false;
+        if (base + t < npairs) act = !*tab[base + t].st.done && !*tab[base + t].rf.R.rdone;
+        const unsigned long long m = __ballot(act);
+        if (lane == 0) swc[wv] = __popcll(m);
+        __syncthreads();
+        int off = na, tot = na;
+        for (int k = 0; k < kHypBlock / 64; ++k) {
+            off += k < wv ? swc[k] : 0;
+            tot += swc[k];
+        }
+        if (act) sact[off + __popcll(m & ((1ull << lane) - 1ull))] = base + t;
+        na = tot;
+        __syncthreads();
+    }
+    const long long items = (long long)na * chunk;
+    for (long long q = blockIdx.x; q < items; q += gridDim.x) {
+        const int fr = __builtin_amdgcn_readfirstlane(sact[q % na]);
+        const int h = (int)(q / na);
+        const PairDev A = tab[fr];
+        const size_t c3 = 3 * (size_t)A.rf.cap;
+        ransac_hyp_one(A.rf.all, A.rf.all + c3, A.rf.all + 2 * c3, *A.rf.cnt_all, A.rf.R, dist_thr, h);
+    }
+}
+__global__ __launch_bounds__(64) void k_ransac_select_b(const PairDev* __restrict__ tab, int chunk, int max_iterations,
+                                                        double min_pct) {
+    const PairDev A = tab[blockIdx.y];
+    if (*A.st.done || *A.rf.R.rdone) return;
+    ransac_select_body(A.rf.cnt_all, A.rf.R, chunk, max_iterations, min_pct);
+}
+__global__ void k_ransac_check_inliers_b(const PairDev* __restrict__ tab) {
+    const PairDev A = tab[blockIdx.y];
+    if (threadIdx.x || *A.st.done) return;
+    if (*A.rf.cnt_in == 0) {
+        *A.st.status = IMLS_FRAME_SOLVE_FAILED;
+        *A.st.done = 1;
+    }
+}
+__global__ void k_ransac_trace_b(const PairDev* __restrict__ tab, int it) {
+    const PairDev A = tab[blockIdx.y];
+    if (threadIdx.x || !*A.rf.R.active) return;
+    A.trace[it].n_valid = (unsigned long long)*A.rf.cnt_all;
+    A.trace[it].n_kept = 0;
+}
+__global__ __launch_bounds__(256) void k_drpm_eig_b(const PairDev* __restrict__ tab) {
+    const PairDev A = tab[blockIdx.y];
+    drpm_eig_body(A.st.partial1, solve_blocks_of(A.rf.cap), A.st, A.rf.Dv);
+}
+__global__ __launch_bounds__(kBlock) void k_drpm_noise_b(const PairDev* __restrict__ tab, double sp, double sn) {
+    const PairDev A = tab[blockIdx.y];
+    if ((int)blockIdx.x >= solve_blocks_of(A.rf.cap)) return;
+    drpm_noise_body(frame_rows(A, 1, 1), A.rf.cap, A.st, A.rf.Dv, sp, sn);
+}
+__global__ __launch_bounds__(256) void k_drpm_final_b(const PairDev* __restrict__ tab, KParams kp, double threshold, int it) {
+    const PairDev A = tab[blockIdx.y];
+    drpm_final_body(solve_blocks_of(A.rf.cap), A.st, A.rf.Dv, A.trace + it, kp, threshold, A.rf.cnt_all, A.rf.cnt_in, 1);
+}
+
+// chunk sizes of the hypothesis loop: 16, 64, 256, 1024, then kHypMax, up to max_iterations in all
+std::vector<int> ransac_chunks(int max_iterations) {
+    std::vector<int> v;
+    int started = 0;
+    for (long long chunk = 16; started < max_iterations; chunk *= 4) {
+        const int cn = (int)std::min<long long>(std::min<long long>(chunk, kHypMax), max_iterations - started);
+        v.push_back(cn);
+        started += cn;
+    }
+    return v;
+}
+
 }  // namespace
 
 size_t ransac_bytes(int cap) {
     // the carve sequence of launch_solve, each piece rounded up to 256 B (+ slack per piece)
     const size_t c = (size_t)std::max(cap, 1);
     const size_t nb = (c + kBlock - 1) / kBlock + 1;
-    return 2 * (10 * c + 8) * 8 + nb * (4 + 8) + (size_t)kHypMax * (4 + 4 + 16 * 8) + nb * kDrpmSlab * 8 +
+    return 2 * (10 * c + 8) * 8 + nb * (4 + 8) + (size_t)kHypMax * (4 + 16 * 8) + nb * kDrpmSlab * 8 +
            (36 + 6 + 36 + 6 + 16) * 8 + 32 * 256;
 }
 
@@ -744,98 +938,169 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
                            L.rows_are_double, L.count);
         return;
     }
-    // carve the RANSAC scratch
     const int cap = std::max(L.N, 1);
     const size_t c = (size_t)cap;
     const int nb = (cap + kBlock - 1) / kBlock;
-    char* p = (char*)L.scratch;
-    auto carve = [&](size_t bytes) { char* r = p; p += (bytes + 255) / 256 * 256; return r; };
-    double* all = (double*)carve((10 * c + 8) * 8);
-    double* inl = (double*)carve((10 * c + 8) * 8);
-    int* blkcnt = (int*)carve((size_t)(nb + 1) * 4);
-    double* blkw = (double*)carve((size_t)(nb + 1) * 8);
-    int* cnt_all = (int*)carve(64);
-    int* cnt_in = (int*)carve(64);
-    double* wsum = (double*)carve(64);
-    RansacDev R;
-    R.rng = L.rng;
-    R.first = (int*)carve((size_t)kHypMax * 4);
-    R.counts = (int*)carve((size_t)kHypMax * 4);
-    R.T = (double*)carve((size_t)kHypMax * 16 * 8);
-    R.best = (int*)carve(64);
-    R.evaluated = (int*)carve(64);
-    R.rdone = (int*)carve(64);
-    R.bestT = (double*)carve(16 * 8);
-    R.active = (int*)carve(64);
-    DrpmDev Dv;
-    Dv.H = (double*)carve(36 * 8);
-    Dv.g = (double*)carve(6 * 8);
-    Dv.U = (double*)carve(36 * 8);
-    Dv.ev = (double*)carve(6 * 8);
-    Dv.slabs = (double*)carve((size_t)(nb + 1) * kDrpmSlab * 8);
+    const RansacFrame F = ransac_frame(L.scratch, cap, L.rng);
+    const RansacDev& R = F.R;
     const int* done = L.st.done;
 
     // 1. compact the valid correspondences (fp64 rows from the host API are already compact)
     Source src{};
-    CompactOut out{all, cnt_all, nullptr, cap};
+    CompactOut out{F.all, F.cnt_all, nullptr, cap};
     if (!L.rows_are_double) {
         src.cs = L.cs; src.cd = L.cd; src.cn = L.cn;
-        k_compact_count<<<nb, kBlock, 0, s>>>(src, L.N, blkcnt, blkw, done);
-        k_compact_scan<<<1, 1024, 0, s>>>(blkcnt, blkw, nb, out, done);
-        k_compact_scatter<<<nb, kBlock, 0, s>>>(src, L.N, blkcnt, out, done);
+        k_compact_count<<<nb, kBlock, 0, s>>>(src, L.N, F.blkcnt, F.blkw, done);
+        k_compact_scan<<<1, 1024, 0, s>>>(F.blkcnt, F.blkw, nb, out, done);
+        k_compact_scatter<<<nb, kBlock, 0, s>>>(src, L.N, F.blkcnt, out, done);
     } else {
-        (void)hipMemcpyAsync(all, L.rows_d, 9 * c * 8, hipMemcpyDeviceToDevice, s);
-        k_set_count<<<1, 64, 0, s>>>(cnt_all, L.N);
+        (void)hipMemcpyAsync(F.all, L.rows_d, 9 * c * 8, hipMemcpyDeviceToDevice, s);
+        k_set_count<<<1, 64, 0, s>>>(F.cnt_all, L.N);
     }
-    k_ransac_begin<<<1, 64, 0, s>>>(cnt_all, kp.correspond_number, L.update_pose, L.st, L.tr, R);
-
     // 2. hypotheses in growing chunks
-    int started = 0;
-    for (int chunk = 16; started < L.ransac.max_iterations; chunk *= 4) {
-        const int cn = std::min(std::min(chunk, kHypMax), L.ransac.max_iterations - started);
-        k_ransac_draws<<<1, 64, 0, s>>>(cnt_all, R, cn, done);
-        k_ransac_hyp<<<cn, kHypBlock, 0, s>>>(all, cnt_all, cap, R, L.ransac.distance_threshold, done);
-        k_ransac_select<<<1, 64, 0, s>>>(cnt_all, R, cn, L.ransac.max_iterations, L.ransac.min_inliers_percentage, done);
-        started += cn;
+    const std::vector<int> chunks = ransac_chunks(L.ransac.max_iterations);
+    k_ransac_begin<<<1, 64, 0, s>>>(F.cnt_all, kp.correspond_number, L.update_pose, L.st, L.tr, R);
+    for (const int cn : chunks) {
+        k_ransac_hyp<<<cn, kHypBlock, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done);
+        k_ransac_select<<<1, 64, 0, s>>>(F.cnt_all, R, cn, L.ransac.max_iterations, L.ransac.min_inliers_percentage, done);
     }
 
     // 3. inliers of the best Δ with their Huber-like weights (order kept), Σw
     Source isrc{};
-    isrc.rows = all;
-    isrc.count = cnt_all;
+    isrc.rows = F.all;
+    isrc.count = F.cnt_all;
     isrc.cap = cap;
     isrc.T = R.bestT;
     isrc.dist_thr = L.ransac.distance_threshold;
     isrc.h2 = L.ransac.huber_threshold * L.ransac.distance_threshold;
-    CompactOut iout{inl, cnt_in, wsum, cap};
-    k_compact_count<<<nb, kBlock, 0, s>>>(isrc, cap, blkcnt, blkw, done);
-    k_compact_scan<<<1, 1024, 0, s>>>(blkcnt, blkw, nb, iout, done);
-    k_compact_scatter<<<nb, kBlock, 0, s>>>(isrc, cap, blkcnt, iout, done);
-    k_ransac_check_inliers<<<1, 64, 0, s>>>(cnt_in, L.st, L.tr);
+    CompactOut iout{F.inl, F.cnt_in, F.wsum, cap};
+    k_compact_count<<<nb, kBlock, 0, s>>>(isrc, cap, F.blkcnt, F.blkw, done);
+    k_compact_scan<<<1, 1024, 0, s>>>(F.blkcnt, F.blkw, nb, iout, done);
+    k_compact_scatter<<<nb, kBlock, 0, s>>>(isrc, cap, F.blkcnt, iout, done);
+    k_ransac_check_inliers<<<1, 64, 0, s>>>(F.cnt_in, L.st, L.tr);
 
     // 4. final solve on the inliers
     KParams fk = kp;
     fk.correspond_number = 0;                       // the count gate ran before RANSAC
-    Rows rows{nullptr, nullptr, nullptr, inl, inl + 3 * c, inl + 6 * c, inl + 9 * c, 1, cnt_in, wsum};
+    double* inl = F.inl;
+    Rows rows{nullptr, nullptr, nullptr, inl, inl + 3 * c, inl + 6 * c, inl + 9 * c, 1, F.cnt_in, F.wsum};
     switch (L.ransac.final_method) {
         case IMLS_FINAL_LS:
             fk.solve_method = IMLS_SOLVE_LS;
             fk.ls_threshold = L.ransac.ls_threshold;
-            launch_solve_chain(s, cap, 0, fk, nullptr, nullptr, nullptr, inl, nullptr, st, L.tr, L.update_pose, 1, cnt_in, nullptr);
+            launch_solve_chain(s, cap, 0, fk, nullptr, nullptr, nullptr, inl, nullptr, st, L.tr, L.update_pose, 1, F.cnt_in, nullptr);
             break;
         case IMLS_FINAL_WEIGHTED_LS:
             fk.solve_method = IMLS_SOLVE_WEIGHTED_LS;
-            launch_solve_chain(s, cap, 0, fk, nullptr, nullptr, nullptr, inl, inl + 9 * c, st, L.tr, L.update_pose, 1, cnt_in, wsum);
+            launch_solve_chain(s, cap, 0, fk, nullptr, nullptr, nullptr, inl, inl + 9 * c, st, L.tr, L.update_pose, 1, F.cnt_in, F.wsum);
             break;
         default: {   // DRPM
             const int b1 = solve_blocks(cap);
             launch_rows_pass1(s, rows, cap, L.st.partial1, b1);
-            k_drpm_eig<<<1, 256, 0, s>>>(L.st.partial1, b1, L.st, Dv);
-            k_drpm_noise<<<b1, kBlock, 0, s>>>(rows, cap, L.st, Dv, L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals);
-            k_drpm_final<<<1, 256, 0, s>>>(b1, L.st, Dv, L.tr, fk, L.ransac.drpm_threshold, cnt_all, cnt_in, L.update_pose);
+            k_drpm_eig<<<1, 256, 0, s>>>(L.st.partial1, b1, L.st, F.Dv);
+            k_drpm_noise<<<b1, kBlock, 0, s>>>(rows, cap, L.st, F.Dv, L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals);
+            k_drpm_final<<<1, 256, 0, s>>>(b1, L.st, F.Dv, L.tr, fk, L.ransac.drpm_threshold, F.cnt_all, F.cnt_in, L.update_pose);
         }
     }
-    if (L.tr) k_ransac_trace<<<1, 64, 0, s>>>(cnt_all, R, L.tr);
+    if (L.tr) k_ransac_trace<<<1, 64, 0, s>>>(F.cnt_all, R, L.tr);
+}
+
+RansacFrame ransac_frame(void* scratch, int cap, int* rng) {
+    // the carve sequence sized by ransac_bytes, each piece rounded up to 256 B
+    const size_t c = (size_t)std::max(cap, 1);
+    const int nb = (int)((c + kBlock - 1) / kBlock);
+    char* p = (char*)scratch;
+    auto carve = [&](size_t bytes) { char* r = p; p += (bytes + 255) / 256 * 256; return r; };
+    RansacFrame F{};
+    F.cap = (int)c;
+    F.all = (double*)carve((10 * c + 8) * 8);
+    F.inl = (double*)carve((10 * c + 8) * 8);
+    F.blkcnt = (int*)carve((size_t)(nb + 1) * 4);
+    F.blkw = (double*)carve((size_t)(nb + 1) * 8);
+    F.cnt_all = (int*)carve(64);
+    F.cnt_in = (int*)carve(64);
+    F.wsum = (double*)carve(64);
+    F.R.rng = rng;
+    F.R.counts = (int*)carve((size_t)kHypMax * 4);
+    F.R.T = (double*)carve((size_t)kHypMax * 16 * 8);
+    F.R.best = (int*)carve(64);
+    F.R.evaluated = (int*)carve(64);
+    F.R.rdone = (int*)carve(64);
+    F.R.bestT = (double*)carve(16 * 8);
+    F.R.active = (int*)carve(64);
+    F.Dv.H = (double*)carve(36 * 8);
+    F.Dv.g = (double*)carve(6 * 8);
+    F.Dv.U = (double*)carve(36 * 8);
+    F.Dv.ev = (double*)carve(6 * 8);
+    F.Dv.slabs = (double*)carve((size_t)(nb + 1) * kDrpmSlab * 8);
+    return F;
+}
+
+void launch_ransac_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp,
+                         const RansacParams& rp, int it) {
+    if (npairs <= 0 || npairs > kMaxRansacBatch) return;
+    std::vector<int> caps((size_t)npairs);
+    int maxc = 1;
+    for (int k = 0; k < npairs; ++k) {
+        caps[k] = std::max(n_host[k], 1);
+        maxc = std::max(maxc, caps[k]);
+    }
+    const dim3 gc((maxc + kBlock - 1) / kBlock, npairs), g1(1, npairs);
+    const double h2 = rp.huber_threshold * rp.distance_threshold;
+    // 1. every frame's valid correspondences, compacted (order kept) to fp64
+    k_compact_count_b<<<gc, kBlock, 0, s>>>(tab, 0, 0.0, 0.0);
+    k_compact_scan_b<<<g1, 1024, 0, s>>>(tab, 0);
+    k_compact_scatter_b<<<gc, kBlock, 0, s>>>(tab, 0, 0.0, 0.0);
+    // 2. hypotheses: each chunk's items of the still-running frames spread over one grid
+    const std::vector<int> chunks = ransac_chunks(rp.max_iterations);
+    k_ransac_begin_b<<<g1, 64, 0, s>>>(tab, kp.correspond_number, it);
+    for (const int cn : chunks) {
+        k_ransac_hyp_b<<<std::min(cn * npairs, kHypGrid), kHypBlock, 0, s>>>(tab, npairs, cn, rp.distance_threshold);
+        k_ransac_select_b<<<g1, 64, 0, s>>>(tab, cn, rp.max_iterations, rp.min_inliers_percentage);
+    }
+    // 3. inliers of each frame's best Δ with their weights
+    k_compact_count_b<<<gc, kBlock, 0, s>>>(tab, 1, rp.distance_threshold, h2);
+    k_compact_scan_b<<<g1, 1024, 0, s>>>(tab, 1);
+    k_compact_scatter_b<<<gc, kBlock, 0, s>>>(tab, 1, rp.distance_threshold, h2);
+    k_ransac_check_inliers_b<<<g1, 64, 0, s>>>(tab);
+    // 4. final solve
+    KParams fk = kp;
+    fk.correspond_number = 0;
+    switch (rp.final_method) {
+        case IMLS_FINAL_LS:
+            fk.solve_method = IMLS_SOLVE_LS;
+            fk.ls_threshold = rp.ls_threshold;
+            launch_solve_batch(s, tab, caps.data(), npairs, fk, it, 1);
+            break;
+        case IMLS_FINAL_WEIGHTED_LS:
+            fk.solve_method = IMLS_SOLVE_WEIGHTED_LS;
+            launch_solve_batch(s, tab, caps.data(), npairs, fk, it, 1);
+            break;
+        default:
+            launch_rows_pass1_batch(s, tab, caps.data(), npairs, 1);
+            k_drpm_eig_b<<<g1, 256, 0, s>>>(tab);
+            k_drpm_noise_b<<<dim3(solve_blocks_of(maxc), npairs), kBlock, 0, s>>>(tab, rp.drpm_stdev_points, rp.drpm_stdev_normals);
+            k_drpm_final_b<<<g1, 256, 0, s>>>(tab, fk, rp.drpm_threshold, it);
+    }
+    k_ransac_trace_b<<<g1, 64, 0, s>>>(tab, it);
+}
+
+int ransac_init_tables(int device) {
+    // C[k][j] over k < kHypMax: C[m − 31] = e_m (m < 31), C[k] = C[k − 31] + C[k − 3] (mod 2^32)
+    static std::mutex mu;
+    static std::vector<int> ready;
+    std::lock_guard<std::mutex> lock(mu);
+    if (device < 0) return -1;
+    if ((int)ready.size() <= device) ready.resize(device + 1, 0);
+    if (ready[device]) return 0;
+    std::vector<uint32_t> T((size_t)(kHypMax + 31) * 31, 0u);
+    for (int j = 0; j < 31; ++j) T[(size_t)j * 31 + j] = 1u;
+    for (int k = 0; k < kHypMax; ++k)
+        for (int j = 0; j < 31; ++j)
+            T[(size_t)(k + 31) * 31 + j] = T[(size_t)k * 31 + j] + T[(size_t)(k + 28) * 31 + j];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_rand_jump), T.data() + 31 * 31, (size_t)kHypMax * 31 * 4) != hipSuccess) return -1;
+    ready[device] = 1;
+    return 0;
 }
 
 void ransac_seed_host(uint32_t seed, int st[34]) {

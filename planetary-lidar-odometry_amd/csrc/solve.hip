@@ -32,7 +32,7 @@ constexpr int kCollectBlocks = 128;
 // ---------------------------------------------------------------------------------------------
 // pass 1 for double rows (host API); float rows get it fused in k_project
 template <int NT>
-__global__ __launch_bounds__(NT) void k_rows_pass1(Rows rows, int N, double* __restrict__ partial) {
+__device__ __forceinline__ void rows_pass1_body(const Rows& rows, int N, double* __restrict__ partial) {
     __shared__ double red[(NT / 64) * kNormEq];
     __shared__ double out[kNormEq];
     const int i = blockIdx.x * NT + threadIdx.x;
@@ -45,6 +45,16 @@ __global__ __launch_bounds__(NT) void k_rows_pass1(Rows rows, int N, double* __r
     }
     block_normeq<NT>(a, b, cnt, red, out);
     if (threadIdx.x < kNormEq) partial[(size_t)blockIdx.x * kNormEq + threadIdx.x] = out[threadIdx.x];
+}
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows_pass1(Rows rows, int N, double* __restrict__ partial) {
+    rows_pass1_body<NT>(rows, N, partial);
+}
+// batched: every frame's RANSAC inlier rows (grid y = frame)
+__global__ __launch_bounds__(kBlock) void k_rows_pass1_b(const PairDev* __restrict__ tab, int weighted) {
+    const PairDev A = tab[blockIdx.y];
+    if ((int)blockIdx.x >= solve_blocks_of(A.rf.cap)) return;
+    rows_pass1_body<kBlock>(frame_rows(A, 1, weighted), A.rf.cap, A.st.partial1);
 }
 
 // Reduce pass-1 partials, first solve, set up the trim; or, for WLS, the only solve.
@@ -618,37 +628,43 @@ __host__ __device__ __forceinline__ int collect_blocks_of(int N) {
 __host__ __device__ __forceinline__ int pass1_blocks_of(int N) {   // project_blocks(N): wave slabs + fallback slabs
     return (N + kPass1Block - 1) / kPass1Block + kPass1Fallback;
 }
-__device__ __forceinline__ Rows float_rows(const PairDev& A) {
-    return Rows{A.cs, A.cd, A.cn, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr};
-}
+// batched chain: src 0 = the projection's float rows (k_solve_small for N ≤ kSmallRows, the grid
+// chain above), src 1 = the RANSAC inlier rows (the grid chain always, as launch_solve runs it)
+__device__ __forceinline__ int frame_rows_n(const PairDev& A, int src) { return src ? A.rf.cap : A.N; }
+__device__ __forceinline__ bool frame_big(const PairDev& A, int src) { return src || A.N > kSmallRows; }
 
 __global__ __launch_bounds__(kSmallBlock) void k_solve_small_b(const PairDev* __restrict__ tab, KParams kp, int weighted,
                                                               int it) {
     const PairDev A = tab[blockIdx.y];
     if (A.N > kSmallRows) return;
-    solve_small_body(float_rows(A), A.N, A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, weighted, 1);
+    solve_small_body(frame_rows(A, 0, 0), A.N, A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, weighted, 1);
 }
-__global__ __launch_bounds__(256) void k_solve_first_b(const PairDev* __restrict__ tab, KParams kp, int weighted, int it) {
+__global__ __launch_bounds__(256) void k_solve_first_b(const PairDev* __restrict__ tab, KParams kp, int weighted, int it,
+                                                       int src) {
     const PairDev A = tab[blockIdx.y];
-    if (A.N <= kSmallRows) return;
-    solve_first_body(A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, weighted, 1);
+    if (!frame_big(A, src)) return;
+    solve_first_body(A.st.partial1, src ? solve_blocks_of(A.rf.cap) : pass1_blocks_of(A.N), A.st, A.trace + it, kp,
+                     weighted, 1);
 }
-__global__ __launch_bounds__(kResidBlock) void k_resid_hist_b(const PairDev* __restrict__ tab) {
+__global__ __launch_bounds__(kResidBlock) void k_resid_hist_b(const PairDev* __restrict__ tab, int src) {
     const PairDev A = tab[blockIdx.y];
-    const int nb = resid_blocks_of(A.N);
-    if (A.N <= kSmallRows || (int)blockIdx.x >= nb || *A.st.done) return;
-    resid_hist_core(float_rows(A), A.N, A.st, nb, A.st.x0);
+    const int N = frame_rows_n(A, src);
+    const int nb = resid_blocks_of(N);
+    if (!frame_big(A, src) || (int)blockIdx.x >= nb || *A.st.done) return;
+    resid_hist_core(frame_rows(A, src, 0), N, A.st, nb, A.st.x0);
 }
-__global__ __launch_bounds__(kBlock) void k_collect_b(const PairDev* __restrict__ tab) {
+__global__ __launch_bounds__(kBlock) void k_collect_b(const PairDev* __restrict__ tab, int src) {
     const PairDev A = tab[blockIdx.y];
-    const int nb = collect_blocks_of(A.N);
-    if (A.N <= kSmallRows || (int)blockIdx.x >= nb) return;
-    collect_body<kBlock>(float_rows(A), A.N, A.st, A.st.partial2, nb);
+    const int N = frame_rows_n(A, src);
+    const int nb = collect_blocks_of(N);
+    if (!frame_big(A, src) || (int)blockIdx.x >= nb) return;
+    collect_body<kBlock>(frame_rows(A, src, 0), N, A.st, A.st.partial2, nb);
 }
-__global__ __launch_bounds__(kFinalBlock) void k_solve_final_b(const PairDev* __restrict__ tab, KParams kp, int it) {
+__global__ __launch_bounds__(kFinalBlock) void k_solve_final_b(const PairDev* __restrict__ tab, KParams kp, int it, int src) {
     const PairDev A = tab[blockIdx.y];
-    if (A.N <= kSmallRows) return;
-    solve_final_body(float_rows(A), A.N, A.st, A.trace + it, A.st.partial2, collect_blocks_of(A.N), kp, 1);
+    if (!frame_big(A, src)) return;
+    const int N = frame_rows_n(A, src);
+    solve_final_body(frame_rows(A, src, 0), N, A.st, A.trace + it, A.st.partial2, collect_blocks_of(N), kp, 1);
 }
 
 }  // namespace
@@ -692,21 +708,29 @@ extern "C" int imls_debug_solve(unsigned long long* out) {
 #endif
 
 namespace imlsgpu {
-void launch_solve_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp, int it) {
+void launch_rows_pass1_batch(hipStream_t s, const PairDev* tab, const int* cap_host, int npairs, int weighted) {
+    int maxc = 1;
+    for (int k = 0; k < npairs; ++k) maxc = std::max(maxc, cap_host[k]);
+    k_rows_pass1_b<<<dim3(solve_blocks_of(maxc), npairs), kBlock, 0, s>>>(tab, weighted);
+}
+
+void launch_solve_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp, int it,
+                        int src) {
     if (npairs <= 0) return;
     int maxN = 0;
     bool any_small = false, any_large = false;
     for (int k = 0; k < npairs; ++k) {
         maxN = std::max(maxN, n_host[k]);
-        (n_host[k] <= kSmallRows ? any_small : any_large) = true;
+        (n_host[k] <= kSmallRows && !src ? any_small : any_large) = true;
     }
     const int weighted = kp.solve_method == IMLS_SOLVE_WEIGHTED_LS;
+    if (src) launch_rows_pass1_batch(s, tab, n_host, npairs, weighted);
     if (any_small) k_solve_small_b<<<dim3(1, npairs), kSmallBlock, 0, s>>>(tab, kp, weighted, it);
     if (!any_large) return;
-    k_solve_first_b<<<dim3(1, npairs), 256, 0, s>>>(tab, kp, weighted, it);
+    k_solve_first_b<<<dim3(1, npairs), 256, 0, s>>>(tab, kp, weighted, it, src);
     if (weighted) return;
-    k_resid_hist_b<<<dim3(resid_blocks_of(maxN), npairs), kResidBlock, 0, s>>>(tab);
-    k_collect_b<<<dim3(collect_blocks_of(maxN), npairs), kBlock, 0, s>>>(tab);
-    k_solve_final_b<<<dim3(1, npairs), kFinalBlock, 0, s>>>(tab, kp, it);
+    k_resid_hist_b<<<dim3(resid_blocks_of(maxN), npairs), kResidBlock, 0, s>>>(tab, src);
+    k_collect_b<<<dim3(collect_blocks_of(maxN), npairs), kBlock, 0, s>>>(tab, src);
+    k_solve_final_b<<<dim3(1, npairs), kFinalBlock, 0, s>>>(tab, kp, it, src);
 }
 }  // namespace imlsgpu

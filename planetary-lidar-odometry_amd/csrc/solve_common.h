@@ -43,6 +43,18 @@ struct Rows {
     }
 };
 
+// Rows of a batched frame: the projection's float rows (src 0) or the frame's RANSAC inlier rows
+// (src 1: fp64, device-side count; weights w / Σw when weighted) — what launch_solve builds for the
+// same solve of a one-frame launch.
+__device__ __forceinline__ Rows frame_rows(const PairDev& A, int src, int weighted) {
+    if (!src) return Rows{A.cs, A.cd, A.cn, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr};
+    const size_t c = (size_t)A.rf.cap;
+    const double* r = A.rf.inl;
+    return Rows{nullptr, nullptr, nullptr, r, r + 3 * c, r + 6 * c, weighted ? r + 9 * c : nullptr, 1, A.rf.cnt_in,
+                weighted ? A.rf.wsum : nullptr};
+}
+__host__ __device__ __forceinline__ int solve_blocks_of(int N) { return (N + kBlock - 1) / kBlock; }
+
 // pass 1 of the LS chain (weighted normal equations) on any rows; solve.hip
 void launch_rows_pass1(hipStream_t s, const Rows& rows, int N, double* partial, int blocks);
 
@@ -383,6 +395,106 @@ __device__ void sym_eig(const double* Hin, double* ev, double* U) {
 #pragma unroll
             for (int k = 0; k < N; ++k) val = ord[c] == k ? v[r][k] : val;
             U[c * N + r] = val;
+        }
+    }
+}
+
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+constexpr double kDrpmEigRelTol = 1e-30;   // the oracle's DRPM Jacobi stop (imls_oracle.cpp sym_eig)
+
+// sym_eig<6> by one wave, lane k < 6 holding row k of the matrix and of the eigenvector accumulator:
+// the same sweeps, rotations and per-element expressions in the same order (a rotation's column
+// update is lane-local, its row update reads rows p and q after it, as the sequential loops do), so
+// the result is the one-thread routine's (with the relative stop below); ~6× shorter dependency chains.  a_row: row k of the
+// symmetric input (lanes < 6).  Every lane of the wave calls; ev / U (as sym_eig) written by lanes < 6.
+__device__ inline void sym_eig6_wave(const double (&a_row)[6], double* __restrict__ ev, double* __restrict__ U) {
+    constexpr int N = 6;
+    const int lane = threadIdx.x & 63;
+    double a[N], v[N];
+#pragma unroll
+    for (int c = 0; c < N; ++c) { a[c] = a_row[c]; v[c] = lane == c ? 1.0 : 0.0; }
+    // stop at off-diagonal mass < max(1e-300, 1e-30·‖H‖_F²) (the oracle's sym_eig with DRPM's rel_tol)
+    double fro = 0;
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            const double x = readlane_f64(a[c], r);
+            fro += x * x;
+        }
+    const double stop = fmax(1e-300, kDrpmEigRelTol * fro);
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0;
+#pragma unroll
+        for (int p = 0; p < N; ++p)
+#pragma unroll
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = readlane_f64(a[q], p);
+                off += apq * apq;
+            }
+        if (off < stop) break;
+#pragma unroll
+        for (int p = 0; p < N; ++p)
+#pragma unroll
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = readlane_f64(a[q], p);
+                if (apq != 0) {
+                    const double app = readlane_f64(a[p], p), aqq = readlane_f64(a[q], q);
+                    const double theta = (aqq - app) / (2 * apq);
+                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
+                    const double c = 1 / sqrt(t * t + 1), s = t * c;
+                    {
+                        const double akp = a[p], akq = a[q];
+                        a[p] = c * akp - s * akq;
+                        a[q] = s * akp + c * akq;
+                    }
+                    double rp[N], rq[N];
+#pragma unroll
+                    for (int k = 0; k < N; ++k) { rp[k] = readlane_f64(a[k], p); rq[k] = readlane_f64(a[k], q); }
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        const double apk = rp[k], aqk = rq[k];
+                        if (lane == p) a[k] = c * apk - s * aqk;
+                        if (lane == q) a[k] = s * apk + c * aqk;
+                    }
+                    {
+                        const double vkp = v[p], vkq = v[q];
+                        v[p] = c * vkp - s * vkq;
+                        v[q] = s * vkp + c * vkq;
+                    }
+                }
+            }
+    }
+    int ord[N];
+    double dg[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) { ord[k] = k; dg[k] = readlane_f64(a[k], k); }
+#pragma unroll
+    for (int i = 1; i < N; ++i)
+#pragma unroll
+        for (int j = i; j > 0; --j) {
+            const bool sw = dg[j] < dg[j - 1];
+            const double td = dg[j];
+            const int to = ord[j];
+            dg[j] = sw ? dg[j - 1] : dg[j];
+            ord[j] = sw ? ord[j - 1] : ord[j];
+            dg[j - 1] = sw ? td : dg[j - 1];
+            ord[j - 1] = sw ? to : ord[j - 1];
+        }
+    if (lane < N) {
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            if (lane == c) ev[c] = dg[c];
+            double val = 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) val = ord[c] == k ? v[k] : val;
+            U[c * N + lane] = val;
         }
     }
 }

@@ -103,18 +103,44 @@ def test_too_few_and_weighted_ls(vlp_pairs):
     _check(p, frames)
 
 
-def test_unfused_solver_runs_per_frame(vlp_pairs):
-    """The shipped RANSAC → DRPM solver keeps one launch sequence per frame inside the call (each
-    context continues its own rand() stream): results equal fresh single contexts'."""
-    p = config.params_from_config(config.load())
-    p.iterations = 3
-    frames = [(synth.fps_subsample(q.source, 1500, seed=k), q.target) for k, q in enumerate(vlp_pairs[:2])]
+def _check_fresh(p, frames):
+    """Batched vs each frame alone in a FRESH context (a fresh seeded rand() stream per frame, as the
+    batch's fresh contexts have): pose, iterations, status and trace bit for bit."""
     ref = []
-    for src, tgt in frames:           # a fresh context per frame = a fresh seeded rand() stream
+    for src, tgt in frames:
         ref += _single(p, [(src, tgt)])
-    poses, iters, status, _ = _batched(p, frames)
+    poses, iters, status, traces = _batched(p, frames)
     for k, r in enumerate(ref):
-        assert np.array_equal(r["pose"], poses[k]) and r["iters"] == iters[k] and r["status"] == status[k]
+        assert np.array_equal(r["pose"], poses[k]), (k, np.abs(r["pose"] - poses[k]).max())
+        assert (r["iters"], r["status"]) == (iters[k], status[k]), k
+        assert all(_trace_equal(a, b) for a, b in zip(r["trace"], traces[k])), k
+    return ref
+
+
+@pytest.mark.parametrize("final", [_abi.IMLS_FINAL_DRPM, _abi.IMLS_FINAL_LS, _abi.IMLS_FINAL_WEIGHTED_LS])
+def test_ransac_frames_one_launch(vlp_pairs, final):
+    """The shipped RANSAC → DRPM solver (and RANSAC's LS / weighted-LS finals) through the batched
+    launch: every RANSAC step is one launch for all frames, each frame on its own context's rand()
+    stream; a TOO_FEW frame shares the launch."""
+    p = config.params_from_config(config.load())
+    p.iterations = 4
+    p.ransac_final_method = final
+    frames = [(synth.fps_subsample(q.source, 1300 + 150 * k, seed=k), q.target) for k, q in enumerate(vlp_pairs[:3])]
+    frames.append((vlp_pairs[3].source[:4], vlp_pairs[3].target))
+    ref = _check_fresh(p, frames)
+    assert ref[3]["status"] == _abi.IMLS_FRAME_TOO_FEW
+
+
+def test_ransac_frames_all_chunks(vlp_pairs, hdl_pair):
+    """No early exit (min inliers 100 %): every hypothesis chunk runs (16, 64, 256, …), strided over
+    the batch's blocks; a large frame (grid inlier chain) next to small ones."""
+    p = config.params_from_config(config.load())
+    p.iterations = 2
+    p.ransac_min_inliers_percentage = 1.0
+    p.ransac_max_iterations = 700
+    frames = [(synth.fps_subsample(hdl_pair.source, 6000, seed=7), hdl_pair.target),
+              (synth.fps_subsample(vlp_pairs[0].source, 1500, seed=8), vlp_pairs[0].target)]
+    _check_fresh(p, frames)
 
 
 def test_errors(vlp_pairs):
