@@ -235,12 +235,15 @@ class Pipeline:
         self.prep = prep                  # prep(list of context indices)
         self.offs = bounds[:g]
         self.inflight = [False] * len(self.halves)
+        self.t_wait = self.t_launch = 0.0   # host time in result waits / in register_frames_async
 
     def _collect(self, h):
         if not self.inflight[h]:
             return []
         self.inflight[h] = False
+        t0 = time.perf_counter()
         poses, iters, st, _ = imls_icp.register_frames_result(self.halves[h])
+        self.t_wait += time.perf_counter() - t0
         return list(zip(poses, iters, st))
 
     def step(self):
@@ -248,7 +251,9 @@ class Pipeline:
         for h, half in enumerate(self.halves):
             out += self._collect(h)
             self.prep(range(self.offs[h], self.offs[h] + len(half)))
-            imls_icp.register_frames_async(half)
+            t0 = time.perf_counter()
+            imls_icp.register_frames_async(half)    # builds (after the filter counts) + the batch's launches
+            self.t_launch += time.perf_counter() - t0
             self.inflight[h] = True
         return out
 
@@ -499,12 +504,17 @@ def main():
 
     if hasattr(runner, "t_prep"):
         runner.t_prep = runner.t_reg = 0.0
+    if getattr(runner, "pipe", None):
+        runner.pipe.t_wait = runner.pipe.t_launch = 0.0
     elapsed, per_step, res = timed_steps(runner.step, args.steps, world, dev, torch.cuda.synchronize)
     if getattr(runner, "pipe", None):
         res += runner.pipe.drain()        # the batches still in flight (already finished: synchronized)
     if hasattr(runner, "t_prep"):
         log(f"[rank {rank}] host time per step: uploads (+ filters) {runner.t_prep / args.steps * 1e3:.2f} ms, "
             f"rest (builds, launches, waits) {runner.t_reg / args.steps * 1e3:.2f} ms")
+    if getattr(runner, "pipe", None):
+        log(f"[rank {rank}] pipeline host time per step: result waits {runner.pipe.t_wait / args.steps * 1e3:.2f} ms, "
+            f"register_frames_async (builds + launches) {runner.pipe.t_launch / args.steps * 1e3:.2f} ms")
     poses = [r[0] for r in res]
     allp, traj = exchange_poses(poses, world)          # the one RCCL exchange (trajectory chaining)
     n_pairs = args.steps * P

@@ -238,7 +238,7 @@ void launch_tensor_gather(hipStream_t s, const float* ten6_in, size_t n_in, cons
                           float4* mten);
 
 // ransac.hip — RANSAC (+ final LS / weighted LS / DRPM) and the solve-method dispatcher
-constexpr int kHypMax = 4096;          // hypotheses per chunk (chunks grow 16, 64, 256, 1024, 4096)
+constexpr int kHypMax = 8192;          // hypotheses per chunk (chunks: 16, then up to kHypMax each)
 struct RansacParams {
     int max_iterations;
     double distance_threshold, min_inliers_percentage, huber_threshold;

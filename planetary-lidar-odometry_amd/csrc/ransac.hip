@@ -6,12 +6,12 @@
 //   1. the valid correspondences (float rows, source order) are compacted, order kept, into fp64
 //      rows S/D/N — the reference's std::vector<Vector3d> inputs; the TOO_FEW gate
 //      (laser_odometry.cpp:570-576) runs on their count;
-//   2. hypotheses in growing chunks (16, 64, 256, 1024, 4096): k_ransac_begin / k_ransac_select
-//      replay glibc rand() (one draw per hypothesis of the next chunk: the FPS start index),
-//      k_ransac_hyp runs one hypothesis per block at a time — FPS (two arg-max passes, first index wins ties as the sequential `>` does), the 3×6
-//      column-pivoted Householder QR basic solution (Eigen ColPivHouseholderQR, not normal
-//      equations: a rank-3 system squared would misjudge the rank), Δ, and the inlier count;
-//      k_ransac_select scans the chunk in order with the reference's strict `>` and early exit
+//   2. hypotheses in chunks (16, then up to kHypMax): k_ransac_hyp runs one hypothesis per block at
+//      a time — its glibc rand() draw (the FPS start index) by the jump table below, FPS (two
+//      arg-max passes, first index wins ties as the sequential `>` does), the 3×6 column-pivoted
+//      Householder QR basic solution (Eigen ColPivHouseholderQR, not normal equations: a rank-3
+//      system squared would misjudge the rank), Δ, and the inlier count; k_ransac_select (one
+//      wave) scans the chunk in order with the reference's strict `>` and early exit
 //      (best > ⌊pct·N⌋) and commits exactly the draws consumed; later chunks return at once;
 //   3. inliers of the best Δ are compacted (order kept) with weights
 //      w = √a < h₂ ? a : 2h₂√a − h₂², a = e^{−|r|}, h₂ = huber·distance (solver.cpp:334-356),
@@ -33,8 +33,12 @@
 namespace imlsgpu {
 namespace {
 
-constexpr int kHypBlock = 256;
-constexpr int kHypGrid = 2048;        // batched hypothesis grid (blocks stride over the running frames' items)
+// threads per hypothesis: one wave for small frames (its serial part — QR, Δ by one lane — then
+// overlaps with other hypotheses on the same CU instead of idling three more waves), four for
+// large ones (the three passes over the rows dominate).  Exact either way (arg-max and counts).
+constexpr int kHypSmallRows = 4096;
+__host__ __device__ constexpr int hyp_block_of(int cap) { return cap <= kHypSmallRows ? 64 : 256; }
+constexpr int kHypGrid = 8192;        // batched hypothesis grid (blocks stride over the running frames' items)
 constexpr int kDrpmSlab = 42;         // 36 noise-mean terms + 6 variance terms per block
 
 // ---------------------------------------------------------------------------------------------
@@ -152,9 +156,49 @@ __device__ __forceinline__ void compact_count_body(const Source& src, int n, int
     }
 }
 
+// What runs after a compaction, by thread 0 with the kept count (one launch fewer each): the RANSAC
+// begin (the TOO_FEW gate, laser_odometry.cpp:570-576, and the selection reset) after the valid-row
+// compaction; the empty-inlier check after the inlier one.
+struct CompactPost {
+    int kind;                         // 0 none, 1 RANSAC begin, 2 inlier check
+    int correspond_number, update_pose;
+    SolveState st;
+    imls_iter_trace* tr;
+    RansacDev R;
+};
+__device__ __forceinline__ void ransac_begin_t0(int n, int correspond_number, int update_pose, const SolveState& st,
+                                                imls_iter_trace* tr, const RansacDev& R) {
+    *R.active = 1;
+    if (update_pose && n < correspond_number) {
+        *st.status = IMLS_FRAME_TOO_FEW;
+        *st.done = 1;
+        if (tr) tr->n_valid = (unsigned long long)n;
+        return;
+    }
+    *R.best = 0;
+    *R.evaluated = 0;
+    *R.rdone = n < 3 ? 1 : 0;   // FPS needs three distinct points
+#pragma unroll
+    for (int k = 0; k < 16; ++k) R.bestT[k] = (k % 5 == 0) ? 1.0 : 0.0;
+}
+__device__ __forceinline__ void compact_post(const CompactPost& P, int n) {
+    if (P.kind == 1) {
+        ransac_begin_t0(n, P.correspond_number, P.update_pose, P.st, P.tr, P.R);
+    } else if (P.kind == 2 && n == 0) {   // nothing to solve on (the oracle's N == 0 → false): a failed solve
+        *P.st.status = IMLS_FRAME_SOLVE_FAILED;
+        *P.st.done = 1;
+    }
+}
+// a finished frame skips the compaction; its RANSAC solve is then inactive (no trace record)
+__device__ __forceinline__ bool compact_skip(const CompactPost& P) {
+    if (!*P.st.done) return false;
+    if (P.kind == 1 && threadIdx.x == 0) *P.R.active = 0;
+    return true;
+}
+
 // One block: exclusive scan of the block counts (in place), total count and Σw in fixed order.
 __device__ __forceinline__ void compact_scan_body(int* __restrict__ blkcnt, const double* __restrict__ blkw, int nb,
-                                                  const CompactOut& out) {
+                                                  const CompactOut& out, const CompactPost& P) {
     __shared__ int sc[1024];
     __shared__ double sw[1024];
     int carry = 0;
@@ -185,6 +229,59 @@ __device__ __forceinline__ void compact_scan_body(int* __restrict__ blkcnt, cons
     if (threadIdx.x == 0) {
         *out.count = carry;
         if (out.wsum) *out.wsum = wcarry;
+        compact_post(P, carry);
+    }
+}
+
+// The whole compaction in one 1024-thread block (count + scan + scatter, for caps ≤ kCompactOne):
+// tiles of 1024 rows in order; Σw accumulated exactly as the three-kernel path does it (per-wave
+// sums, 4 waves per 256-row block in order, then the block sums in block order) — same bits.
+constexpr int kCompactOne = 16384;
+__device__ __forceinline__ void compact_one_body(const Source& src, int n, const CompactOut& out, const CompactPost& P) {
+    __shared__ int wc[16];
+    __shared__ double ws[16];
+    __shared__ int sbase;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) sbase = 0;
+    double wacc = 0.0;                                     // thread 0
+    for (int tile = 0; tile < n; tile += 1024) {
+        const int i = tile + t;
+        double s[3], d[3], nn[3], w = 0.0;
+        const bool keep = i < n && src.get(i, s, d, nn, w);
+        const unsigned long long m = __ballot(keep);
+        const double wvs = wave_sum(keep ? w : 0.0);
+        if (lane == 0) { wc[wv] = __popcll(m); ws[wv] = wvs; }
+        __syncthreads();
+        int off = sbase;
+        for (int k = 0; k < wv; ++k) off += wc[k];
+        off += __popcll(m & ((1ull << lane) - 1ull));
+        if (keep) {
+            const size_t c3 = 3 * (size_t)out.cap, o = (size_t)off;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                out.rows[3 * o + k] = s[k];
+                out.rows[c3 + 3 * o + k] = d[k];
+                out.rows[2 * c3 + 3 * o + k] = nn[k];
+            }
+            out.rows[3 * c3 + o] = w;
+        }
+        __syncthreads();
+        if (t == 0) {
+            int tot = 0;
+            for (int b = 0; b < 4; ++b) {
+                if (tile + 256 * b >= n) break;            // blocks past n do not exist in the 3-kernel path
+                double sw = 0.0;
+                for (int k = 0; k < 4; ++k) { sw += ws[4 * b + k]; tot += wc[4 * b + k]; }
+                wacc += sw;
+            }
+            sbase += tot;
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        *out.count = sbase;
+        if (out.wsum) *out.wsum = wacc;
+        compact_post(P, sbase);
     }
 }
 
@@ -219,9 +316,13 @@ __global__ __launch_bounds__(kBlock) void k_compact_count(Source src, int n, int
     compact_count_body(src, n, blkcnt, blkw);
 }
 __global__ __launch_bounds__(1024) void k_compact_scan(int* __restrict__ blkcnt, const double* __restrict__ blkw, int nb,
-                                                       CompactOut out, const int* __restrict__ done) {
-    if (done && *done) return;
-    compact_scan_body(blkcnt, blkw, nb, out);
+                                                       CompactOut out, CompactPost P) {
+    if (compact_skip(P)) return;
+    compact_scan_body(blkcnt, blkw, nb, out, P);
+}
+__global__ __launch_bounds__(1024) void k_compact_one(Source src, int n, CompactOut out, CompactPost P) {
+    if (compact_skip(P)) return;
+    compact_one_body(src, n, out, P);
 }
 __global__ __launch_bounds__(kBlock) void k_compact_scatter(Source src, int n, const int* __restrict__ blkoff, CompactOut out,
                                                             const int* __restrict__ done) {
@@ -254,13 +355,28 @@ __global__ __launch_bounds__(kBlock) void k_compact_count_b(const PairDev* __res
     if ((int)blockIdx.x >= (n + kBlock - 1) / kBlock || *A.st.done) return;
     compact_count_body(src, n, A.rf.blkcnt, A.rf.blkw);
 }
-__global__ __launch_bounds__(1024) void k_compact_scan_b(const PairDev* __restrict__ tab, int mode) {
+__device__ __forceinline__ CompactPost frame_post(const PairDev& A, int mode, int correspond_number, int it) {
+    return CompactPost{mode == 0 ? 1 : 2, correspond_number, 1, A.st, A.trace + it, A.rf.R};
+}
+__global__ __launch_bounds__(1024) void k_compact_scan_b(const PairDev* __restrict__ tab, int mode, int correspond_number,
+                                                         int it) {
     const PairDev A = tab[blockIdx.y];
-    if (*A.st.done) return;
+    const CompactPost P = frame_post(A, mode, correspond_number, it);
+    if (compact_skip(P)) return;
     Source src;
     CompactOut out;
     const int n = frame_compact(A, mode, 0.0, 0.0, src, out);
-    compact_scan_body(A.rf.blkcnt, A.rf.blkw, (n + kBlock - 1) / kBlock, out);
+    compact_scan_body(A.rf.blkcnt, A.rf.blkw, (n + kBlock - 1) / kBlock, out, P);
+}
+__global__ __launch_bounds__(1024) void k_compact_one_b(const PairDev* __restrict__ tab, int mode, double dist_thr, double h2,
+                                                        int correspond_number, int it) {
+    const PairDev A = tab[blockIdx.y];
+    const CompactPost P = frame_post(A, mode, correspond_number, it);
+    if (compact_skip(P)) return;
+    Source src;
+    CompactOut out;
+    const int n = frame_compact(A, mode, dist_thr, h2, src, out);
+    compact_one_body(src, n, out, P);
 }
 __global__ __launch_bounds__(kBlock) void k_compact_scatter_b(const PairDev* __restrict__ tab, int mode, double dist_thr,
                                                               double h2) {
@@ -281,31 +397,16 @@ __global__ void k_set_count(int* __restrict__ c, int v) {
     if (threadIdx.x == 0) *c = v;
 }
 
-// gate on the compacted count, reset the RANSAC selection state
-__device__ __forceinline__ void ransac_begin_body(const int* __restrict__ count, int correspond_number, int update_pose,
-                                                  const SolveState& st, imls_iter_trace* tr, const RansacDev& R) {
-    if (threadIdx.x) return;
-    *R.active = *st.done ? 0 : 1;
-    if (*st.done) return;
-    const int n = *count;
-    if (update_pose && n < correspond_number) {
-        *st.status = IMLS_FRAME_TOO_FEW;
-        *st.done = 1;
-        if (tr) tr->n_valid = (unsigned long long)n;
-        return;
-    }
-    *R.best = 0;
-    *R.evaluated = 0;
-    *R.rdone = n < 3 ? 1 : 0;   // FPS needs three distinct points
-#pragma unroll
-    for (int k = 0; k < 16; ++k) R.bestT[k] = (k % 5 == 0) ? 1.0 : 0.0;
-}
+// gate on the count, reset the RANSAC selection state (host fp64 rows, no compaction to fold it into)
 __global__ void k_ransac_begin(const int* __restrict__ count, int correspond_number, int update_pose, SolveState st,
                                imls_iter_trace* tr, RansacDev R) {
-    ransac_begin_body(count, correspond_number, update_pose, st, tr, R);
+    if (threadIdx.x) return;
+    if (*st.done) { *R.active = 0; return; }
+    ransac_begin_t0(*count, correspond_number, update_pose, st, tr, R);
 }
 
 // block arg-max of (value, index): larger value, then smaller index
+template <int NT>
 __device__ __forceinline__ void argmax_pair(double& v, int& i, double* sv, int* si) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -317,7 +418,7 @@ __device__ __forceinline__ void argmax_pair(double& v, int& i, double* sv, int* 
     if (lane == 0) { sv[wv] = v; si[wv] = i; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int k = 1; k < kHypBlock / 64; ++k)
+        for (int k = 1; k < NT / 64; ++k)
             if (sv[k] > sv[0] || (sv[k] == sv[0] && si[k] < si[0])) { sv[0] = sv[k]; si[0] = si[k]; }
     }
     __syncthreads();
@@ -470,33 +571,34 @@ __device__ void colpiv_qr_small(double A[RR][6], double b[RR], double x[6]) {
 
 // Hypothesis h of the current chunk, by one block: its draw (the FPS start) from the committed
 // rand() state, FPS(3), the 3×6 QR, Δ, its inlier count.
+template <int NT>
 __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, const double* __restrict__ Dp,
                                                const double* __restrict__ Np, int n, const RansacDev& R,
                                                double dist_thr, int h) {
-    __shared__ double sv[kHypBlock / 64];
-    __shared__ int si[kHypBlock / 64];
+    __shared__ double sv[NT / 64];
+    __shared__ int si[NT / 64];
     __shared__ double T[16];
-    __shared__ int cnt_s[kHypBlock / 64];
+    __shared__ int cnt_s[NT / 64];
     const int f0 = (int)(rand_word_ahead(R.rng, h) >> 1) % n;   // rand() % n (solver.cpp / common.cpp:49)
     // pass 1: farthest from f0 (common.cpp:48-66: strict `>` from −1, taken points skipped)
     double bv = -1.0;
     int bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < n; i += kHypBlock) {
+    for (int i = threadIdx.x; i < n; i += NT) {
         if (i == f0) continue;
         const double md = pdist(S, f0, i);
         if (md > bv) { bv = md; bi = i; }
     }
-    argmax_pair(bv, bi, sv, si);
+    argmax_pair<NT>(bv, bi, sv, si);
     const int f1 = bi;
     // pass 2: farthest from {f0, f1} by the running minimum distance
     bv = -1.0;
     bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < n; i += kHypBlock) {
+    for (int i = threadIdx.x; i < n; i += NT) {
         if (i == f0 || i == f1) continue;
         const double md = fmin(pdist(S, f0, i), pdist(S, f1, i));
         if (md > bv) { bv = md; bi = i; }
     }
-    argmax_pair(bv, bi, sv, si);
+    argmax_pair<NT>(bv, bi, sv, si);
     const int f2 = bi;
     if (threadIdx.x == 0) {
         const int id[3] = {f0, f1, f2};
@@ -523,7 +625,7 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
     }
     __syncthreads();
     int c = 0;
-    for (int i = threadIdx.x; i < n; i += kHypBlock) {
+    for (int i = threadIdx.x; i < n; i += NT) {
         const size_t i3 = 3 * (size_t)i;
         const double s0 = S[i3], s1 = S[i3 + 1], s2 = S[i3 + 2];
         double tp[3];
@@ -538,19 +640,20 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
     __syncthreads();
     if (threadIdx.x == 0) {
         int tot = 0;
-        for (int k = 0; k < kHypBlock / 64; ++k) tot += cnt_s[k];
+        for (int k = 0; k < NT / 64; ++k) tot += cnt_s[k];
         R.counts[h] = tot;
     }
     if (threadIdx.x < 16) R.T[(size_t)h * 16 + threadIdx.x] = T[threadIdx.x];
 }
 // one frame: hypotheses blockIdx.x, blockIdx.x + gridDim.x, … of the chunk
-__global__ __launch_bounds__(kHypBlock) void k_ransac_hyp(const double* __restrict__ rows, const int* __restrict__ count,
-                                                          int cap, RansacDev R, double dist_thr, int chunk,
-                                                          const int* __restrict__ done) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ransac_hyp(const double* __restrict__ rows, const int* __restrict__ count,
+                                                   int cap, RansacDev R, double dist_thr, int chunk,
+                                                   const int* __restrict__ done) {
     if (*done || *R.rdone) return;
     const int n = *count;
     const size_t c3 = 3 * (size_t)cap;
-    for (int h = blockIdx.x; h < chunk; h += gridDim.x) ransac_hyp_one(rows, rows + c3, rows + 2 * c3, n, R, dist_thr, h);
+    for (int h = blockIdx.x; h < chunk; h += gridDim.x) ransac_hyp_one<NT>(rows, rows + c3, rows + 2 * c3, n, R, dist_thr, h);
 }
 
 // Sequential semantics of the hypothesis loop (solver.cpp:244-326) over one chunk, by one wave: the
@@ -599,13 +702,6 @@ __global__ void k_ransac_trace(const int* __restrict__ count_all, RansacDev R, i
     tr->n_kept = 0;
 }
 
-__global__ void k_ransac_check_inliers(const int* __restrict__ count_in, SolveState st, imls_iter_trace* tr) {
-    if (threadIdx.x || *st.done) return;
-    if (*count_in == 0) {   // nothing to solve on (the oracle's N == 0 → false): stop like a failed solve
-        *st.status = IMLS_FRAME_SOLVE_FAILED;
-        *st.done = 1;
-    }
-}
 
 // ---------------------------------------------------------------------------------------------
 // DRPM (solver.cpp:499-603, degeneracy.h:14-131)
@@ -804,37 +900,44 @@ __global__ __launch_bounds__(256) void k_drpm_eig(const double* __restrict__ par
 __global__ __launch_bounds__(kBlock) void k_drpm_noise(Rows rows, int N, SolveState st, DrpmDev Dv, double sp, double sn) {
     drpm_noise_body(rows, N, st, Dv, sp, sn);
 }
+// rtr: RANSAC's own trace record (n_valid = correspondences, n_kept = 0) when the solve was active,
+// written after the final solve's; null for the stand-alone DRPM
+__device__ __forceinline__ void ransac_trace_t0(const RansacDev& R, const int* __restrict__ count_all, imls_iter_trace* rtr) {
+    if (threadIdx.x == 0 && rtr && *R.active) {
+        rtr->n_valid = (unsigned long long)*count_all;
+        rtr->n_kept = 0;
+    }
+}
 __global__ __launch_bounds__(256) void k_drpm_final(int blocks, SolveState st, DrpmDev Dv, imls_iter_trace* tr, KParams kp,
                                                     double threshold, const int* __restrict__ count_all,
-                                                    const int* __restrict__ count_in, int update_pose) {
+                                                    const int* __restrict__ count_in, int update_pose, RansacDev R,
+                                                    imls_iter_trace* rtr) {
     drpm_final_body(blocks, st, Dv, tr, kp, threshold, count_all, count_in, update_pose);
+    ransac_trace_t0(R, count_all, rtr);
 }
 
 // ---------------------------------------------------------------------------------------------
 // Batched RANSAC / DRPM kernels (launch_ransac_batch): frame = tab[blockIdx.y], the same bodies as
 // the one-frame kernels above; the frame's RANSAC scratch is A.rf, its pose update always on.
 // ---------------------------------------------------------------------------------------------
-__global__ void k_ransac_begin_b(const PairDev* __restrict__ tab, int correspond_number, int it) {
-    const PairDev A = tab[blockIdx.y];
-    ransac_begin_body(A.rf.cnt_all, correspond_number, 1, A.st, A.trace + it, A.rf.R);
-}
 // The chunk's hypotheses of the frames still running, spread evenly over the grid: each block first
 // lists the running frames (done / RANSAC-finished ones drop out), then strides over
 // (frame, hypothesis) items — one frame without an early exit gets the whole grid, not a slice.
-__global__ __launch_bounds__(kHypBlock) void k_ransac_hyp_b(const PairDev* __restrict__ tab, int npairs, int chunk,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ransac_hyp_b(const PairDev* __restrict__ tab, int npairs, int chunk,
                                                             double dist_thr) {
     __shared__ int sact[kMaxRansacBatch];
-    __shared__ int swc[kHypBlock / 64];
+    __shared__ int swc[NT / 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     int na = 0;
-    for (int base = 0; base < npairs; base += kHypBlock) {
+    for (int base = 0; base < npairs; base += NT) {
         bool act = false;
         if (base + t < npairs) act = !*tab[base + t].st.done && !*tab[base + t].rf.R.rdone;
         const unsigned long long m = __ballot(act);
         if (lane == 0) swc[wv] = __popcll(m);
         __syncthreads();
         int off = na, tot = na;
-        for (int k = 0; k < kHypBlock / 64; ++k) {
+        for (int k = 0; k < NT / 64; ++k) {
             off += k < wv ? swc[k] : 0;
             tot += swc[k];
         }
@@ -848,7 +951,7 @@ __global__ __launch_bounds__(kHypBlock) void k_ransac_hyp_b(const PairDev* __res
         const int h = (int)(q / na);
         const PairDev A = tab[fr];
         const size_t c3 = 3 * (size_t)A.rf.cap;
-        ransac_hyp_one(A.rf.all, A.rf.all + c3, A.rf.all + 2 * c3, *A.rf.cnt_all, A.rf.R, dist_thr, h);
+        ransac_hyp_one<NT>(A.rf.all, A.rf.all + c3, A.rf.all + 2 * c3, *A.rf.cnt_all, A.rf.R, dist_thr, h);
     }
 }
 __global__ __launch_bounds__(64) void k_ransac_select_b(const PairDev* __restrict__ tab, int chunk, int max_iterations,
@@ -857,14 +960,8 @@ __global__ __launch_bounds__(64) void k_ransac_select_b(const PairDev* __restric
     if (*A.st.done || *A.rf.R.rdone) return;
     ransac_select_body(A.rf.cnt_all, A.rf.R, chunk, max_iterations, min_pct);
 }
-__global__ void k_ransac_check_inliers_b(const PairDev* __restrict__ tab) {
-    const PairDev A = tab[blockIdx.y];
-    if (threadIdx.x || *A.st.done) return;
-    if (*A.rf.cnt_in == 0) {
-        *A.st.status = IMLS_FRAME_SOLVE_FAILED;
-        *A.st.done = 1;
-    }
-}
+// trace of a RANSAC iteration as the oracle records it (n_valid = correspondences, n_kept = 0) —
+// LS / weighted-LS finals; the DRPM final writes it itself
 __global__ void k_ransac_trace_b(const PairDev* __restrict__ tab, int it) {
     const PairDev A = tab[blockIdx.y];
     if (threadIdx.x || !*A.rf.R.active) return;
@@ -883,14 +980,17 @@ __global__ __launch_bounds__(kBlock) void k_drpm_noise_b(const PairDev* __restri
 __global__ __launch_bounds__(256) void k_drpm_final_b(const PairDev* __restrict__ tab, KParams kp, double threshold, int it) {
     const PairDev A = tab[blockIdx.y];
     drpm_final_body(solve_blocks_of(A.rf.cap), A.st, A.rf.Dv, A.trace + it, kp, threshold, A.rf.cnt_all, A.rf.cnt_in, 1);
+    ransac_trace_t0(A.rf.R, A.rf.cnt_all, A.trace + it);
 }
 
-// chunk sizes of the hypothesis loop: 16, 64, 256, 1024, then kHypMax, up to max_iterations in all
+// chunk sizes of the hypothesis loop: 16 (the usual early exit: the shipped 95 % inlier bar is mostly
+// met by the first hypotheses), 256, then the rest in chunks of kHypMax — three chunks for
+// max_iterations ≤ kHypMax + 272.  (Results do not depend on the chunking: exactly the draws
+// consumed are committed.)
 std::vector<int> ransac_chunks(int max_iterations) {
     std::vector<int> v;
-    int started = 0;
-    for (long long chunk = 16; started < max_iterations; chunk *= 4) {
-        const int cn = (int)std::min<long long>(std::min<long long>(chunk, kHypMax), max_iterations - started);
+    for (int started = 0; started < max_iterations;) {
+        const int cn = std::min(started == 0 ? 16 : started == 16 ? 256 : kHypMax, max_iterations - started);
         v.push_back(cn);
         started += cn;
     }
@@ -930,7 +1030,8 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
         launch_rows_pass1(s, rows, cap, L.st.partial1, b1);
         k_drpm_eig<<<1, 256, 0, s>>>(L.st.partial1, b1, L.st, Dv);
         k_drpm_noise<<<b1, kBlock, 0, s>>>(rows, cap, L.st, Dv, L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals);
-        k_drpm_final<<<1, 256, 0, s>>>(b1, L.st, Dv, L.tr, kp, L.ransac.drpm_threshold, cnt, cnt, L.update_pose);
+        k_drpm_final<<<1, 256, 0, s>>>(b1, L.st, Dv, L.tr, kp, L.ransac.drpm_threshold, cnt, cnt, L.update_pose,
+                                       RansacDev{}, nullptr);
         return;
     }
     if (kp.solve_method != IMLS_SOLVE_RANSAC) {
@@ -945,27 +1046,39 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
     const RansacDev& R = F.R;
     const int* done = L.st.done;
 
-    // 1. compact the valid correspondences (fp64 rows from the host API are already compact)
-    Source src{};
-    CompactOut out{F.all, F.cnt_all, nullptr, cap};
+    // one compaction (valid rows → all, or inliers → inl) with its post step folded in
+    auto compact = [&](const Source& src, int n, const CompactOut& out, int kind) {
+        const CompactPost P{kind, kp.correspond_number, L.update_pose, L.st, L.tr, R};
+        if (cap <= kCompactOne) {
+            k_compact_one<<<1, 1024, 0, s>>>(src, n, out, P);
+        } else {
+            k_compact_count<<<nb, kBlock, 0, s>>>(src, n, F.blkcnt, F.blkw, done);
+            k_compact_scan<<<1, 1024, 0, s>>>(F.blkcnt, F.blkw, nb, out, P);
+            k_compact_scatter<<<nb, kBlock, 0, s>>>(src, n, F.blkcnt, out, done);
+        }
+    };
+
+    // 1. compact the valid correspondences (fp64 rows from the host API are already compact), then
+    //    the count gate and the selection reset
     if (!L.rows_are_double) {
+        Source src{};
         src.cs = L.cs; src.cd = L.cd; src.cn = L.cn;
-        k_compact_count<<<nb, kBlock, 0, s>>>(src, L.N, F.blkcnt, F.blkw, done);
-        k_compact_scan<<<1, 1024, 0, s>>>(F.blkcnt, F.blkw, nb, out, done);
-        k_compact_scatter<<<nb, kBlock, 0, s>>>(src, L.N, F.blkcnt, out, done);
+        compact(src, L.N, CompactOut{F.all, F.cnt_all, nullptr, cap}, 1);
     } else {
         (void)hipMemcpyAsync(F.all, L.rows_d, 9 * c * 8, hipMemcpyDeviceToDevice, s);
         k_set_count<<<1, 64, 0, s>>>(F.cnt_all, L.N);
+        k_ransac_begin<<<1, 64, 0, s>>>(F.cnt_all, kp.correspond_number, L.update_pose, L.st, L.tr, R);
     }
-    // 2. hypotheses in growing chunks
-    const std::vector<int> chunks = ransac_chunks(L.ransac.max_iterations);
-    k_ransac_begin<<<1, 64, 0, s>>>(F.cnt_all, kp.correspond_number, L.update_pose, L.st, L.tr, R);
-    for (const int cn : chunks) {
-        k_ransac_hyp<<<cn, kHypBlock, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done);
+    // 2. hypotheses in chunks
+    for (const int cn : ransac_chunks(L.ransac.max_iterations)) {
+        if (hyp_block_of(cap) == 64)
+            k_ransac_hyp<64><<<cn, 64, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done);
+        else
+            k_ransac_hyp<256><<<cn, 256, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done);
         k_ransac_select<<<1, 64, 0, s>>>(F.cnt_all, R, cn, L.ransac.max_iterations, L.ransac.min_inliers_percentage, done);
     }
 
-    // 3. inliers of the best Δ with their Huber-like weights (order kept), Σw
+    // 3. inliers of the best Δ with their Huber-like weights (order kept), Σw; an empty set stops
     Source isrc{};
     isrc.rows = F.all;
     isrc.count = F.cnt_all;
@@ -973,13 +1086,9 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
     isrc.T = R.bestT;
     isrc.dist_thr = L.ransac.distance_threshold;
     isrc.h2 = L.ransac.huber_threshold * L.ransac.distance_threshold;
-    CompactOut iout{F.inl, F.cnt_in, F.wsum, cap};
-    k_compact_count<<<nb, kBlock, 0, s>>>(isrc, cap, F.blkcnt, F.blkw, done);
-    k_compact_scan<<<1, 1024, 0, s>>>(F.blkcnt, F.blkw, nb, iout, done);
-    k_compact_scatter<<<nb, kBlock, 0, s>>>(isrc, cap, F.blkcnt, iout, done);
-    k_ransac_check_inliers<<<1, 64, 0, s>>>(F.cnt_in, L.st, L.tr);
+    compact(isrc, cap, CompactOut{F.inl, F.cnt_in, F.wsum, cap}, 2);
 
-    // 4. final solve on the inliers
+    // 4. final solve on the inliers (+ RANSAC's own trace record)
     KParams fk = kp;
     fk.correspond_number = 0;                       // the count gate ran before RANSAC
     double* inl = F.inl;
@@ -989,20 +1098,22 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
             fk.solve_method = IMLS_SOLVE_LS;
             fk.ls_threshold = L.ransac.ls_threshold;
             launch_solve_chain(s, cap, 0, fk, nullptr, nullptr, nullptr, inl, nullptr, st, L.tr, L.update_pose, 1, F.cnt_in, nullptr);
+            if (L.tr) k_ransac_trace<<<1, 64, 0, s>>>(F.cnt_all, R, L.tr);
             break;
         case IMLS_FINAL_WEIGHTED_LS:
             fk.solve_method = IMLS_SOLVE_WEIGHTED_LS;
             launch_solve_chain(s, cap, 0, fk, nullptr, nullptr, nullptr, inl, inl + 9 * c, st, L.tr, L.update_pose, 1, F.cnt_in, F.wsum);
+            if (L.tr) k_ransac_trace<<<1, 64, 0, s>>>(F.cnt_all, R, L.tr);
             break;
         default: {   // DRPM
             const int b1 = solve_blocks(cap);
             launch_rows_pass1(s, rows, cap, L.st.partial1, b1);
             k_drpm_eig<<<1, 256, 0, s>>>(L.st.partial1, b1, L.st, F.Dv);
             k_drpm_noise<<<b1, kBlock, 0, s>>>(rows, cap, L.st, F.Dv, L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals);
-            k_drpm_final<<<1, 256, 0, s>>>(b1, L.st, F.Dv, L.tr, fk, L.ransac.drpm_threshold, F.cnt_all, F.cnt_in, L.update_pose);
+            k_drpm_final<<<1, 256, 0, s>>>(b1, L.st, F.Dv, L.tr, fk, L.ransac.drpm_threshold, F.cnt_all, F.cnt_in, L.update_pose,
+                                           R, L.tr);
         }
     }
-    if (L.tr) k_ransac_trace<<<1, 64, 0, s>>>(F.cnt_all, R, L.tr);
 }
 
 RansacFrame ransac_frame(void* scratch, int cap, int* rng) {
@@ -1047,22 +1158,30 @@ void launch_ransac_batch(hipStream_t s, const PairDev* tab, const int* n_host, i
     }
     const dim3 gc((maxc + kBlock - 1) / kBlock, npairs), g1(1, npairs);
     const double h2 = rp.huber_threshold * rp.distance_threshold;
+    // one compaction per frame (mode 0: valid rows → all, then the count gate and selection reset;
+    // mode 1: the inliers of the best Δ, then the empty-set check)
+    auto compact = [&](int mode, double dt, double hh) {
+        if (maxc <= kCompactOne) {
+            k_compact_one_b<<<g1, 1024, 0, s>>>(tab, mode, dt, hh, kp.correspond_number, it);
+        } else {
+            k_compact_count_b<<<gc, kBlock, 0, s>>>(tab, mode, dt, hh);
+            k_compact_scan_b<<<g1, 1024, 0, s>>>(tab, mode, kp.correspond_number, it);
+            k_compact_scatter_b<<<gc, kBlock, 0, s>>>(tab, mode, dt, hh);
+        }
+    };
     // 1. every frame's valid correspondences, compacted (order kept) to fp64
-    k_compact_count_b<<<gc, kBlock, 0, s>>>(tab, 0, 0.0, 0.0);
-    k_compact_scan_b<<<g1, 1024, 0, s>>>(tab, 0);
-    k_compact_scatter_b<<<gc, kBlock, 0, s>>>(tab, 0, 0.0, 0.0);
+    compact(0, 0.0, 0.0);
     // 2. hypotheses: each chunk's items of the still-running frames spread over one grid
-    const std::vector<int> chunks = ransac_chunks(rp.max_iterations);
-    k_ransac_begin_b<<<g1, 64, 0, s>>>(tab, kp.correspond_number, it);
-    for (const int cn : chunks) {
-        k_ransac_hyp_b<<<std::min(cn * npairs, kHypGrid), kHypBlock, 0, s>>>(tab, npairs, cn, rp.distance_threshold);
+    for (const int cn : ransac_chunks(rp.max_iterations)) {
+        const int grid = std::min(cn * npairs, kHypGrid);
+        if (hyp_block_of(maxc) == 64)
+            k_ransac_hyp_b<64><<<grid, 64, 0, s>>>(tab, npairs, cn, rp.distance_threshold);
+        else
+            k_ransac_hyp_b<256><<<grid, 256, 0, s>>>(tab, npairs, cn, rp.distance_threshold);
         k_ransac_select_b<<<g1, 64, 0, s>>>(tab, cn, rp.max_iterations, rp.min_inliers_percentage);
     }
     // 3. inliers of each frame's best Δ with their weights
-    k_compact_count_b<<<gc, kBlock, 0, s>>>(tab, 1, rp.distance_threshold, h2);
-    k_compact_scan_b<<<g1, 1024, 0, s>>>(tab, 1);
-    k_compact_scatter_b<<<gc, kBlock, 0, s>>>(tab, 1, rp.distance_threshold, h2);
-    k_ransac_check_inliers_b<<<g1, 64, 0, s>>>(tab);
+    compact(1, rp.distance_threshold, h2);
     // 4. final solve
     KParams fk = kp;
     fk.correspond_number = 0;
@@ -1080,9 +1199,9 @@ void launch_ransac_batch(hipStream_t s, const PairDev* tab, const int* n_host, i
             launch_rows_pass1_batch(s, tab, caps.data(), npairs, 1);
             k_drpm_eig_b<<<g1, 256, 0, s>>>(tab);
             k_drpm_noise_b<<<dim3(solve_blocks_of(maxc), npairs), kBlock, 0, s>>>(tab, rp.drpm_stdev_points, rp.drpm_stdev_normals);
-            k_drpm_final_b<<<g1, 256, 0, s>>>(tab, fk, rp.drpm_threshold, it);
+            k_drpm_final_b<<<g1, 256, 0, s>>>(tab, fk, rp.drpm_threshold, it);   // + RANSAC's trace record
     }
-    k_ransac_trace_b<<<g1, 64, 0, s>>>(tab, it);
+    if (rp.final_method == IMLS_FINAL_LS || rp.final_method == IMLS_FINAL_WEIGHTED_LS) k_ransac_trace_b<<<g1, 64, 0, s>>>(tab, it);
 }
 
 int ransac_init_tables(int device) {

@@ -141,6 +141,9 @@ def test_ransac_frames_all_chunks(vlp_pairs, hdl_pair):
     frames = [(synth.fps_subsample(hdl_pair.source, 6000, seed=7), hdl_pair.target),
               (synth.fps_subsample(vlp_pairs[0].source, 1500, seed=8), vlp_pairs[0].target)]
     _check_fresh(p, frames)
+    # a frame above the one-block compaction size (three-kernel compaction for the whole batch)
+    frames.append((synth.fps_subsample(hdl_pair.source, 20000, seed=9), hdl_pair.target))
+    _check_fresh(p, frames)
 
 
 def test_errors(vlp_pairs):
