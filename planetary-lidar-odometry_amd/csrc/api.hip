@@ -93,6 +93,11 @@ struct imls_ctx {
     bool batch_pending = false, batch_fused = false, batch_traces = false;
     bool batch_member = false;            // part of a pending batch (as lead or member)
     hipEvent_t ev_batch = nullptr;
+    // batched index builds of a batch's members (build_batch): scratch, job table, pinned staging
+    DevBuf bscratch, btable;
+    void* h_btable = nullptr;
+    size_t h_btable_bytes = 0;
+    hipEvent_t ev_build = nullptr;
     // traversal / neighbour counters (imls_traversal_stats): off by default — their per-wave
     // device-scope atomics onto a few shared words cost ~60 µs per projection at config B
     bool collect_stats = false;
@@ -177,6 +182,8 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_VERLET")) k.verlet = k.qverlet = std::atoi(w);
     k.lockstep = 1;
     if (const char* w = std::getenv("IMLS_LOCKSTEP")) k.lockstep = std::atoi(w);
+    k.bcast_lock = 0;
+    if (const char* w = std::getenv("IMLS_BCAST_LOCK")) k.bcast_lock = std::atoi(w);
     // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
     // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)
     k.tv = (p.use_tensor_voting && !p.get_normals && p.matching_method == IMLS_MATCH_IMLS) ? 1 : 0;
@@ -497,6 +504,89 @@ int ensure_built(imls_ctx* c) {
     return finish_source(c);
 }
 
+// The pending builds of a batch's members in ONE launch sequence on the lead's stream (index.hip
+// build_batch: one radix sort for every frame's points): after each member's filter count (one
+// host wait each, all filters already enqueued), the trees and source orders of all of them; the
+// members' streams are then ordered after it.  Members with per-launch timing on keep their own
+// build (its timing events are on their streams).
+int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n) {
+    bool any = false, timing = false;
+    for (size_t k = 0; k < n; ++k) {
+        any |= ctxs[k]->tgt_pending || ctxs[k]->src_pending;
+        timing |= ctxs[k]->timing;
+    }
+    if (!any) return IMLS_OK;
+    if (timing) {
+        for (size_t k = 0; k < n; ++k)
+            if (int rc = ensure_built(ctxs[k])) return fail(L, rc, "context " + std::to_string(k) + ": " + ctxs[k]->err);
+        return IMLS_OK;
+    }
+    std::vector<BuildJob> jobs;
+    std::vector<std::pair<imls_ctx*, int>> who;   // (context, 0 target / 1 source)
+    for (size_t k = 0; k < n; ++k) {
+        imls_ctx* c = ctxs[k];
+        if (c->tgt_pending) {
+            c->tgt_pending = false;
+            if (hipEventSynchronize(c->ev_tgt) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "target filter failed");
+            c->M = c->h_cnt[0];
+            c->Pl = c->levels = 0;
+            c->has_target = c->M > 0;
+            timed_end(c, 1, c->tgt_slot);
+            c->tgt_slot = -1;
+            if (c->M > 0) {
+                const int Lv = (c->M + c->B - 1) / c->B;
+                int P = 1;
+                while (P < Lv) P <<= 1;
+                if (!grow(c->lkeys, (size_t)Lv * 8 + 16) || !grow(c->mpt, (size_t)c->M * 36 + 64) ||
+                    !grow(c->nodes, (size_t)(P + 1) * 48))
+                    return fail(L, IMLS_ERR_DEVICE, "hipMalloc (index)");
+                jobs.push_back(BuildJob{(const float4*)c->tpt.p, (const float4*)c->tnr.p, c->M, c->B,
+                                        (unsigned long long*)c->lkeys.p, (float4*)c->mpt.p, (float4*)c->nodes.p, nullptr, 0, 0});
+                who.push_back({c, 0});
+            }
+        }
+        if (c->src_pending) {
+            c->src_pending = false;
+            if (hipEventSynchronize(c->ev_src) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "source filter failed");
+            c->N = c->h_cnt[1];
+            c->has_source = c->N > 0;
+            c->src_kept_out = nullptr;
+            if (c->N > 0) {
+                if (!grow(c->qperm, (size_t)c->N * 4 + 16)) return fail(L, IMLS_ERR_DEVICE, "hipMalloc (source order)");
+                jobs.push_back(BuildJob{(const float4*)c->spt.p, nullptr, c->N, 0, nullptr, nullptr, nullptr,
+                                        (unsigned*)c->qperm.p, 0, 0});
+                who.push_back({c, 1});
+            }
+            if (int rc = ensure_solve(c, c->N)) return fail(L, rc, c->err);
+        }
+    }
+    if (jobs.empty()) return IMLS_OK;
+    const size_t tb = jobs.size() * build_job_bytes();
+    if (L->h_btable_bytes < tb) {
+        if (L->h_btable) (void)hipHostFree(L->h_btable);
+        L->h_btable = nullptr;
+        L->h_btable_bytes = 0;
+        if (hipHostMalloc(&L->h_btable, tb + tb / 2 + 1024) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "hipHostMalloc (build table)");
+        L->h_btable_bytes = tb + tb / 2 + 1024;
+    }
+    (void)hipSetDevice(L->device);
+    if (int rc = build_batch(L->stream, jobs, L->bscratch, L->btable, L->h_btable, L->h_btable_bytes, L->err)) return rc;
+    for (size_t q = 0; q < jobs.size(); ++q)
+        if (who[q].second == 0) {
+            who[q].first->Pl = jobs[q].P;
+            who[q].first->levels = jobs[q].levels;
+        }
+    // every member's later work on its own stream (its frame's launches when the batch is not fused,
+    // its next uploads) is ordered after the build
+    if (!L->ev_build && hipEventCreateWithFlags(&L->ev_build, hipEventDisableTiming) != hipSuccess)
+        return fail(L, IMLS_ERR_DEVICE, "hipEventCreate (build)");
+    if (hipEventRecord(L->ev_build, L->stream) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "build event");
+    for (size_t k = 0; k < n; ++k)
+        if (ctxs[k] != L && hipStreamWaitEvent(ctxs[k]->stream, L->ev_build, 0) != hipSuccess)
+            return fail(L, IMLS_ERR_DEVICE, "build stream join");
+    return IMLS_OK;
+}
+
 int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
     if (n == 0 || n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "target size out of range");
     if (!grow(c->tkept, n * 4 + 16)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (kept)");
@@ -673,6 +763,10 @@ void imls_destroy(imls_ctx* c) {
     if (c->tab_d.p) (void)hipFree(c->tab_d.p);
     if (c->res_d.p) (void)hipFree(c->res_d.p);
     if (c->ev_batch) (void)hipEventDestroy(c->ev_batch);
+    if (c->bscratch.p) (void)hipFree(c->bscratch.p);
+    if (c->btable.p) (void)hipFree(c->btable.p);
+    if (c->h_btable) (void)hipHostFree(c->h_btable);
+    if (c->ev_build) (void)hipEventDestroy(c->ev_build);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -1152,12 +1246,8 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
             return fail(L, IMLS_ERR_STATE, "context " + std::to_string(k) + " has a frame pending");
     }
     // every member's deferred build: its filter count (one wait each, all filters already enqueued)
-    // then the rest of its index build on its own stream
-    for (size_t k = 0; k < n; ++k) {
-        imls_ctx* c = ctxs[k];
-        if (c != L && check_device(c)) return fail(L, IMLS_ERR_DEVICE, "hipSetDevice");
-        if (int rc = ensure_built(c)) return fail(L, rc, "context " + std::to_string(k) + ": " + c->err);
-    }
+    // then all the members' index builds in one launch sequence on the lead's stream
+    if (int rc = batch_builds(L, ctxs, n)) return rc;
     (void)hipSetDevice(L->device);
     for (size_t k = 0; k < n; ++k) {
         imls_ctx* c = ctxs[k];

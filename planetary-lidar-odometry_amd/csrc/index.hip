@@ -308,4 +308,277 @@ int source_order(hipStream_t s, int N, DevBuf& spt, DevBuf& scratch, DevBuf& qpe
     return morton_perm(s, (const float4*)spt.p, N, scratch, qperm, err);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Batched builds (imls_register_frames): the target trees and source orders of many frames in one
+// launch sequence — per-frame bbox partials, Morton keys with the job index above bit 48 (one radix
+// sort orders every frame's points at once; stable, so each frame's permutation is exactly its own
+// sort's), the Morton-ordered copies / leaf keys / permutations, leaf boxes and the subtree rounds.
+// Every step computes what the per-frame build computes, in the same float operations.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kBBoxParts = 64;          // bbox partial blocks per job (grid-stride)
+constexpr int kSubRounds = 4;           // subtree rounds: ⌈levels / 8⌉ ≤ 3 for levels ≤ 23
+
+struct JobDev {
+    const float4* pts;                  // filtered points (xyz, 0)
+    const float4* nrm;                  // filtered normals (targets)
+    int n, off;                         // points; offset in the concatenated key array
+    int B, L, P, levels;                // targets: bucket, leaves, padded leaves, tree levels (B = 0: source)
+    float* qp;                          // [4] quantisation (targets: after the leaf keys)
+    unsigned long long* lkeys;          // targets: first key of each leaf
+    float4 *mpt, *mnr;                  // targets: Morton-ordered copies
+    unsigned* ipos;                     // targets: input → Morton position
+    float4* nodes;                      // targets: node records
+    unsigned* perm;                     // sources: sorted → input index
+    float* bbpart;                      // [kBBoxParts × 6]
+    float* leafbox;                     // targets: [P × 6]
+    const float* sub_in[kSubRounds];    // subtree round r: input boxes, count, depth, output roots
+    float* sub_out[kSubRounds];
+    int sub_count[kSubRounds], sub_D[kSubRounds];
+};
+
+__global__ __launch_bounds__(kBlock) void k_bbox_b(const JobDev* __restrict__ jobs) {
+    const JobDev& J = jobs[blockIdx.y];
+    __shared__ float red[6][kBlock];
+    const int M = J.n;
+    const int nb = min(kBBoxParts, (int)((M + kBlock - 1) / kBlock));
+    if ((int)blockIdx.x >= nb) return;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < M; i += nb * kBlock) {
+        const float4 p = J.pts[i];
+        lo[0] = fminf(lo[0], p.x); lo[1] = fminf(lo[1], p.y); lo[2] = fminf(lo[2], p.z);
+        hi[0] = fmaxf(hi[0], p.x); hi[1] = fmaxf(hi[1], p.y); hi[2] = fmaxf(hi[2], p.z);
+    }
+    for (int d = 0; d < 3; ++d) { red[d][threadIdx.x] = lo[d]; red[3 + d][threadIdx.x] = hi[d]; }
+    __syncthreads();
+    for (int st = kBlock / 2; st > 0; st >>= 1) {
+        if (threadIdx.x < st)
+            for (int d = 0; d < 3; ++d) {
+                red[d][threadIdx.x] = fminf(red[d][threadIdx.x], red[d][threadIdx.x + st]);
+                red[3 + d][threadIdx.x] = fmaxf(red[3 + d][threadIdx.x], red[3 + d][threadIdx.x + st]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) J.bbpart[blockIdx.x * 6 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// bbox (min / max are exact in any order) → quantisation (k_qparams' arithmetic) → keys tagged
+// with the job index; block 0 of a job publishes its quantisation
+__global__ __launch_bounds__(kBlock) void k_morton_b(const JobDev* __restrict__ jobs, unsigned long long* __restrict__ key,
+                                                     unsigned* __restrict__ val) {
+    const JobDev& J = jobs[blockIdx.y];
+    const int M = J.n;
+    if ((int)blockIdx.x * kBlock >= M) return;
+    __shared__ float qs[4];
+    if (threadIdx.x == 0) {
+        const int nb = min(kBBoxParts, (int)((M + kBlock - 1) / kBlock));
+        float b[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        for (int k = 0; k < nb; ++k)
+            for (int d = 0; d < 3; ++d) {
+                b[d] = fminf(b[d], J.bbpart[k * 6 + d]);
+                b[3 + d] = fmaxf(b[3 + d], J.bbpart[k * 6 + 3 + d]);
+            }
+        const float ext = fmaxf(fmaxf(fmaxf(b[3] - b[0], b[4] - b[1]), b[5] - b[2]), 1e-6f);
+        qs[0] = b[0]; qs[1] = b[1]; qs[2] = b[2];
+        qs[3] = 65535.f / ext;
+        if (blockIdx.x == 0)
+            for (int k = 0; k < 4; ++k) J.qp[k] = qs[k];
+    }
+    __syncthreads();
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M) return;
+    const float4 p = J.pts[i];
+    key[(size_t)J.off + i] = ((unsigned long long)blockIdx.y << 48) | morton48(p.x, p.y, p.z, qs);
+    val[(size_t)J.off + i] = (unsigned)i;
+}
+
+// sorted segment of a job → targets: Morton copies, input → Morton positions, leaf first keys;
+// sources: the permutation
+__global__ __launch_bounds__(kBlock) void k_place_b(const JobDev* __restrict__ jobs, const unsigned long long* __restrict__ key,
+                                                    const unsigned* __restrict__ val) {
+    const JobDev& J = jobs[blockIdx.y];
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= J.n) return;
+    const unsigned j = val[(size_t)J.off + k];
+    if (J.B == 0) {
+        J.perm[k] = j;
+        return;
+    }
+    const float4 p = J.pts[j];
+    J.mpt[k] = make_float4(p.x, p.y, p.z, __uint_as_float(j));
+    J.mnr[k] = J.nrm[j];
+    J.ipos[j] = (unsigned)k;
+    if (k % J.B == 0) J.lkeys[k / J.B] = key[(size_t)J.off + k] & 0xFFFFFFFFFFFFull;
+}
+
+__global__ __launch_bounds__(kBlock) void k_leaf_boxes_b(const JobDev* __restrict__ jobs) {
+    const JobDev& J = jobs[blockIdx.y];
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    if (J.B == 0 || b >= J.P) return;
+    Box bx = {{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
+    const int s = b * J.B, e = min(s + J.B, J.n);
+    for (int k = s; k < e; ++k) {
+        const float4 p = J.mpt[k];
+        bx.lo[0] = fminf(bx.lo[0], p.x); bx.lo[1] = fminf(bx.lo[1], p.y); bx.lo[2] = fminf(bx.lo[2], p.z);
+        bx.hi[0] = fmaxf(bx.hi[0], p.x); bx.hi[1] = fmaxf(bx.hi[1], p.y); bx.hi[2] = fmaxf(bx.hi[2], p.z);
+    }
+    for (int d = 0; d < 3; ++d) { J.leafbox[b * 6 + d] = bx.lo[d]; J.leafbox[b * 6 + 3 + d] = bx.hi[d]; }
+}
+
+// subtree round r of every job (k_subtree's reduction; a job past its last round leaves)
+__global__ __launch_bounds__(kBlock) void k_subtree_b(const JobDev* __restrict__ jobs, int r) {
+    const JobDev& J = jobs[blockIdx.y];
+    if (J.B == 0) return;
+    const int count = J.sub_count[r];
+    if (count <= 1) return;
+    const int width = min(count, kBlock);
+    if ((int)blockIdx.x >= count / width) return;
+    const int D = J.sub_D[r];
+    __shared__ Box sb[kBlock];
+    const int t = threadIdx.x;
+    const int base = blockIdx.x * width;
+    if (t < width) {
+        const float* q = J.sub_in[r] + (size_t)(base + t) * 6;
+        for (int d = 0; d < 3; ++d) { sb[t].lo[d] = q[d]; sb[t].hi[d] = q[3 + d]; }
+    }
+    __syncthreads();
+    int n = width, depth = D;
+    while (n > 1) {
+        n >>= 1;
+        --depth;
+        Box u;
+        const bool act = t < n;
+        if (act) {
+            const Box l = sb[2 * t], rr = sb[2 * t + 1];
+            const int id = (1 << depth) + (base >> (D - depth)) + t;
+            float4* rec = J.nodes + 3 * (size_t)id;
+            rec[0] = make_float4(l.lo[0], l.lo[1], l.lo[2], l.hi[0]);
+            rec[1] = make_float4(l.hi[1], l.hi[2], rr.lo[0], rr.lo[1]);
+            rec[2] = make_float4(rr.lo[2], rr.hi[0], rr.hi[1], rr.hi[2]);
+            u = box_union(l, rr);
+        }
+        __syncthreads();
+        if (act) sb[t] = u;
+        __syncthreads();
+    }
+    if (t == 0)
+        for (int d = 0; d < 3; ++d) { J.sub_out[r][blockIdx.x * 6 + d] = sb[0].lo[d]; J.sub_out[r][blockIdx.x * 6 + 3 + d] = sb[0].hi[d]; }
+}
+
+}  // namespace
+
+size_t build_job_bytes() { return sizeof(JobDev); }
+
+int build_batch(hipStream_t s, std::vector<BuildJob>& jobs, DevBuf& scratch, DevBuf& table, void* h_table,
+                size_t h_table_bytes, std::string& err) {
+    const int nj = (int)jobs.size();
+    if (nj == 0) return IMLS_OK;
+    if ((size_t)nj * sizeof(JobDev) > h_table_bytes) { err = "build table too small"; return IMLS_ERR_CAPACITY; }
+    if (nj > 65535) { err = "too many build jobs"; return IMLS_ERR_CAPACITY; }
+    size_t total = 0, leaf_floats = 0, root_floats = 0;
+    int maxn = 1, maxP = 1;
+    for (auto& b : jobs) {
+        if (b.n <= 0) continue;
+        total += (size_t)b.n;
+        maxn = std::max(maxn, b.n);
+        if (b.B > 0) {
+            const int L = (b.n + b.B - 1) / b.B;
+            int P = 1, levels = 0;
+            while (P < L) { P <<= 1; ++levels; }
+            if (levels > kStackDepth - 1) { err = "tree too deep for the traversal stack"; return IMLS_ERR_CAPACITY; }
+            b.P = P;
+            b.levels = levels;
+            maxP = std::max(maxP, P);
+            leaf_floats += ((size_t)P * 6 + 63) / 64 * 64;
+            root_floats += 2 * (((size_t)P / kBlock + 1) * 6 + 63) / 64 * 64;
+        }
+    }
+    int end_bit = 48;
+    while ((1ll << (end_bit - 48)) < nj) ++end_bit;
+    size_t cub_bytes = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                       (unsigned*)nullptr, (unsigned*)nullptr, (int)std::max<size_t>(total, 1), 0, end_bit, s);
+    const size_t need = 2 * ((total * 8 + 255) / 256 * 256) + 2 * ((total * 4 + 255) / 256 * 256) +
+                        (cub_bytes + 255) / 256 * 256 + (size_t)nj * (kBBoxParts * 6 * 4 + 256) + (leaf_floats + root_floats) * 4 +
+                        (size_t)nj * 4 * 256 + 4096;
+    if (!ensure(scratch, need, err) || !ensure(table, (size_t)nj * sizeof(JobDev) + 256, err)) return IMLS_ERR_DEVICE;
+    char* p = (char*)scratch.p;
+    unsigned long long* k0 = carve<unsigned long long>(p, total);
+    unsigned long long* k1 = carve<unsigned long long>(p, total);
+    unsigned* v0 = carve<unsigned>(p, total);
+    unsigned* v1 = carve<unsigned>(p, total);
+    void* cub_tmp = carve<char>(p, cub_bytes);
+    JobDev* J = (JobDev*)h_table;
+    size_t off = 0;
+    for (int q = 0; q < nj; ++q) {
+        const BuildJob& b = jobs[q];
+        JobDev d{};
+        d.pts = b.pts;
+        d.nrm = b.nrm;
+        d.n = std::max(b.n, 0);
+        d.off = (int)off;
+        off += (size_t)d.n;
+        d.bbpart = carve<float>(p, kBBoxParts * 6);
+        if (b.B > 0 && b.n > 0) {
+            d.B = b.B;
+            d.L = (b.n + b.B - 1) / b.B;
+            d.P = b.P;
+            d.levels = b.levels;
+            d.lkeys = b.lkeys;
+            d.qp = (float*)(b.lkeys + d.L);          // the quantisation lives after the leaf keys
+            d.mpt = b.mpt;
+            d.mnr = b.mpt + b.n;
+            d.ipos = (unsigned*)(b.mpt + 2 * (size_t)b.n);
+            d.nodes = b.nodes;
+            d.leafbox = carve<float>(p, (size_t)b.P * 6);
+            float* ra = carve<float>(p, ((size_t)b.P / kBlock + 1) * 6);
+            float* rb = carve<float>(p, ((size_t)b.P / kBlock + 1) * 6);
+            // the rounds of the per-frame bottom-up reduction, precomputed
+            const float* in = d.leafbox;
+            float* outs[2] = {ra, rb};
+            int count = b.P, D = b.levels, which = 0;
+            for (int r = 0; r < kSubRounds; ++r) {
+                d.sub_in[r] = in;
+                d.sub_out[r] = outs[which];
+                d.sub_count[r] = count;
+                d.sub_D[r] = D;
+                if (count <= 1) continue;
+                const int width = std::min(count, kBlock);
+                int lg = 0;
+                while ((1 << lg) < width) ++lg;
+                in = outs[which];
+                which ^= 1;
+                count /= width;
+                D -= lg;
+            }
+            if (count > 1) { err = "tree too deep for the batched build"; return IMLS_ERR_CAPACITY; }
+        } else {
+            d.B = 0;
+            d.qp = carve<float>(p, 4);
+            d.perm = b.perm;
+        }
+        J[q] = d;
+    }
+    const JobDev* jd = (const JobDev*)table.p;
+    hipMemcpyAsync(table.p, h_table, (size_t)nj * sizeof(JobDev), hipMemcpyHostToDevice, s);
+    const unsigned gx = grid_for((size_t)maxn);
+    k_bbox_b<<<dim3(std::min<unsigned>(kBBoxParts, gx), nj), kBlock, 0, s>>>(jd);
+    k_morton_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd, k0, v0);
+    if (total > 0) hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, v1, (int)total, 0, end_bit, s);
+    k_place_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd, k1, v1);
+    bool any_tree = false;
+    for (auto& b : jobs) any_tree |= b.B > 0 && b.n > 0;
+    if (any_tree) {
+        k_leaf_boxes_b<<<dim3(grid_for((size_t)maxP), nj), kBlock, 0, s>>>(jd);
+        for (int r = 0, cnt = maxP; r < kSubRounds && cnt > 1; ++r) {
+            const int width = std::min(cnt, kBlock);
+            k_subtree_b<<<dim3(cnt / width, nj), kBlock, 0, s>>>(jd, r);
+            cnt /= width;
+        }
+    }
+    if (hipGetLastError() != hipSuccess) { err = "batched index build launch failed"; return IMLS_ERR_DEVICE; }
+    return IMLS_OK;
+}
+
 }  // namespace imlsgpu

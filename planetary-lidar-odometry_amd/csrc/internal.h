@@ -57,6 +57,7 @@ struct KParams {
     int verlet;               // reuse a query's list without traversal while its certification holds
     int qverlet;              // the same for the wave-per-query traversal (off by default: measured slower)
     int lockstep;             // packet traversal: per-lane candidate masks, then lockstep insertion
+    int bcast_lock;           // … also for broadcast leaves: 0 never, 1 first ICP iteration, 2 always
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
     int tv;                   // tensor-voting normals (use_tensor_voting && !get_normals, IMLS matcher)
     int tv_k;                 // use_tensor_voting.k (≤ kTvMaxK)
@@ -182,6 +183,22 @@ int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& t
                       DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* P_out, int* levels_out,
                       std::string& err);
 int source_order(hipStream_t s, int N, DevBuf& spt, DevBuf& scratch, DevBuf& qperm, std::string& err);
+// (B) for many frames at once, one launch sequence: each job a target tree (B > 0: lkeys [L + 2]
+// words, mpt [3·n] records, nodes [(P+1)·3] float4, sized by the caller; P / levels returned in the
+// job) or a source order (B = 0: perm [n]).  h_table: pinned host memory for the job table.
+struct BuildJob {
+    const float4* pts;
+    const float4* nrm;
+    int n, B;
+    unsigned long long* lkeys;
+    float4* mpt;
+    float4* nodes;
+    unsigned* perm;
+    int P, levels;                     // out (targets)
+};
+int build_batch(hipStream_t s, std::vector<BuildJob>& jobs, DevBuf& scratch, DevBuf& table, void* h_table,
+                size_t h_table_bytes, std::string& err);
+size_t build_job_bytes();              // bytes per job of the device job table
 
 // project.hip
 // k_knn_wave → k_finish (+ the exact k_project_lane fallback for uncertified queries); lane_mode

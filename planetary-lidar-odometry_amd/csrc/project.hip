@@ -406,6 +406,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     // leaf `leaf` against their bound; `listed`: the leaf may hold points already in a lane's
     // list (prefilled or seeded), which must not be inserted twice
     int sparse_thr = kp.sparse_lanes;
+    const bool bcast_lock = kp.bcast_lock == 2 || (kp.bcast_lock == 1 && !use_prev);
 #ifdef IMLS_DEBUG_WAVE_TRACE
     unsigned dbg_ev = 0, dbg_ins = 0;
     unsigned dbg_sparse = 0, dbg_bcast = 0, dbg_sparse_lanes = 0, dbg_sparse_ins = 0;
@@ -428,16 +429,31 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
 #ifdef IMLS_DEBUG_WAVE_TRACE
         if (__popcll(want) <= sparse_thr) { ++dbg_sparse; dbg_sparse_lanes += __popcll(want); } else { ++dbg_bcast; }
 #endif
-        if (LOCKSTEP && __popcll(want) <= sparse_thr) {
+        const bool sparse = __popcll(want) <= sparse_thr;
+        if (LOCKSTEP && (sparse || bcast_lock)) {
             // few lanes want this leaf (spread-out queries in a dense region): per wanting lane,
             // all leaf points are measured at once (one per lane) and the ones under that lane's
             // bound and not yet listed become its candidate mask; then the lanes insert their own
             // candidates in lockstep, each its lowest pending point per step (index order) read
             // back from LDS — max(per-lane candidates) insertion steps instead of one per
-            // candidate of every lane.  (The broadcast path keeps inline insertion: there the
-            // candidates of different lanes mostly coincide in time.)
+            // candidate of every lane.  bcast_lock: many lanes want the leaf, each lane's mask is
+            // built by the broadcast scan, then the same lockstep insertion (loose early bounds:
+            // the candidates of different lanes fall at different points).  Per lane, the
+            // insertions are exactly the sequential scan's (same order, re-tested at the current
+            // bound; a non-candidate was above the leaf-start bound already).
             unsigned long long cm = 0ull;
-            {
+            if (!sparse) {
+                const bool wants = (want >> lane) & 1ull;
+                for (int j = 0; j < cnt; ++j) {
+                    const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
+                    const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.y), j));
+                    const float pz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.z), j));
+                    const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
+                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                    cm |= (wants && d32 <= bnd) ? (1ull << j) : 0ull;
+                }
+                cm &= ~inl;
+            } else {
                 unsigned long long m = want;
                 while (m) {
                     const int q = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
