@@ -715,7 +715,8 @@ imls_ctx* imls_create(int device, const imls_params* p) {
     }
     c->stream = c->own;
     if (hipHostMalloc((void**)&c->h_misc, 32 * sizeof(double)) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_cnt, 4 * sizeof(int)) != hipSuccess) {
+        // coherent: the NaN filter's compaction kernel writes the kept counts here directly
+        hipHostMalloc((void**)&c->h_cnt, 4 * sizeof(int), hipHostMallocCoherent) != hipSuccess) {
         delete c;
         return nullptr;
     }

@@ -44,10 +44,14 @@ __global__ void k_flag_finite(const float* __restrict__ soa, size_t n, unsigned*
 // scatter kept points to float4 records; pos = exclusive prefix sum of flags
 __global__ void k_compact(const float* __restrict__ soa, size_t n, const unsigned* __restrict__ flag,
                           const unsigned* __restrict__ pos, float4* __restrict__ pt, float4* __restrict__ nr,
-                          unsigned* __restrict__ kept_index, int* __restrict__ count) {
+                          unsigned* __restrict__ kept_index, int* __restrict__ count, int* __restrict__ h_count) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (i == n - 1) *count = (int)(pos[i] + flag[i]);
+    if (i == n - 1) {
+        const int c = (int)(pos[i] + flag[i]);
+        *count = c;
+        *h_count = c;   // pinned host memory, written directly (no copy launch per filter)
+    }
     if (!flag[i]) return;
     unsigned o = pos[i];
     pt[o] = make_float4(soa[i], soa[n + i], soa[2 * n + i], 0.f);
@@ -194,8 +198,8 @@ inline unsigned grid_for(size_t n, int b = kBlock) { return (unsigned)((n + b - 
 
 }  // namespace
 
-// NaN filter + order-keeping compaction, asynchronous: the kept count lands in *h_count (pinned
-// host memory) by an async copy behind the compaction — valid once the stream has passed it.
+// NaN filter + order-keeping compaction, asynchronous: the kept count lands in *h_count (pinned,
+// device-visible host memory) from the compaction kernel itself — valid once the stream has passed it.
 int filter_async(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, DevBuf& nr, DevBuf& scratch,
                  unsigned* d_kept, int* h_count, std::string& err) {
     size_t cub_bytes = 0;
@@ -212,9 +216,8 @@ int filter_async(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, De
     void* cub_tmp = carve<char>(p, cub_bytes);
     k_flag_finite<<<grid_for(n_in), kBlock, 0, s>>>(d_soa6, n_in, flag);
     hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, flag, pos, (int)n_in, s);
-    k_compact<<<grid_for(n_in), kBlock, 0, s>>>(d_soa6, n_in, flag, pos, (float4*)pt.p, (float4*)nr.p, d_kept, cnt);
-    if (hipMemcpyAsync(h_count, cnt, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipGetLastError() != hipSuccess) {
+    k_compact<<<grid_for(n_in), kBlock, 0, s>>>(d_soa6, n_in, flag, pos, (float4*)pt.p, (float4*)nr.p, d_kept, cnt, h_count);
+    if (hipGetLastError() != hipSuccess) {
         err = "filter/compact launch failed";
         return IMLS_ERR_DEVICE;
     }
@@ -363,33 +366,36 @@ __global__ __launch_bounds__(kBlock) void k_bbox_b(const JobDev* __restrict__ jo
     if (threadIdx.x < 6) J.bbpart[blockIdx.x * 6 + threadIdx.x] = red[threadIdx.x][0];
 }
 
-// bbox (min / max are exact in any order) → quantisation (k_qparams' arithmetic) → keys tagged
-// with the job index; block 0 of a job publishes its quantisation
+// bbox (min / max are exact in any order) → quantisation (k_qparams' arithmetic), one wave per job
+__global__ __launch_bounds__(64) void k_qparams_b(const JobDev* __restrict__ jobs) {
+    const JobDev& J = jobs[blockIdx.x];
+    const int M = J.n;
+    if (M <= 0) return;
+    const int nb = min(kBBoxParts, (int)((M + kBlock - 1) / kBlock));
+    const int t = threadIdx.x;
+    float b[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    if (t < nb)
+        for (int d = 0; d < 3; ++d) { b[d] = J.bbpart[t * 6 + d]; b[3 + d] = J.bbpart[t * 6 + 3 + d]; }
+    for (int o = 32; o > 0; o >>= 1)
+        for (int d = 0; d < 3; ++d) {
+            b[d] = fminf(b[d], __shfl_xor(b[d], o, 64));
+            b[3 + d] = fmaxf(b[3 + d], __shfl_xor(b[3 + d], o, 64));
+        }
+    if (t == 0) {
+        const float ext = fmaxf(fmaxf(fmaxf(b[3] - b[0], b[4] - b[1]), b[5] - b[2]), 1e-6f);
+        J.qp[0] = b[0]; J.qp[1] = b[1]; J.qp[2] = b[2];
+        J.qp[3] = 65535.f / ext;
+    }
+}
+
+// keys tagged with the job index above bit 48
 __global__ __launch_bounds__(kBlock) void k_morton_b(const JobDev* __restrict__ jobs, unsigned long long* __restrict__ key,
                                                      unsigned* __restrict__ val) {
     const JobDev& J = jobs[blockIdx.y];
-    const int M = J.n;
-    if ((int)blockIdx.x * kBlock >= M) return;
-    __shared__ float qs[4];
-    if (threadIdx.x == 0) {
-        const int nb = min(kBBoxParts, (int)((M + kBlock - 1) / kBlock));
-        float b[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        for (int k = 0; k < nb; ++k)
-            for (int d = 0; d < 3; ++d) {
-                b[d] = fminf(b[d], J.bbpart[k * 6 + d]);
-                b[3 + d] = fmaxf(b[3 + d], J.bbpart[k * 6 + 3 + d]);
-            }
-        const float ext = fmaxf(fmaxf(fmaxf(b[3] - b[0], b[4] - b[1]), b[5] - b[2]), 1e-6f);
-        qs[0] = b[0]; qs[1] = b[1]; qs[2] = b[2];
-        qs[3] = 65535.f / ext;
-        if (blockIdx.x == 0)
-            for (int k = 0; k < 4; ++k) J.qp[k] = qs[k];
-    }
-    __syncthreads();
     const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= M) return;
+    if (i >= J.n) return;
     const float4 p = J.pts[i];
-    key[(size_t)J.off + i] = ((unsigned long long)blockIdx.y << 48) | morton48(p.x, p.y, p.z, qs);
+    key[(size_t)J.off + i] = ((unsigned long long)blockIdx.y << 48) | morton48(p.x, p.y, p.z, J.qp);
     val[(size_t)J.off + i] = (unsigned)i;
 }
 
@@ -564,6 +570,7 @@ int build_batch(hipStream_t s, std::vector<BuildJob>& jobs, DevBuf& scratch, Dev
     hipMemcpyAsync(table.p, h_table, (size_t)nj * sizeof(JobDev), hipMemcpyHostToDevice, s);
     const unsigned gx = grid_for((size_t)maxn);
     k_bbox_b<<<dim3(std::min<unsigned>(kBBoxParts, gx), nj), kBlock, 0, s>>>(jd);
+    k_qparams_b<<<nj, 64, 0, s>>>(jd);
     k_morton_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd, k0, v0);
     if (total > 0) hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, v1, (int)total, 0, end_bit, s);
     k_place_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd, k1, v1);
