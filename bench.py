@@ -220,13 +220,13 @@ def solver_params(solver: str, iters: int) -> _abi.ImlsParams:
 
 
 class Pipeline:
-    """Fused steps, double-buffered: the contexts are split into two halves, each registered as ONE
-    launch sequence (register_frames_async).  A half is collected, re-loaded (deferred uploads and
-    NaN filters: no host wait) and launched again while the other half's batch still runs, so two
-    batches overlap on the GPU (one fills the other's tail) and the host work hides behind them.
-    A step registers every context once and returns the results collected during it; the batches
-    launched last stay in flight into the next step (the timed region's device-wide synchronize on
-    both sides covers them)."""
+    """Fused steps: the contexts are split into `groups` parts, each registered as ONE launch
+    sequence (register_frames_async).  A part is collected, re-loaded (deferred uploads and NaN
+    filters: no host wait) and launched again while the other parts' batches still run, so batches
+    overlap on the GPU (one fills another's tail) and the host work hides behind them (groups = 1:
+    one batch per step, collected at the next step).  A step registers every context once and
+    returns the results collected during it; the batches launched last stay in flight into the
+    next step (the timed region's device-wide synchronize on both sides covers them)."""
 
     def __init__(self, ctxs, prep, groups=2):
         g = max(1, min(groups, len(ctxs)))
@@ -441,13 +441,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--queries", type=int, default=0, help="config B: 0 = all source points; else FPS subsample")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="independent pairs / sequences per step (0 = workload default: B 4, A 16, stream 128)")
+                    help="independent pairs / sequences per step (0 = workload default: B 4, A 64, stream 512)")
     ap.add_argument("--no-fuse", action="store_true",
                     help="one launch sequence per pair on its own stream instead of one for the whole step")
     ap.add_argument("--unique-seqs", type=int, default=8, help="stream: distinct produced sequences")
     ap.add_argument("--groups", type=int, default=0,
                     help="fused: launch sequences the step's pairs are split into, kept in flight together "
-                         "(0 = workload default: B 4, A 2, stream 2)")
+                         "(0 = workload default: B 4, A 1, stream 1)")
     ap.add_argument("--host-inputs", action="store_true",
                     help="stream: frames handed over in host memory (PCIe inside the timed region)")
     ap.add_argument("--latency-pairs", type=int, default=50, help="single-pair latency / roofline probe size")
@@ -465,9 +465,13 @@ def main():
     # best (pairs per sequence × sequences: 1×4 264.7, 2×2 252.4, 2×4 255.7, 3×2 237.2, 4×2 231,
     # 8×2 205 pairs/s: more per launch only adds cache pressure).  The ~1900-query stream frames
     # need many per launch: 64 per sequence × 2 → 2819 frames/s (32 × 4: 1841)
-    P = args.inflight if args.inflight > 0 else {"B": 4, "A": 16, "stream": 128}[args.workload]
+    # measured (profiles/r02_final): B pairs fill the GPU alone and run best as 4 one-pair launch
+    # sequences in flight; the small A / stream frames run best as ONE large batch per step (two
+    # half batches in flight share hardware queues, so a filter of one half can wait behind the
+    # other half's launch sequence)
+    P = args.inflight if args.inflight > 0 else {"B": 4, "A": 64, "stream": 512}[args.workload]
     if args.groups <= 0:
-        args.groups = {"B": 4, "A": 2, "stream": 2}[args.workload]
+        args.groups = {"B": 4, "A": 1, "stream": 1}[args.workload]
     fuse = not args.no_fuse
     p = solver_params(args.solver, args.iters)
     t0 = time.time()
