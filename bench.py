@@ -221,8 +221,9 @@ def solver_params(solver: str, iters: int) -> _abi.ImlsParams:
 
 class Pipeline:
     """Fused steps: the contexts are split into `groups` parts, each registered as ONE launch
-    sequence (register_frames_async).  A part is collected, re-loaded (deferred uploads and NaN
-    filters: no host wait) and launched again while the other parts' batches still run, so batches
+    sequence (register_frames_async).  A part is re-loaded (deferred uploads and NaN filters: no
+    host wait, enqueued behind its running batch), collected and launched again while the other
+    parts' batches still run, so batches
     overlap on the GPU (one fills another's tail) and the host work hides behind them (groups = 1:
     one batch per step, collected at the next step).  A step registers every context once and
     returns the results collected during it; the batches launched last stay in flight into the
@@ -249,8 +250,11 @@ class Pipeline:
     def step(self):
         out = []
         for h, half in enumerate(self.halves):
-            out += self._collect(h)
+            # the part's next inputs are enqueued while its previous batch still runs (each
+            # context's stream is ordered after the batch: set_target / map_push / set_source
+            # touch nothing the batch reads before it ends), then its results are collected
             self.prep(range(self.offs[h], self.offs[h] + len(half)))
+            out += self._collect(h)
             t0 = time.perf_counter()
             imls_icp.register_frames_async(half)    # builds (after the filter counts) + the batch's launches
             self.t_launch += time.perf_counter() - t0

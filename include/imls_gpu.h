@@ -213,6 +213,9 @@ int imls_set_source_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t*
  * imls_set_target replaces the index without touching the FIFO. */
 int imls_map_push(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n, size_t stride_floats,
                   size_t* n_map);
+/* Device-resident scan (SoA6 floats in HBM), read on the context's stream (the buffer must stay
+ * valid until that stream has passed the push).  With max_queue_size 1 the map is this scan alone
+ * and is indexed in place (no FIFO copy); raising max_queue_size afterwards needs a fresh push. */
 int imls_map_push_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_map);
 int imls_map_clear(imls_ctx* ctx);
 /* FIFO entries and their total point count (before the NaN filter). */

@@ -33,7 +33,7 @@ struct imls_ctx {
     DevBuf spt, snr, sscratch, qperm, upload_s, skept;
     // map FIFO (accumulateTargetCloud, laser_odometry.cpp:116-136): the last max_queue_size filtered
     // scans, each SoA6 in its own slot, and their concatenation (oldest first) the index is built from
-    struct MapSlot { DevBuf buf; size_t n = 0; };
+    struct MapSlot { DevBuf buf; size_t n = 0; bool ghost = false; };
     std::deque<MapSlot> fifo;
     std::vector<DevBuf> slot_pool;        // freed slots, reused (no allocation per frame)
     DevBuf macc;
@@ -850,6 +850,28 @@ int imls_set_target_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n
 static int map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, size_t stride, const float* d_soa6,
                     size_t* n_map) {
     if (n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "scan too large");
+    // max_queue_size 1 with a device scan (the shipped config, device frames): the map IS this
+    // scan, dropped at the next push — index it where it lies (its NaN filter reads it on this
+    // stream, as the slot copy would), no FIFO copy
+    if (d_soa6 && c->P.max_queue_size == 1) {
+        for (auto& e : c->fifo)
+            if (!e.ghost) c->slot_pool.push_back(e.buf);
+        c->fifo.clear();
+        imls_ctx::MapSlot ghost;          // bookkeeping only: its data stays with the caller
+        ghost.n = n;
+        ghost.ghost = true;
+        c->fifo.push_back(ghost);
+        c->map_points = n;
+        if (n == 0) {
+            c->tgt_pending = false;
+            c->has_target = false;
+            c->has_corr = false;
+            c->M = 0;
+            if (n_map) *n_map = 0;
+            return IMLS_OK;
+        }
+        return do_set_target(c, d_soa6, n, n_map);
+    }
     imls_ctx::MapSlot sl;
     if (!c->slot_pool.empty()) { sl.buf = c->slot_pool.back(); c->slot_pool.pop_back(); }
     sl.n = n;
@@ -868,9 +890,11 @@ static int map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, s
     c->map_points += n;
     if (c->fifo.size() > (size_t)std::max(c->P.max_queue_size, 0)) {
         c->map_points -= c->fifo.front().n;
-        c->slot_pool.push_back(c->fifo.front().buf);
+        if (!c->fifo.front().ghost) c->slot_pool.push_back(c->fifo.front().buf);
         c->fifo.pop_front();
     }
+    for (const auto& e : c->fifo)     // a scan indexed in place (max_queue_size was 1) is not held
+        if (e.ghost && e.n > 0) return fail(c, IMLS_ERR_STATE, "map FIFO holds a scan pushed with max_queue_size 1 (not kept): push again");
     const size_t M = c->map_points;
     if (M == 0) {                     // empty map (max_queue_size 0 or empty scans): no target
         c->tgt_pending = false;
@@ -909,7 +933,8 @@ int imls_map_push_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_m
 
 int imls_map_clear(imls_ctx* c) {
     if (!c) return IMLS_ERR_ARG;
-    for (auto& e : c->fifo) c->slot_pool.push_back(e.buf);
+    for (auto& e : c->fifo)
+        if (!e.ghost) c->slot_pool.push_back(e.buf);
     c->fifo.clear();
     c->map_points = 0;
     return IMLS_OK;
