@@ -198,7 +198,12 @@ int imls_set_target(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n,
 int imls_set_source(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n,
                     size_t stride_floats, size_t* n_kept, uint32_t* kept_index);
 /* Same, for clouds already resident in device memory as SoA float32[6][n]
- * (x[], y[], z[], nx[], ny[], nz[]) — inputs stay in HBM, no PCIe in the hot loop. */
+ * (x[], y[], z[], nx[], ny[], nz[]) — inputs stay in HBM, no PCIe in the hot loop.
+ * Deferred mode (n_kept NULL, and no kept_index): the call returns at once; the NaN filter and the
+ * index build run at the first use of the cloud (a registration, a projection, or all the frames of
+ * an imls_register_frames batch together, in one launch sequence), reading d_soa6 THEN — the
+ * device buffer must stay valid and unchanged until that first use.  Host-pointer calls copy their
+ * input at the call, so their buffers are free on return. */
 int imls_set_target_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
 int imls_set_source_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
 
@@ -213,9 +218,10 @@ int imls_set_source_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t*
  * imls_set_target replaces the index without touching the FIFO. */
 int imls_map_push(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n, size_t stride_floats,
                   size_t* n_map);
-/* Device-resident scan (SoA6 floats in HBM), read on the context's stream (the buffer must stay
- * valid until that stream has passed the push).  With max_queue_size 1 the map is this scan alone
- * and is indexed in place (no FIFO copy); raising max_queue_size afterwards needs a fresh push. */
+/* Device-resident scan (SoA6 floats in HBM).  With max_queue_size 1 the map is this scan alone and
+ * is indexed in place (no FIFO copy): the buffer must then stay valid until the map's first use
+ * (deferred mode, n_map NULL) or until the context's stream has passed the push; raising
+ * max_queue_size afterwards needs a fresh push.  Larger FIFOs copy the scan into a FIFO slot. */
 int imls_map_push_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_map);
 int imls_map_clear(imls_ctx* ctx);
 /* FIFO entries and their total point count (before the NaN filter). */

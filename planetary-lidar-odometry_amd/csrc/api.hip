@@ -63,6 +63,13 @@ struct imls_ctx {
     int* h_cnt = nullptr;                 // pinned [4]: kept counts of the pending target / source
     hipEvent_t ev_tgt = nullptr, ev_src = nullptr;
     bool tgt_pending = false, src_pending = false;
+    // deferred filters (no count requested): the NaN filter itself waits for the first use, reading
+    // its input (an owned upload / FIFO buffer, or the caller's device scan) then — a batch runs all
+    // its members' filters in one launch sequence (filter_batch)
+    const float* tf_soa = nullptr;
+    const float* sf_soa = nullptr;
+    size_t tf_n = 0, sf_n = 0;
+    bool tgt_filter_deferred = false, src_filter_deferred = false;
     int tgt_slot = -1;                    // timing event slot of the pending target build
     uint32_t* src_kept_out = nullptr;
     // pinned staging of host uploads (0: target / map scans, 1: source), reused once its copy ran
@@ -86,7 +93,8 @@ struct imls_ctx {
     // batched registration led by this context (imls_register_frames*): frame table, results
     PairDev* tab_h = nullptr;             // pinned [tab_cap]
     DevBuf tab_d, res_d;
-    double* res_h = nullptr;              // pinned [tab_cap][kResStride]
+    double* res_h = nullptr;              // pinned: [n][kResStride] results, then [n][iters] traces
+    size_t res_h_bytes = 0;
     int tab_cap = 0;
     std::vector<imls_ctx*> members;       // frames of the pending batch (members[0] == this)
     std::vector<int> member_n;
@@ -97,6 +105,9 @@ struct imls_ctx {
     DevBuf bscratch, btable;
     void* h_btable = nullptr;
     size_t h_btable_bytes = 0;
+    DevBuf fscratch, ftable;              // batched filters (filter_batch)
+    void* h_ftable = nullptr;
+    size_t h_ftable_bytes = 0;
     hipEvent_t ev_build = nullptr;
     // traversal / neighbour counters (imls_traversal_stats): off by default — their per-wave
     // device-scope atomics onto a few shared words cost ~60 µs per projection at config B
@@ -472,6 +483,13 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
 int finish_target(imls_ctx* c) {
     if (!c->tgt_pending) return IMLS_OK;
     c->tgt_pending = false;
+    if (c->tgt_filter_deferred) {
+        c->tgt_filter_deferred = false;
+        if (int rc = filter_async(c->stream, c->tf_soa, c->tf_n, c->tpt, c->tnr, c->tscratch, (unsigned*)c->tkept.p,
+                                  &c->h_cnt[0], c->err))
+            return rc;
+        if (hipEventRecord(c->ev_tgt, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "event record");
+    }
     if (hipEventSynchronize(c->ev_tgt) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "target filter failed");
     c->M = c->h_cnt[0];
     int rc = build_target_tree(c->stream, c->M, c->B, c->lkeys, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch,
@@ -486,6 +504,12 @@ int finish_target(imls_ctx* c) {
 int finish_source(imls_ctx* c) {
     if (!c->src_pending) return IMLS_OK;
     c->src_pending = false;
+    if (c->src_filter_deferred) {
+        c->src_filter_deferred = false;
+        if (int rc = filter_async(c->stream, c->sf_soa, c->sf_n, c->spt, c->snr, c->sscratch, nullptr, &c->h_cnt[1], c->err))
+            return rc;
+        if (hipEventRecord(c->ev_src, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "event record");
+    }
     if (hipEventSynchronize(c->ev_src) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "source filter failed");
     c->N = c->h_cnt[1];
     c->has_source = false;
@@ -520,6 +544,38 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n) {
         for (size_t k = 0; k < n; ++k)
             if (int rc = ensure_built(ctxs[k])) return fail(L, rc, "context " + std::to_string(k) + ": " + ctxs[k]->err);
         return IMLS_OK;
+    }
+    // the deferred NaN filters of every member: one launch sequence on the lead's stream, ordered
+    // after each member's stream (its uploads), then one wait for all their counts
+    {
+        std::vector<FilterJob> fj;
+        for (size_t k = 0; k < n; ++k) {
+            imls_ctx* c = ctxs[k];
+            if (c->tgt_pending && c->tgt_filter_deferred) {
+                if (c != L && hipStreamWaitEvent(L->stream, c->ev_tgt, 0) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "filter join");
+                if (!grow(c->tkept, c->tf_n * 4 + 16)) return fail(L, IMLS_ERR_DEVICE, "hipMalloc (kept)");
+                fj.push_back(FilterJob{c->tf_soa, c->tf_n, &c->tpt, &c->tnr, (unsigned*)c->tkept.p, &c->h_cnt[0]});
+                c->tgt_filter_deferred = false;
+            }
+            if (c->src_pending && c->src_filter_deferred) {
+                if (c != L && hipStreamWaitEvent(L->stream, c->ev_src, 0) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "filter join");
+                fj.push_back(FilterJob{c->sf_soa, c->sf_n, &c->spt, &c->snr, nullptr, &c->h_cnt[1]});
+                c->src_filter_deferred = false;
+            }
+        }
+        if (!fj.empty()) {
+            const size_t tb = fj.size() * filter_job_bytes();
+            if (L->h_ftable_bytes < tb) {
+                if (L->h_ftable) (void)hipHostFree(L->h_ftable);
+                L->h_ftable = nullptr;
+                L->h_ftable_bytes = 0;
+                if (hipHostMalloc(&L->h_ftable, tb + tb / 2 + 1024) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "hipHostMalloc (filter table)");
+                L->h_ftable_bytes = tb + tb / 2 + 1024;
+            }
+            (void)hipSetDevice(L->device);
+            if (int rc = filter_batch(L->stream, fj, L->fscratch, L->ftable, L->h_ftable, L->h_ftable_bytes, L->err)) return rc;
+            if (hipStreamSynchronize(L->stream) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "batched filter failed");
+        }
     }
     std::vector<BuildJob> jobs;
     std::vector<std::pair<imls_ctx*, int>> who;   // (context, 0 target / 1 source)
@@ -594,9 +650,16 @@ int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
         return fail(c, IMLS_ERR_DEVICE, "hipEventCreate");
     c->has_tensors = false;
     c->tgt_pending = false;
+    c->tgt_filter_deferred = false;
     timed_begin(c, 1, c->tgt_slot);
-    int rc = filter_async(c->stream, d_soa6, n, c->tpt, c->tnr, c->tscratch, (unsigned*)c->tkept.p, &c->h_cnt[0], c->err);
-    if (rc) return rc;
+    if (n_kept) {
+        int rc = filter_async(c->stream, d_soa6, n, c->tpt, c->tnr, c->tscratch, (unsigned*)c->tkept.p, &c->h_cnt[0], c->err);
+        if (rc) return rc;
+    } else {
+        c->tf_soa = d_soa6;                // filtered at first use (alone, or with a whole batch)
+        c->tf_n = n;
+        c->tgt_filter_deferred = true;
+    }
     if (hipEventRecord(c->ev_tgt, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "event record");
     c->n_target_in = n;
     c->tgt_pending = true;
@@ -616,9 +679,16 @@ int do_set_source(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept, ui
     if (!c->ev_src && hipEventCreateWithFlags(&c->ev_src, hipEventDisableTiming) != hipSuccess)
         return fail(c, IMLS_ERR_DEVICE, "hipEventCreate");
     c->src_pending = false;
-    int rc = filter_async(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, kept_index ? (unsigned*)c->skept.p : nullptr,
-                          &c->h_cnt[1], c->err);
-    if (rc) return rc;
+    c->src_filter_deferred = false;
+    if (n_kept || kept_index) {
+        int rc = filter_async(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, kept_index ? (unsigned*)c->skept.p : nullptr,
+                              &c->h_cnt[1], c->err);
+        if (rc) return rc;
+    } else {
+        c->sf_soa = d_soa6;
+        c->sf_n = n;
+        c->src_filter_deferred = true;
+    }
     if (hipEventRecord(c->ev_src, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "event record");
     c->src_pending = true;
     c->src_kept_out = kept_index;
@@ -767,6 +837,9 @@ void imls_destroy(imls_ctx* c) {
     if (c->bscratch.p) (void)hipFree(c->bscratch.p);
     if (c->btable.p) (void)hipFree(c->btable.p);
     if (c->h_btable) (void)hipHostFree(c->h_btable);
+    if (c->fscratch.p) (void)hipFree(c->fscratch.p);
+    if (c->ftable.p) (void)hipFree(c->ftable.p);
+    if (c->h_ftable) (void)hipHostFree(c->h_ftable);
     if (c->ev_build) (void)hipEventDestroy(c->ev_build);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -1214,13 +1287,19 @@ __global__ void k_batch_init(const PairDev* __restrict__ tab, int iters) {
     for (int k = t; k < words; k += blockDim.x) tr[k] = 0ull;
 }
 
-__global__ void k_batch_results(const PairDev* __restrict__ tab, int n, double* __restrict__ out) {
+// per frame: pose, iterations, status ([n][kResStride]), then every frame's trace records gathered
+// after them ([n][iters] records) — one device-to-host copy for the whole batch
+__global__ void k_batch_results(const PairDev* __restrict__ tab, int n, double* __restrict__ out, int iters) {
+    const int words = iters * (int)(sizeof(imls_iter_trace) / 8);
+    unsigned long long* tout = reinterpret_cast<unsigned long long*>(out + (size_t)n * kResStride);
     for (int k = blockIdx.x; k < n; k += gridDim.x) {
         const PairDev A = tab[k];
         const int t = threadIdx.x;
         if (t < 16) out[(size_t)k * kResStride + t] = A.st.pose[t];
         if (t == 16) out[(size_t)k * kResStride + 16] = (double)*A.st.iters;
         if (t == 17) out[(size_t)k * kResStride + 17] = (double)*A.st.status;
+        const unsigned long long* tr = reinterpret_cast<const unsigned long long*>(A.trace);
+        for (int w = t; w < words; w += blockDim.x) tout[(size_t)k * words + w] = tr[w];
     }
 }
 
@@ -1296,18 +1375,23 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         return IMLS_OK;
     }
     const int iters = L->P.iterations;
+    const size_t res_bytes = n * (kResStride * sizeof(double) + (size_t)std::max(iters, 0) * sizeof(imls_iter_trace));
     if ((size_t)L->tab_cap < n) {
         if (L->tab_h) (void)hipHostFree(L->tab_h);
-        if (L->res_h) (void)hipHostFree(L->res_h);
         L->tab_h = nullptr;
-        L->res_h = nullptr;
         L->tab_cap = 0;
-        if (hipHostMalloc((void**)&L->tab_h, n * sizeof(PairDev)) != hipSuccess ||
-            hipHostMalloc((void**)&L->res_h, n * kResStride * sizeof(double)) != hipSuccess)
+        if (hipHostMalloc((void**)&L->tab_h, n * sizeof(PairDev)) != hipSuccess)
             return fail(L, IMLS_ERR_DEVICE, "hipHostMalloc (batch)");
         L->tab_cap = (int)n;
     }
-    if (!grow(L->tab_d, n * sizeof(PairDev)) || !grow(L->res_d, n * kResStride * sizeof(double)))
+    if (L->res_h_bytes < res_bytes) {
+        if (L->res_h) (void)hipHostFree(L->res_h);
+        L->res_h = nullptr;
+        L->res_h_bytes = 0;
+        if (hipHostMalloc((void**)&L->res_h, res_bytes) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "hipHostMalloc (batch)");
+        L->res_h_bytes = res_bytes;
+    }
+    if (!grow(L->tab_d, n * sizeof(PairDev)) || !grow(L->res_d, res_bytes))
         return fail(L, IMLS_ERR_DEVICE, "hipMalloc (batch)");
     if (!L->ev_batch && hipEventCreateWithFlags(&L->ev_batch, hipEventDisableTiming) != hipSuccess)
         return fail(L, IMLS_ERR_DEVICE, "hipEventCreate (batch)");
@@ -1349,13 +1433,9 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
             launch_solve_batch(s, tab, nh, (int)n, kp, it);
         timed_end(L, 2, slot);
     }
-    k_batch_results<<<(unsigned)std::min<size_t>(n, 256), 64, 0, s>>>(tab, (int)n, (double*)L->res_d.p);
-    hipMemcpyAsync(L->res_h, L->res_d.p, n * kResStride * sizeof(double), hipMemcpyDeviceToHost, s);
+    k_batch_results<<<(unsigned)std::min<size_t>(n, 1024), 64, 0, s>>>(tab, (int)n, (double*)L->res_d.p, std::max(iters, 0));
+    hipMemcpyAsync(L->res_h, L->res_d.p, res_bytes, hipMemcpyDeviceToHost, s);
     L->batch_traces = iters > 0;
-    if (L->batch_traces)
-        for (size_t k = 0; k < n; ++k)
-            hipMemcpyAsync(ctxs[k]->h_trace, ctxs[k]->trace_mem.p, (size_t)iters * sizeof(imls_iter_trace),
-                           hipMemcpyDeviceToHost, s);
     if (hipGetLastError() != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "batch launch failed");
     // every member's later work (its next uploads / index build) is ordered after the batch
     if (hipEventRecord(L->ev_batch, s) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "batch event");
@@ -1398,7 +1478,10 @@ int frames_result(imls_ctx* L, double* poses_out, int32_t* iters_out, int32_t* s
         if (poses_out) std::memcpy(poses_out + 16 * k, r, 16 * sizeof(double));
         if (iters_out) iters_out[k] = (int32_t)r[16];
         if (status_out) status_out[k] = (int32_t)r[17];
-        if (traces && iters > 0) std::memcpy(traces + k * (size_t)iters, L->members[k]->h_trace, (size_t)iters * sizeof(imls_iter_trace));
+        if (traces && iters > 0)
+            std::memcpy(traces + k * (size_t)iters,
+                        reinterpret_cast<const imls_iter_trace*>(L->res_h + n * kResStride) + k * (size_t)iters,
+                        (size_t)iters * sizeof(imls_iter_trace));
     }
     return IMLS_OK;
 }

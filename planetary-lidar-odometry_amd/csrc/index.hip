@@ -224,6 +224,135 @@ int filter_async(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, De
     return IMLS_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Batched NaN filters (imls_register_frames): every pending filter of a batch's members in three
+// launches — per 256-point block counts, one scan block per job (its kept count also to the
+// job's pinned host word), order-keeping scatter.  Same output as filter_async, frame by frame.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+struct FilterJobDev {
+    const float* soa;                 // SoA6 input [6][n]
+    size_t n;
+    float4 *pt, *nr;                  // kept points / normals
+    unsigned* kept;                   // kept → input index, or null
+    int* d_count;
+    int* h_count;                     // pinned host word
+    int* blk;                         // [nb] block counts → offsets
+};
+
+__device__ __forceinline__ bool finite_at(const float* soa, size_t n, size_t i) {
+    return isfinite(soa[i]) && isfinite(soa[n + i]) && isfinite(soa[2 * n + i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_filter_count_b(const FilterJobDev* __restrict__ jobs) {
+    const FilterJobDev& J = jobs[blockIdx.y];
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if ((size_t)blockIdx.x * kBlock >= J.n) return;
+    const bool keep = i < J.n && finite_at(J.soa, J.n, i);
+    __shared__ int wc[kBlock / 64];
+    const unsigned long long m = __ballot(keep);
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int c = 0;
+        for (int k = 0; k < kBlock / 64; ++k) c += wc[k];
+        J.blk[blockIdx.x] = c;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_filter_scan_b(const FilterJobDev* __restrict__ jobs) {
+    const FilterJobDev& J = jobs[blockIdx.x];
+    const int nb = (int)((J.n + kBlock - 1) / kBlock);
+    __shared__ int sc[1024];
+    int carry = 0;
+    for (int base = 0; base < nb; base += 1024) {
+        const int b = base + threadIdx.x;
+        const int v = b < nb ? J.blk[b] : 0;
+        sc[threadIdx.x] = v;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            const int t = threadIdx.x >= off ? sc[threadIdx.x - off] : 0;
+            __syncthreads();
+            sc[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (b < nb) J.blk[b] = carry + sc[threadIdx.x] - v;
+        __syncthreads();
+        carry += sc[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        *J.d_count = carry;
+        *J.h_count = carry;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_filter_scatter_b(const FilterJobDev* __restrict__ jobs) {
+    const FilterJobDev& J = jobs[blockIdx.y];
+    if ((size_t)blockIdx.x * kBlock >= J.n) return;
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool keep = i < J.n && finite_at(J.soa, J.n, i);
+    __shared__ int wc[kBlock / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(keep);
+    if (lane == 0) wc[wv] = __popcll(m);
+    __syncthreads();
+    if (!keep) return;
+    int o = J.blk[blockIdx.x];
+    for (int k = 0; k < wv; ++k) o += wc[k];
+    o += __popcll(m & ((1ull << lane) - 1ull));
+    const float* s = J.soa;
+    const size_t n = J.n;
+    J.pt[o] = make_float4(s[i], s[n + i], s[2 * n + i], 0.f);
+    J.nr[o] = make_float4(s[3 * n + i], s[4 * n + i], s[5 * n + i], 0.f);
+    if (J.kept) J.kept[o] = (unsigned)i;
+}
+
+}  // namespace
+
+size_t filter_job_bytes() { return sizeof(FilterJobDev); }
+
+int filter_batch(hipStream_t s, const std::vector<FilterJob>& jobs, DevBuf& scratch, DevBuf& table, void* h_table,
+                 size_t h_table_bytes, std::string& err) {
+    const int nj = (int)jobs.size();
+    if (nj == 0) return IMLS_OK;
+    if ((size_t)nj * sizeof(FilterJobDev) > h_table_bytes) { err = "filter table too small"; return IMLS_ERR_CAPACITY; }
+    if (nj > 65535) { err = "too many filter jobs"; return IMLS_ERR_CAPACITY; }
+    size_t blocks = 0, maxn = 1;
+    for (const auto& f : jobs) {
+        blocks += (f.n + kBlock - 1) / kBlock + 64;
+        maxn = std::max(maxn, f.n);
+    }
+    if (!ensure(scratch, blocks * 4 + (size_t)nj * 256 + 4096, err) ||
+        !ensure(table, (size_t)nj * sizeof(FilterJobDev) + 256, err))
+        return IMLS_ERR_DEVICE;
+    char* p = (char*)scratch.p;
+    FilterJobDev* J = (FilterJobDev*)h_table;
+    for (int q = 0; q < nj; ++q) {
+        const FilterJob& f = jobs[q];
+        if (!ensure(*f.pt, f.n * 16 + 16, err) || !ensure(*f.nr, f.n * 16 + 16, err)) return IMLS_ERR_DEVICE;
+        FilterJobDev d{};
+        d.soa = f.soa;
+        d.n = f.n;
+        d.pt = (float4*)f.pt->p;
+        d.nr = (float4*)f.nr->p;
+        d.kept = f.kept;
+        d.d_count = carve<int>(p, 16);
+        d.h_count = f.h_count;
+        d.blk = carve<int>(p, (f.n + kBlock - 1) / kBlock + 1);
+        J[q] = d;
+    }
+    const FilterJobDev* jd = (const FilterJobDev*)table.p;
+    hipMemcpyAsync(table.p, h_table, (size_t)nj * sizeof(FilterJobDev), hipMemcpyHostToDevice, s);
+    const unsigned gx = grid_for(maxn);
+    k_filter_count_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd);
+    k_filter_scan_b<<<nj, 1024, 0, s>>>(jd);
+    k_filter_scatter_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd);
+    if (hipGetLastError() != hipSuccess) { err = "batched filter launch failed"; return IMLS_ERR_DEVICE; }
+    return IMLS_OK;
+}
+
 namespace {
 
 // Permutation (sorted → input index) of n float4 points by 48-bit Morton code over their bbox.

@@ -179,6 +179,18 @@ struct PairDev {
 //     source_order (the source's Morton order = the wave kernels' query order).
 int filter_async(hipStream_t s, const float* d_soa6, size_t n_in, DevBuf& pt, DevBuf& nr, DevBuf& scratch,
                  unsigned* d_kept, int* h_count, std::string& err);
+// (A) for many frames at once (deferred filters of a batch's members), one launch sequence; the
+// kept counts land in each job's pinned host word once the stream has passed it.
+struct FilterJob {
+    const float* soa;
+    size_t n;
+    DevBuf *pt, *nr;                   // grown to n records here
+    unsigned* kept;                    // nullable
+    int* h_count;
+};
+int filter_batch(hipStream_t s, const std::vector<FilterJob>& jobs, DevBuf& scratch, DevBuf& table, void* h_table,
+                 size_t h_table_bytes, std::string& err);
+size_t filter_job_bytes();
 int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& tpt, DevBuf& tnr, DevBuf& mpt,
                       DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* P_out, int* levels_out,
                       std::string& err);
