@@ -533,7 +533,7 @@ int ensure_built(imls_ctx* c) {
 // host wait each, all filters already enqueued), the trees and source orders of all of them; the
 // members' streams are then ordered after it.  Members with per-launch timing on keep their own
 // build (its timing events are on their streams).
-int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n) {
+int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused) {
     bool any = false, timing = false;
     for (size_t k = 0; k < n; ++k) {
         any |= ctxs[k]->tgt_pending || ctxs[k]->src_pending;
@@ -551,14 +551,17 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n) {
         std::vector<FilterJob> fj;
         for (size_t k = 0; k < n; ++k) {
             imls_ctx* c = ctxs[k];
+            // (a join only where the member's stream still has work: an idle stream's is done)
             if (c->tgt_pending && c->tgt_filter_deferred) {
-                if (c != L && hipStreamWaitEvent(L->stream, c->ev_tgt, 0) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "filter join");
+                if (c != L && hipEventQuery(c->ev_tgt) != hipSuccess && hipStreamWaitEvent(L->stream, c->ev_tgt, 0) != hipSuccess)
+                    return fail(L, IMLS_ERR_DEVICE, "filter join");
                 if (!grow(c->tkept, c->tf_n * 4 + 16)) return fail(L, IMLS_ERR_DEVICE, "hipMalloc (kept)");
                 fj.push_back(FilterJob{c->tf_soa, c->tf_n, &c->tpt, &c->tnr, (unsigned*)c->tkept.p, &c->h_cnt[0]});
                 c->tgt_filter_deferred = false;
             }
             if (c->src_pending && c->src_filter_deferred) {
-                if (c != L && hipStreamWaitEvent(L->stream, c->ev_src, 0) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "filter join");
+                if (c != L && hipEventQuery(c->ev_src) != hipSuccess && hipStreamWaitEvent(L->stream, c->ev_src, 0) != hipSuccess)
+                    return fail(L, IMLS_ERR_DEVICE, "filter join");
                 fj.push_back(FilterJob{c->sf_soa, c->sf_n, &c->spt, &c->snr, nullptr, &c->h_cnt[1]});
                 c->src_filter_deferred = false;
             }
@@ -632,8 +635,9 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n) {
             who[q].first->Pl = jobs[q].P;
             who[q].first->levels = jobs[q].levels;
         }
-    // every member's later work on its own stream (its frame's launches when the batch is not fused,
-    // its next uploads) is ordered after the build
+    // every member's later work on its own stream (its frame's launches when the batch is not fused)
+    // is ordered after the build (a fused batch orders them after the whole batch instead)
+    if (fused) return IMLS_OK;
     if (!L->ev_build && hipEventCreateWithFlags(&L->ev_build, hipEventDisableTiming) != hipSuccess)
         return fail(L, IMLS_ERR_DEVICE, "hipEventCreate (build)");
     if (hipEventRecord(L->ev_build, L->stream) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "build event");
@@ -1352,7 +1356,8 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
     }
     // every member's deferred build: its filter count (one wait each, all filters already enqueued)
     // then all the members' index builds in one launch sequence on the lead's stream
-    if (int rc = batch_builds(L, ctxs, n)) return rc;
+    if (int rc = batch_builds(L, ctxs, n, batch_fusable(L) && (L->P.solve_method != IMLS_SOLVE_RANSAC || n <= (size_t)kMaxRansacBatch)))
+        return rc;
     (void)hipSetDevice(L->device);
     for (size_t k = 0; k < n; ++k) {
         imls_ctx* c = ctxs[k];
@@ -1406,8 +1411,9 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         if (int rc = prepare_ransac(c, c->N)) return fail(L, rc, c->err);
         L->tab_h[k] = pair_dev(c);
         L->member_n[k] = c->N;
-        if (c != L) {
-            // the frame's uploads and index build ran on its own stream: the batch waits for them
+        if (c != L && hipStreamQuery(c->stream) != hipSuccess) {
+            // work of the frame still queued on its own stream (uploads, a counted filter or build):
+            // the batch waits for it (an idle stream's work is complete: no join)
             if (!c->ev_batch && hipEventCreateWithFlags(&c->ev_batch, hipEventDisableTiming) != hipSuccess)
                 return fail(L, IMLS_ERR_DEVICE, "hipEventCreate (batch)");
             if (hipEventRecord(c->ev_batch, c->stream) != hipSuccess || hipStreamWaitEvent(s, c->ev_batch, 0) != hipSuccess)

@@ -45,6 +45,7 @@ constexpr int kWaveBlock = 256;
 typedef float kf4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(4))) const kf4v kconst_f4;
 constexpr int kFallbackBlocks = 64;
+constexpr int kFallbackBlocksBatched = 4;   // physical blocks per frame of a large batch (same slabs)
 static_assert(kWaveBlock == kPass1Block && kFallbackBlocks == kPass1Fallback, "pass-1 slab layout (solve.hip)");
 constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query up to this many queries
 constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
@@ -1098,7 +1099,7 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
                                                              float4* __restrict__ cs, float4* __restrict__ cd,
                                                              float4* __restrict__ cn, double* __restrict__ partial1,
                                                              imls_iter_trace* __restrict__ tr,
-                                                             unsigned long long* __restrict__ nbr_stats) {
+                                                             unsigned long long* __restrict__ nbr_stats, int nlog) {
     if (done && *done) return;
     __shared__ uint2 stack[kStackDepth][kProjBlock];
     __shared__ double red[kProjBlock / 64][kNormEq];
@@ -1108,8 +1109,11 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
     if (tid < IMLS_NUM_REJ + 3) rej_s[tid] = 0;
     __syncthreads();
     const int total = qlist ? (int)*qcount : N;
+    // nlog logical blocks (one pass-1 slab each, the rows base = lb·128 + k·nlog·128) taken by the
+    // physical blocks in turn: the slabs do not depend on the physical grid
+    for (int lb = blockIdx.x; lb < nlog; lb += gridDim.x) {
     double acc_out = 0.0;   // thread tid < 28 accumulates its normal-equation term over rounds
-    for (int base = blockIdx.x * kProjBlock; base < total; base += gridDim.x * kProjBlock) {
+    for (int base = lb * kProjBlock; base < total; base += nlog * kProjBlock) {
         const int q = base + tid;
         const bool active = q < total;
         const int i = active ? (qlist ? (int)qlist[q] : q) : 0;
@@ -1240,8 +1244,9 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
         block_normeq<kProjBlock>(a, bb, one, red, out);
         if (tid < kNormEq) acc_out += out[tid];
     }
+    if (tid < kNormEq) partial1[(size_t)lb * kNormEq + tid] = acc_out;
+    }
     __syncthreads();
-    if (tid < kNormEq) partial1[(size_t)blockIdx.x * kNormEq + tid] = acc_out;
     if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
@@ -1287,7 +1292,8 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(
         const unsigned* __restrict__ qcount, int N, const double* __restrict__ pose, const int* __restrict__ done,
         KParams kp, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
         double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats) {
-    project_lane_body<KCAP>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats);
+    project_lane_body<KCAP>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats,
+                            kFallbackBlocks);
 }
 
 __device__ __forceinline__ int wave_blocks_of(int N) { return (N + kWaveBlock - 1) / kWaveBlock; }
@@ -1335,7 +1341,8 @@ template <int KCAP>
 __global__ __launch_bounds__(kProjBlock) void k_project_lane_b(const PairDev* __restrict__ tab, KParams kp, int it) {
     const PairDev A = tab[blockIdx.y];
     project_lane_body<KCAP>(A.t, A.spt, A.snr, A.fb_list, A.fb_count, A.N, A.st.pose, A.st.done, kp, A.cs, A.cd, A.cn,
-                            A.st.partial1 + (size_t)wave_blocks_of(A.N) * kNormEq, A.trace + it, A.stats);
+                            A.st.partial1 + (size_t)wave_blocks_of(A.N) * kNormEq, A.trace + it, A.stats,
+                            kFallbackBlocks);
 }
 
 template <int KL>
@@ -1412,8 +1419,10 @@ void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     else if (K <= 16) launch_wave_batch<20>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else if (K <= 20) launch_wave_batch<22>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else launch_wave_batch<36>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
-    // exact fallback for uncertified queries: every frame's kFallbackBlocks slabs are written
-    const dim3 g(kFallbackBlocks, npairs);
+    // exact fallback for uncertified queries: every frame's kFallbackBlocks slabs are written, by
+    // fewer physical blocks per frame when many frames share the launch (uncertified queries are
+    // rare; a grid of 64 mostly idle blocks per frame cost ~130 µs at 512 frames)
+    const dim3 g(npairs >= 16 ? kFallbackBlocksBatched : kFallbackBlocks, npairs);
     if (K <= 8) k_project_lane_b<8><<<g, kProjBlock, 0, s>>>(tab, kp, it);
     else if (K <= 16) k_project_lane_b<16><<<g, kProjBlock, 0, s>>>(tab, kp, it);
     else if (K <= 20) k_project_lane_b<20><<<g, kProjBlock, 0, s>>>(tab, kp, it);
