@@ -199,11 +199,12 @@ int imls_set_source(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n,
                     size_t stride_floats, size_t* n_kept, uint32_t* kept_index);
 /* Same, for clouds already resident in device memory as SoA float32[6][n]
  * (x[], y[], z[], nx[], ny[], nz[]) — inputs stay in HBM, no PCIe in the hot loop.
- * Deferred mode (n_kept NULL, and no kept_index): the call returns at once; the NaN filter and the
- * index build run at the first use of the cloud (a registration, a projection, or all the frames of
- * an imls_register_frames batch together, in one launch sequence), reading d_soa6 THEN — the
- * device buffer must stay valid and unchanged until that first use.  Host-pointer calls copy their
- * input at the call, so their buffers are free on return. */
+ * Deferred mode (n_kept NULL, and no kept_index): the call returns at once; the index build runs
+ * at the first use of the cloud (a registration, a projection, or all the frames of an
+ * imls_register_frames batch together, in one launch sequence), and when the context was last
+ * registered in a batch of 8 or more frames the NaN filter waits for that first use too, reading
+ * d_soa6 THEN — so the device buffer must stay valid and unchanged until that first use.
+ * Host-pointer calls copy their input at the call, so their buffers are free on return. */
 int imls_set_target_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
 int imls_set_source_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
 

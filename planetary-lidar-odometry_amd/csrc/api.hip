@@ -70,6 +70,7 @@ struct imls_ctx {
     const float* sf_soa = nullptr;
     size_t tf_n = 0, sf_n = 0;
     bool tgt_filter_deferred = false, src_filter_deferred = false;
+    size_t last_batch_n = 0;              // frames of the last batch this context was part of
     int tgt_slot = -1;                    // timing event slot of the pending target build
     uint32_t* src_kept_out = nullptr;
     // pinned staging of host uploads (0: target / map scans, 1: source), reused once its copy ran
@@ -647,6 +648,12 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused) {
     return IMLS_OK;
 }
 
+// A count-less load defers its NaN filter to the first use when the context was last registered
+// in a batch of ≥ kDeferBatch frames (the batch then filters all its members in three launches);
+// otherwise the filter is enqueued at once, behind the context's running work, so it overlaps it.
+constexpr size_t kDeferBatch = 8;
+bool defer_filter(const imls_ctx* c) { return c->last_batch_n >= kDeferBatch; }
+
 int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
     if (n == 0 || n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "target size out of range");
     if (!grow(c->tkept, n * 4 + 16)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (kept)");
@@ -656,7 +663,7 @@ int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
     c->tgt_pending = false;
     c->tgt_filter_deferred = false;
     timed_begin(c, 1, c->tgt_slot);
-    if (n_kept) {
+    if (n_kept || !defer_filter(c)) {
         int rc = filter_async(c->stream, d_soa6, n, c->tpt, c->tnr, c->tscratch, (unsigned*)c->tkept.p, &c->h_cnt[0], c->err);
         if (rc) return rc;
     } else {
@@ -684,7 +691,7 @@ int do_set_source(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept, ui
         return fail(c, IMLS_ERR_DEVICE, "hipEventCreate");
     c->src_pending = false;
     c->src_filter_deferred = false;
-    if (n_kept || kept_index) {
+    if (n_kept || kept_index || !defer_filter(c)) {
         int rc = filter_async(c->stream, d_soa6, n, c->spt, c->snr, c->sscratch, kept_index ? (unsigned*)c->skept.p : nullptr,
                               &c->h_cnt[1], c->err);
         if (rc) return rc;
@@ -1365,6 +1372,7 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
             return fail(L, IMLS_ERR_STATE, "context " + std::to_string(k) + ": set_target and set_source first");
     }
     L->members.assign(ctxs, ctxs + n);
+    for (size_t k = 0; k < n; ++k) ctxs[k]->last_batch_n = n;
     L->batch_fused = batch_fusable(L) && (L->P.solve_method != IMLS_SOLVE_RANSAC || n <= (size_t)kMaxRansacBatch);
     if (!L->batch_fused) {
         // one launch sequence per frame, each on its own context stream
