@@ -195,6 +195,8 @@ KParams make_kparams(const imls_params& p) {
     k.lockstep = 1;
     if (const char* w = std::getenv("IMLS_LOCKSTEP")) k.lockstep = std::atoi(w);
     k.bcast_lock = 0;
+    k.xcd = -1;
+    if (const char* w = std::getenv("IMLS_XCD")) k.xcd = std::atoi(w);
     if (const char* w = std::getenv("IMLS_BCAST_LOCK")) k.bcast_lock = std::atoi(w);
     // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
     // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)

@@ -58,6 +58,7 @@ struct KParams {
     int qverlet;              // the same for the wave-per-query traversal (off by default: measured slower)
     int lockstep;             // packet traversal: per-lane candidate masks, then lockstep insertion
     int bcast_lock;           // … also for broadcast leaves: 0 never, 1 first ICP iteration, 2 always
+    int xcd;                  // batched projection: frames grouped per XCD round-robin slot (−1 auto: ≥ 16 frames)
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
     int tv;                   // tensor-voting normals (use_tensor_voting && !get_normals, IMLS matcher)
     int tv_k;                 // use_tensor_voting.k (≤ kTvMaxK)

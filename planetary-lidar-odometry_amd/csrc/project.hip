@@ -322,14 +322,14 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                                                          int* __restrict__ lists, float* __restrict__ wlist,
                                                          float4* __restrict__ xref, float* __restrict__ nref,
                                                          int use_prev, unsigned long long* __restrict__ nbr_stats,
-                                                         unsigned* __restrict__ fb_count) {
+                                                         unsigned* __restrict__ fb_count, int bx) {
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float4 sbox[kWaveBlock / 64][kWaveStack][2];
     __shared__ float4 sleaf[kWaveBlock / 64][64];   // the current leaf's points (lockstep insertion)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int slot = blockIdx.x * kWaveBlock + tid;
+    const int slot = bx * kWaveBlock + tid;
     const bool active = slot < N;
     float xf[3] = {0.f, 0.f, 0.f};
     if (active) {
@@ -723,7 +723,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         unsigned sins = dbg_sparse_ins;
         for (int o = 1; o < 64; o <<= 1) sins += __shfl_xor(sins, o);
         if (lane == 0) {
-            const int w = blockIdx.x * (kWaveBlock / 64) + wv;
+            const int w = bx * (kWaveBlock / 64) + wv;
             if (w < kDbgWaves) {
                 unsigned* r = g_dbg_wave[w];
                 r[0] = (unsigned)(dbg_t1 - dbg_t0); r[1] = (unsigned)(wall_clock64() - dbg_t1);
@@ -742,7 +742,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     // k_finish's deferred-query counter, zeroed at the END of the kernel: a global store ahead
     // of the traversal may-clobbers every later load, and the node records are then fetched by
     // vector loads instead of through the scalar cache
-    if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = 0u;
+    if (bx == 0 && threadIdx.x == 0) *fb_count = 0u;
 }
 
 // =============================================================================================
@@ -761,14 +761,14 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
                                                           int* __restrict__ lists, float* __restrict__ wlist,
                                                           float4* __restrict__ xref, float* __restrict__ nref,
                                                           int use_prev, unsigned long long* __restrict__ nbr_stats,
-                                                          unsigned* __restrict__ fb_count) {
+                                                          unsigned* __restrict__ fb_count, int bx) {
     static_assert(KL <= 64, "one list entry per lane");
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float sdist[kWaveBlock / 64][kWaveStack];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (kWaveBlock / 64) + wv);
+    const int slot = __builtin_amdgcn_readfirstlane(bx * (kWaveBlock / 64) + wv);
     if (slot >= N) return;
     float xf[3];
     {
@@ -968,7 +968,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
     // k_finish's deferred-query counter, zeroed at the END of the kernel: a global store ahead
     // of the traversal may-clobbers every later load, and the node records are then fetched by
     // vector loads instead of through the scalar cache
-    if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = 0u;
+    if (bx == 0 && threadIdx.x == 0) *fb_count = 0u;
 }
 
 // =============================================================================================
@@ -990,7 +990,8 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
                                                        float4* __restrict__ cn, double* __restrict__ partial1,
                                                        imls_iter_trace* __restrict__ tr,
                                                        unsigned long long* __restrict__ nbr_stats,
-                                                       unsigned* __restrict__ fb_list, unsigned* __restrict__ fb_count) {
+                                                       unsigned* __restrict__ fb_list, unsigned* __restrict__ fb_count,
+                                                       int bx) {
     if (done && *done) return;
     __shared__ double red[kWaveBlock / 64][kNormEq];
     __shared__ double out[kNormEq];
@@ -998,7 +999,7 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
     const int tid = threadIdx.x;
     if (tid < IMLS_NUM_REJ + 3) rej_s[tid] = 0;
     __syncthreads();
-    const int slot = blockIdx.x * kWaveBlock + tid;
+    const int slot = bx * kWaveBlock + tid;
     const bool active = slot < N;
     const int i = active ? (int)qperm[slot] : 0;
     float xf[3] = {0.f, 0.f, 0.f};
@@ -1079,7 +1080,7 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
     double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
     if (cat == -1) { plane_row(xf, yf, nf, a, bb); one = 1.0; }
     block_normeq<kWaveBlock>(a, bb, one, red, out);
-    if (tid < kNormEq) partial1[(size_t)blockIdx.x * kNormEq + tid] = out[tid];
+    if (tid < kNormEq) partial1[(size_t)bx * kNormEq + tid] = out[tid];
     if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
@@ -1263,7 +1264,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(
         int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
         int use_prev, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_count) {
     knn_wave_body<KL, LOCKSTEP>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats,
-                                fb_count);
+                                fb_count, (int)blockIdx.x);
 }
 
 template <int KL>
@@ -1272,7 +1273,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(
         const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
         int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
         int use_prev, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_count) {
-    knn_qwave_body<KL>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats, fb_count);
+    knn_qwave_body<KL>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats, fb_count,
+                       (int)blockIdx.x);
 }
 
 template <int KL>
@@ -1283,7 +1285,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(
         double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats,
         unsigned* __restrict__ fb_list, unsigned* __restrict__ fb_count) {
     finish_body<KL>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr, nbr_stats, fb_list,
-                    fb_count);
+                    fb_count, (int)blockIdx.x);
 }
 
 template <int KCAP>
@@ -1308,33 +1310,60 @@ __device__ __forceinline__ float4* xref_dev(int* lists, int N) {
     return reinterpret_cast<float4*>(reinterpret_cast<char*>(lists) + ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256);
 }
 
+// The (frame, block) a batched block works on.  xcd: blocks are dealt round-robin over the 8 XCDs
+// (b and b + 8 share one, MI355X_MICROARCH.md §Workgroup dispatch), so frame f takes the blocks of
+// one round-robin slot (f mod 8) — its blocks share that XCD's L2 (a frame's map and tree),
+// instead of every frame being spread over all eight.  grid.y is then padded to a multiple of 8.
+__device__ __forceinline__ void batch_block(int xcd, int& frame, int& bx) {
+    if (!xcd) {
+        frame = (int)blockIdx.y;
+        bx = (int)blockIdx.x;
+        return;
+    }
+    const unsigned nx = gridDim.x;
+    const unsigned p = blockIdx.x + blockIdx.y * nx;
+    const unsigned s = p >> 3;
+    frame = (int)((p & 7u) + 8u * (s / nx));
+    bx = (int)(s % nx);
+}
+
 template <int KL, bool LOCKSTEP>
 __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const PairDev* __restrict__ tab, KParams kp,
-                                                                          int use_prev) {
-    const PairDev A = tab[blockIdx.y];
-    if (use_qwave(kp, A.N) || (int)blockIdx.x >= wave_blocks_of(A.N)) return;
+                                                                          int use_prev, int npairs) {
+    int f, bx;
+    batch_block(kp.xcd, f, bx);
+    if (f >= npairs) return;
+    const PairDev A = tab[f];
+    if (use_qwave(kp, A.N) || bx >= wave_blocks_of(A.N)) return;
     float4* xref = xref_dev(A.lists, A.N);
     knn_wave_body<KL, LOCKSTEP>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
                                 wlist_of<KL>(A.lists, A.N), xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats,
-                                A.fb_count);
+                                A.fb_count, bx);
 }
 
 template <int KL>
-__global__ __launch_bounds__(kWaveBlock) void k_knn_qwave_b(const PairDev* __restrict__ tab, KParams kp, int use_prev) {
-    const PairDev A = tab[blockIdx.y];
-    if (!use_qwave(kp, A.N) || (int)blockIdx.x * (kWaveBlock / 64) >= A.N) return;
+__global__ __launch_bounds__(kWaveBlock) void k_knn_qwave_b(const PairDev* __restrict__ tab, KParams kp, int use_prev,
+                                                            int npairs) {
+    int f, bx;
+    batch_block(kp.xcd, f, bx);
+    if (f >= npairs) return;
+    const PairDev A = tab[f];
+    if (!use_qwave(kp, A.N) || bx * (kWaveBlock / 64) >= A.N) return;
     float4* xref = xref_dev(A.lists, A.N);
     knn_qwave_body<KL>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists, wlist_of<KL>(A.lists, A.N),
-                       xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats, A.fb_count);
+                       xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats, A.fb_count, bx);
 }
 
 template <int KL>
 __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish_b(const PairDev* __restrict__ tab, KParams kp,
-                                                                           int it) {
-    const PairDev A = tab[blockIdx.y];
-    if ((int)blockIdx.x >= wave_blocks_of(A.N)) return;
+                                                                           int it, int npairs) {
+    int f, bx;
+    batch_block(kp.xcd, f, bx);
+    if (f >= npairs) return;
+    const PairDev A = tab[f];
+    if (bx >= wave_blocks_of(A.N)) return;
     finish_body<KL>(A.t, A.spt, A.snr, A.qperm, A.N, A.st.pose, A.st.done, kp, A.lists, wlist_of<KL>(A.lists, A.N), A.cs,
-                    A.cd, A.cn, A.st.partial1, A.trace + it, A.stats, A.fb_list, A.fb_count);
+                    A.cd, A.cn, A.st.partial1, A.trace + it, A.stats, A.fb_list, A.fb_count, bx);
 }
 
 template <int KCAP>
@@ -1349,15 +1378,16 @@ template <int KL>
 void launch_wave_batch(hipStream_t s, const PairDev* tab, int npairs, int maxN, bool any_small, bool any_large,
                        const KParams& kp, int it, int use_prev) {
     const int wb = (maxN + kWaveBlock - 1) / kWaveBlock;
+    const int gy = kp.xcd ? (npairs + 7) / 8 * 8 : npairs;
     if (any_small) {
         const int n = kp.qwave > 0 ? maxN : std::min(maxN, kQwaveAutoN);
-        k_knn_qwave_b<KL><<<dim3((n + kWaveBlock / 64 - 1) / (kWaveBlock / 64), npairs), kWaveBlock, 0, s>>>(tab, kp, use_prev);
+        k_knn_qwave_b<KL><<<dim3((n + kWaveBlock / 64 - 1) / (kWaveBlock / 64), gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
     }
     if (any_large) {
-        if (kp.lockstep) k_knn_wave_b<KL, true><<<dim3(wb, npairs), kWaveBlock, 0, s>>>(tab, kp, use_prev);
-        else k_knn_wave_b<KL, false><<<dim3(wb, npairs), kWaveBlock, 0, s>>>(tab, kp, use_prev);
+        if (kp.lockstep) k_knn_wave_b<KL, true><<<dim3(wb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        else k_knn_wave_b<KL, false><<<dim3(wb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
     }
-    k_finish_b<KL><<<dim3(wb, npairs), kWaveBlock, 0, s>>>(tab, kp, it);
+    k_finish_b<KL><<<dim3(wb, gy), kWaveBlock, 0, s>>>(tab, kp, it, npairs);
 }
 
 template <int KCAP>
@@ -1407,6 +1437,8 @@ void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     long long total = 0;
     for (int k = 0; k < npairs; ++k) total += n_host[k];
     if (kp.qwave < 0 && total > kQwaveAutoN) kp.qwave = 0;
+    // XCD-grouped frames for batches of many frames (their maps together outgrow the L2s)
+    if (kp.xcd < 0) kp.xcd = npairs >= 16 ? 1 : 0;
     int maxN = 0;
     bool any_small = false, any_large = false;
     for (int k = 0; k < npairs; ++k) {
