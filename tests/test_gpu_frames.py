@@ -226,3 +226,70 @@ def test_two_batches_in_flight(vlp_pairs):
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_deferred_filters_in_large_batches(vlp_pairs):
+    """After a batch of >= 8 frames a context defers its NaN filter to the first use: the next
+    batch filters and builds all its members in one launch sequence (device inputs, a queue-1 map
+    pushed in place, NaN points in the maps); a member registered alone afterwards filters on its
+    own.  Every result equals a fresh single context fed the same clouds from the host."""
+    p = _params(5)
+    p.max_queue_size = 1
+    frames = []
+    for k in range(10):
+        q = vlp_pairs[k % len(vlp_pairs)]
+        tgt = np.array(q.target, copy=True)
+        tgt["x"][k::17] = np.nan                      # the filter must drop these
+        frames.append((synth.fps_subsample(q.source, 1200 + 37 * k, seed=30 + k), tgt))
+    hip = _hip()
+    dev = [(_DevSoa(hip, synth.soa(s)), _DevSoa(hip, synth.soa(t))) for s, t in frames]
+    ref = _single(p, frames)
+    ctxs = [imls_icp.ImlsContext(p) for _ in frames]
+    try:
+        for rnd in range(2):                          # round 0: filters at once; round 1: deferred
+            for c, (sd, td) in zip(ctxs, dev):
+                c.map_push_device(td.ptr, td.n, count=False)
+                c.set_source_device(sd.ptr, sd.n, count=False)
+            poses, iters, status, _ = imls_icp.register_frames(ctxs)
+            for k, r in enumerate(ref):
+                assert np.array_equal(r["pose"], poses[k]), (rnd, k)
+                assert (r["iters"], r["status"]) == (iters[k], status[k]), (rnd, k)
+        c = ctxs[3]                                   # alone, deferred filters on its own stream
+        sd, td = dev[3]
+        c.map_push_device(td.ptr, td.n, count=False)
+        c.set_source_device(sd.ptr, sd.n, count=False)
+        assert np.array_equal(c.register_frame()["pose"], ref[3]["pose"])
+    finally:
+        for c in ctxs:
+            c.close()
+        for a, b in dev:
+            a.free()
+            b.free()
+
+
+def _hip():
+    """The HIP runtime the product library runs on (device buffers for the *_device entry points;
+    no second runtime in the process)."""
+    import ctypes
+    h = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    h.hipFree.argtypes = [ctypes.c_void_p]
+    return h
+
+
+class _DevSoa:
+    """A (6, n) float32 SoA cloud copied to device memory."""
+
+    def __init__(self, hip, a):
+        import ctypes
+        a = np.ascontiguousarray(a, np.float32)
+        self.hip, self.n = hip, a.shape[1]
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), a.nbytes) == 0
+        assert hip.hipMemcpy(p, a.ctypes.data_as(ctypes.c_void_p), a.nbytes, 1) == 0   # host → device
+        self.ptr = p.value
+
+    def free(self):
+        import ctypes
+        self.hip.hipFree(ctypes.c_void_p(self.ptr))
