@@ -445,7 +445,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--queries", type=int, default=0, help="config B: 0 = all source points; else FPS subsample")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="independent pairs / sequences per step (0 = workload default: B 4, A 64, stream 512)")
+                    help="independent pairs / sequences per step (0 = workload default: B 4, A 256, stream 1024)")
     ap.add_argument("--no-fuse", action="store_true",
                     help="one launch sequence per pair on its own stream instead of one for the whole step")
     ap.add_argument("--unique-seqs", type=int, default=8, help="stream: distinct produced sequences")
@@ -473,7 +473,7 @@ def main():
     # sequences in flight; the small A / stream frames run best as ONE large batch per step (two
     # half batches in flight share hardware queues, so a filter of one half can wait behind the
     # other half's launch sequence)
-    P = args.inflight if args.inflight > 0 else {"B": 4, "A": 64, "stream": 512}[args.workload]
+    P = args.inflight if args.inflight > 0 else {"B": 4, "A": 256, "stream": 1024}[args.workload]
     if args.groups <= 0:
         args.groups = {"B": 4, "A": 1, "stream": 1}[args.workload]
     fuse = not args.no_fuse
