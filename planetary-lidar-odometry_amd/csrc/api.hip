@@ -1316,11 +1316,12 @@ __global__ void k_batch_results(const PairDev* __restrict__ tab, int n, double* 
     }
 }
 
-// The batched path covers both matchers with the LS-family solvers and RANSAC (+ its LS / weighted
-// LS / DRPM final solve); tensor voting, the projected-distance rule and the exact per-lane mode
-// keep one launch sequence per frame (each on its own context stream, so they still overlap).
+// The batched path covers both matchers (tensor-voting normals included) with the LS-family solvers
+// and RANSAC (+ its LS / weighted LS / DRPM final solve); the projected-distance rule and the exact
+// per-lane mode keep one launch sequence per frame (each on its own context stream, so they still
+// overlap).
 bool batch_fusable(const imls_ctx* c) {
-    return !c->lane_mode && !c->kp.proj && !c->kp.tv &&
+    return !c->lane_mode && !c->kp.proj &&
            (c->P.solve_method == IMLS_SOLVE_LS || c->P.solve_method == IMLS_SOLVE_WEIGHTED_LS ||
             c->P.solve_method == IMLS_SOLVE_RANSAC);
 }
@@ -1418,6 +1419,7 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         if (int rc = ensure_trace(c, iters)) return fail(L, rc, c->err);
         if (!grow(c->stats, 128)) return fail(L, IMLS_ERR_DEVICE, "hipMalloc");
         if (int rc = ensure_map_normals(c)) return fail(L, rc, c->err);
+        if (int rc = check_tv_ready(c)) return fail(L, rc, "context " + std::to_string(k) + ": " + c->err);
         if (int rc = prepare_ransac(c, c->N)) return fail(L, rc, c->err);
         L->tab_h[k] = pair_dev(c);
         L->member_n[k] = c->N;

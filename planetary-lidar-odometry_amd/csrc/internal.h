@@ -266,6 +266,7 @@ void launch_tv_vote(hipStream_t s, const TreeView& t, const float4* spt, int N, 
                     const KParams& kp, double4* tvn);
 void launch_tensor_gather(hipStream_t s, const float* ten6_in, size_t n_in, const unsigned* kept, const float4* mpt, int M,
                           float4* mten);
+void launch_tv_vote_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp);
 
 // ransac.hip — RANSAC (+ final LS / weighted LS / DRPM) and the solve-method dispatcher
 constexpr int kHypMax = 8192;          // hypotheses per chunk (chunks: 16, then up to kHypMax each)

@@ -1439,6 +1439,8 @@ void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     if (kp.qwave < 0 && total > kQwaveAutoN) kp.qwave = 0;
     // XCD-grouped frames for batches of many frames (their maps together outgrow the L2s)
     if (kp.xcd < 0) kp.xcd = npairs >= 16 ? 1 : 0;
+    // tensor voting: every frame's voted normals at its current pose first (imls_icp.cpp:514-546)
+    if (kp.tv) launch_tv_vote_batch(s, tab, n_host, npairs, kp);
     int maxN = 0;
     bool any_small = false, any_large = false;
     for (int k = 0; k < npairs; ++k) {

@@ -18,6 +18,7 @@
 // and cut to the best k (the k-th entry then bounds the search).  Finally the buffer is sorted by
 // (d², index), lane j < k computes voter j's S in fp64, lane 0 sums them in list order (the
 // reference's order) and runs the shared 3×3 Jacobi eigensolver.
+#include <algorithm>
 #include <cfloat>
 
 #include "geom.h"
@@ -59,9 +60,9 @@ __device__ void wave_bitonic(unsigned long long* k, unsigned* ix, unsigned* ps, 
         }
 }
 
-__global__ __launch_bounds__(kTvBlock) void k_tv_vote(TreeView t, const float4* __restrict__ spt, int N,
-                                                      const double* __restrict__ pose, const int* __restrict__ done,
-                                                      KParams kp, double4* __restrict__ tvn) {
+__device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __restrict__ spt, int N,
+                                             const double* __restrict__ pose, const int* __restrict__ done,
+                                             const KParams& kp, double4* __restrict__ tvn, int bx) {
     if (done && *done) return;
     __shared__ unsigned long long ck[kTvWaves][kTvCap];   // exact d² bits (positive doubles order as integers)
     __shared__ unsigned ci[kTvWaves][kTvCap];             // filtered target index (the tie order)
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(kTvBlock) void k_tv_vote(TreeView t, const float4* 
     __shared__ double sv[kTvWaves][kTvMaxK][9];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * kTvWaves + wv);
+    const int q = __builtin_amdgcn_readfirstlane(bx * kTvWaves + wv);
     if (q >= N) return;
     float xf[3];
     {
@@ -240,6 +241,19 @@ __global__ __launch_bounds__(kTvBlock) void k_tv_vote(TreeView t, const float4* 
 }
 
 // Input tensors [6][n_in] (input order) → Morton order, 2 float4 per point.
+__global__ __launch_bounds__(kTvBlock) void k_tv_vote(TreeView t, const float4* __restrict__ spt, int N,
+                                                      const double* __restrict__ pose, const int* __restrict__ done,
+                                                      KParams kp, double4* __restrict__ tvn) {
+    tv_vote_body(t, spt, N, pose, done, kp, tvn, (int)blockIdx.x);
+}
+
+// batched (imls_register_frames): frame = tab[blockIdx.y], the same body
+__global__ __launch_bounds__(kTvBlock) void k_tv_vote_b(const PairDev* __restrict__ tab, KParams kp) {
+    const PairDev A = tab[blockIdx.y];
+    if (A.t.M <= 0 || (int)blockIdx.x * kTvWaves >= A.N) return;
+    tv_vote_body(A.t, A.spt, A.N, A.st.pose, A.st.done, kp, const_cast<double4*>(A.t.tvn), (int)blockIdx.x);
+}
+
 __global__ void k_tensor_gather(const float* __restrict__ ten6, size_t n_in, const unsigned* __restrict__ kept,
                                 const float4* __restrict__ mpt, int M, float4* __restrict__ mten) {
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
@@ -255,6 +269,13 @@ void launch_tv_vote(hipStream_t s, const TreeView& t, const float4* spt, int N, 
                     const KParams& kp, double4* tvn) {
     if (N <= 0 || t.M <= 0) return;
     k_tv_vote<<<(N + kTvWaves - 1) / kTvWaves, kTvBlock, 0, s>>>(t, spt, N, pose, done, kp, tvn);
+}
+
+void launch_tv_vote_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp) {
+    int maxN = 0;
+    for (int k = 0; k < npairs; ++k) maxN = std::max(maxN, n_host[k]);
+    if (maxN <= 0) return;
+    k_tv_vote_b<<<dim3((maxN + kTvWaves - 1) / kTvWaves, npairs), kTvBlock, 0, s>>>(tab, kp);
 }
 
 void launch_tensor_gather(hipStream_t s, const float* ten6_in, size_t n_in, const unsigned* kept, const float4* mpt, int M,

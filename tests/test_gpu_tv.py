@@ -134,3 +134,34 @@ def test_tv_nan_target_points_are_skipped(ctx, g):
     wx, wy, wn, widx, wrej = oc.project(g["src"], tgt, g["pose1"], p, tensors=g["ten"])
     assert np.array_equal(rej, wrej) and np.array_equal(idx, widx)
     assert np.abs(n.astype(np.float64) - wn).max() <= N_TOL
+
+
+def test_tv_frames_one_launch(g):
+    """Tensor-voting frames through imls_register_frames (the vote kernel once for the batch,
+    grid y = frame): every frame's pose, iterations, status and trace equal its own
+    register_frame, bit for bit."""
+    p = tv_params()
+    src = rows(g["src"])
+    sources = [src, src[::2].copy(), src[1::3].copy()]
+    single = []
+    with imls_icp.ImlsContext(p) as c:
+        for s in sources:
+            c.set_target(rows(g["tgt"]))
+            c.set_target_tensors(rows(g["ten"]))
+            c.set_source(s)
+            single.append(c.register_frame())
+    ctxs = [imls_icp.ImlsContext(p) for _ in sources]
+    try:
+        for c, s in zip(ctxs, sources):
+            c.set_target(rows(g["tgt"]))
+            c.set_target_tensors(rows(g["ten"]))
+            c.set_source(s)
+        poses, iters, status, traces = imls_icp.register_frames(ctxs)
+    finally:
+        for c in ctxs:
+            c.close()
+    for k, r in enumerate(single):
+        assert np.array_equal(r["pose"], poses[k]), k
+        assert (r["iters"], r["status"]) == (iters[k], status[k]), k
+        for a, b in zip(r["trace"], traces[k]):
+            assert list(a.delta) == list(b.delta) and list(a.reject) == list(b.reject) and a.n_valid == b.n_valid
