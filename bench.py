@@ -147,7 +147,8 @@ class _Pinned:
         os.sched_setaffinity(0, self.prev)
 
 
-def cpu_baseline(src, tgt, p, label: str, min_seconds: float = 10.0, max_pairs: int = 4, faithful_iters: int = 2):
+def cpu_baseline(src, tgt, p, label: str, min_seconds: float = 10.0, max_pairs: int = 4, faithful_iters: int = 2,
+                 tensors=None):
     """The oracle on the same pair (same parameters): (1) "efficient" port, 1 thread pinned: whole
     registrations repeated to >= min_seconds (<= max_pairs); (2) "faithful": the reference's
     container costs (erase per rejection, AoS copies, per-query heap vectors), 1 thread pinned, on
@@ -160,7 +161,7 @@ def cpu_baseline(src, tgt, p, label: str, min_seconds: float = 10.0, max_pairs: 
     with _Pinned() as pin:
         total, n, t_idx = 0.0, 0, 0.0
         while n < max_pairs and (n == 0 or total < min_seconds):
-            r = oc.register_frame(src, tgt, p)
+            r = oc.register_frame(src, tgt, p, tensors=tensors)
             total += r["seconds_total"]
             t_idx += r["seconds_index"]
             n += 1
@@ -168,7 +169,7 @@ def cpu_baseline(src, tgt, p, label: str, min_seconds: float = 10.0, max_pairs: 
         pf.iterations = min(faithful_iters, iters)
         oc.set_faithful(True)
         try:
-            rf = oc.register_frame(src, tgt, pf)
+            rf = oc.register_frame(src, tgt, pf, tensors=tensors)
         finally:
             oc.set_faithful(False)
     t_iter_f = (rf["seconds_total"] - rf["seconds_index"]) / max(rf["iters"], 1)
@@ -176,7 +177,7 @@ def cpu_baseline(src, tgt, p, label: str, min_seconds: float = 10.0, max_pairs: 
     threads = max(1, min(info["affinity_cpus"], int(os.environ.get("OMP_NUM_THREADS") or 10 ** 6)))
     oc.set_threads(threads)
     try:
-        r2 = oc.register_frame(src, tgt, p)
+        r2 = oc.register_frame(src, tgt, p, tensors=tensors)
     finally:
         oc.set_threads(1)
     return dict(
@@ -273,11 +274,16 @@ class PairRunner:
     step's pairs are registered as ONE launch sequence (imls_register_frames); else one launch
     sequence per pair, each on its context's stream."""
 
-    def __init__(self, pairs, p, dev, local, fuse=True, groups=2):
+    def __init__(self, pairs, p, dev, local, fuse=True, groups=2, tensors=False):
         self.fuse = fuse
         self.pairs = pairs
         self.s_dev = [soa_tensor(q.source, dev) for q in pairs]
         self.t_dev = [soa_tensor(q.target, dev) for q in pairs]
+        # config E: the targets' tensor-voting input tensors, SoA (6, M) in HBM
+        self.ten_dev = None
+        if tensors:
+            import torch
+            self.ten_dev = [torch.from_numpy(np.ascontiguousarray(q.meta["tensors"].T)).to(dev).contiguous() for q in pairs]
         self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in pairs]
         self.pipe = Pipeline(self.ctxs, self._prep, groups) if fuse else None
 
@@ -285,6 +291,8 @@ class PairRunner:
         for k in idx:
             q, c = self.pairs[k], self.ctxs[k]
             c.set_target_device(self.t_dev[k].data_ptr(), q.target.size, count=False)
+            if self.ten_dev:
+                c.set_target_tensors_device(self.ten_dev[k].data_ptr(), q.target.size)
             c.set_source_device(self.s_dev[k].data_ptr(), q.source.size, count=False)
 
     def step(self, ctxs=None, idx=None, fuse=None):
@@ -296,6 +304,8 @@ class PairRunner:
         for c, k in zip(ctxs, idx):
             q = self.pairs[k]
             c.set_target_device(self.t_dev[k].data_ptr(), q.target.size)
+            if self.ten_dev:
+                c.set_target_tensors_device(self.ten_dev[k].data_ptr(), q.target.size)
             c.set_source_device(self.s_dev[k].data_ptr(), q.source.size)
             if not fuse:
                 c.register_frame_async()
@@ -458,7 +468,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
     ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
-    ap.add_argument("--workload", choices=["B", "stream", "A"], default="B")
+    ap.add_argument("--workload", choices=["B", "stream", "A", "E"], default="B")
     ap.add_argument("--solver", choices=["LS", "RANSAC_DRPM"], default="LS")
     args = ap.parse_args()
 
@@ -473,11 +483,16 @@ def main():
     # sequences in flight; the small A / stream frames run best as ONE large batch per step (two
     # half batches in flight share hardware queues, so a filter of one half can wait behind the
     # other half's launch sequence)
-    P = args.inflight if args.inflight > 0 else {"B": 4, "A": 256, "stream": 1024}[args.workload]
+    P = args.inflight if args.inflight > 0 else {"B": 4, "A": 256, "stream": 1024, "E": 256}[args.workload]
     if args.groups <= 0:
-        args.groups = {"B": 4, "A": 1, "stream": 1}[args.workload]
+        args.groups = {"B": 4, "A": 1, "stream": 1, "E": 1}[args.workload]
     fuse = not args.no_fuse
     p = solver_params(args.solver, args.iters)
+    if args.workload == "E":
+        # config E: normals by tensor voting (VoteForAny, k 50, σ 0.2, threshold 0.6) on the targets'
+        # input tensors; the map's IMLS normals recomputed in count mode (get_normals false)
+        p.get_normals, p.recompute_normal_count_mode = 0, 1
+        p.use_tensor_voting, p.tensor_k, p.tensor_sigma, p.tensor_distance_threshold = 1, 50, 0.2, 0.6
     t0 = time.time()
     if args.workload == "stream":
         runner = StreamRunner(P, p, local, rank, fuse=fuse, unique=args.unique_seqs, dev=dev,
@@ -486,13 +501,19 @@ def main():
         queries, map_points = runner.queries, runner.map_points
         single = None
     else:
-        model, map_scans = ("vlp16", 1) if args.workload == "A" else ("hdl64", 10)
-        pairs = synth.make_pairs(P, model, map_scans=map_scans, scene_seed=rank, traj_seed=2000 + rank,
-                                 noise_seed=1000 + 97 * rank)
+        if args.workload == "E":
+            # sparse VLP-16 scans over the planetary heightfield (synth.make_planetary_pair: ~10 s of
+            # host ray casting each): two distinct pairs, replayed by the step's contexts
+            uniq = [synth.make_planetary_pair(scene_seed=3 + rank, start=30 + k) for k in range(min(P, 2))]
+            pairs = [uniq[k % len(uniq)] for k in range(P)]
+        else:
+            model, map_scans = ("vlp16", 1) if args.workload == "A" else ("hdl64", 10)
+            pairs = synth.make_pairs(P, model, map_scans=map_scans, scene_seed=rank, traj_seed=2000 + rank,
+                                     noise_seed=1000 + 97 * rank)
         if args.queries > 0:
             pairs = [synth.Pair(synth.fps_subsample(q.source, args.queries, seed=rank), q.target, q.true_pose, q.meta)
                      for q in pairs]
-        runner = PairRunner(pairs, p, dev, local, fuse=fuse, groups=args.groups)
+        runner = PairRunner(pairs, p, dev, local, fuse=fuse, groups=args.groups, tensors=args.workload == "E")
         probe_ctx = runner.ctxs[0]
         queries, map_points = pairs[0].source.size, pairs[0].target.size
         # the probe runs the one-frame launch sequence: its events separate k_knn_wave and k_finish
@@ -554,7 +575,8 @@ def main():
     if world == 1 and not args.no_cpu and args.workload != "stream":
         log("[rank 0] CPU baseline (oracle) ...")
         q0 = runner.pairs[0]
-        cpu = cpu_baseline(synth.soa(q0.source), synth.soa(q0.target), p, f"config {args.workload}")
+        cpu = cpu_baseline(synth.soa(q0.source), synth.soa(q0.target), p, f"config {args.workload}",
+                           tensors=np.ascontiguousarray(q0.meta["tensors"].T) if args.workload == "E" else None)
         log(f"[rank 0] CPU baseline {cpu['value']:.4f} pairs/s (faithful {cpu['faithful']['value']:.4f}, "
             f"{cpu['all_cores']['cores']} cores {cpu['all_cores']['value']:.3f})")
 
@@ -579,6 +601,11 @@ def main():
     if args.workload == "B":
         metric = "IMLS-ICP scan-pairs/s (HDL-64 ~120k-pt scan vs 10-scan map, 20 ICP iterations)"
         workload = f"config B: HDL-64 scan vs 10-scan local map; a step = {P} independent scan pairs" + (" in one launch sequence" if fuse else " in flight, one stream each")
+        unit = "scan-pairs/s"
+    elif args.workload == "E":
+        metric = ("IMLS-ICP scan-pairs/s (config E: tensor-voting normals + IMLS on sparse VLP-16 planetary scans, "
+                  "20 ICP iterations)")
+        workload = f"config E: planetary VLP-16 scan vs the previous scan, tensor voting; a step = {P} independent pairs" + (" in one launch sequence" if fuse else " in flight, one stream each")
         unit = "scan-pairs/s"
     elif args.workload == "A":
         metric = "IMLS-ICP scan-pairs/s (config A: VLP-16 scan vs 1-scan map, 20 ICP iterations)"

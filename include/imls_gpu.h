@@ -233,7 +233,9 @@ int imls_map_size(imls_ctx* ctx, size_t* entries, size_t* points);
  * 535; the DP cloud of setTargetPointCloudDP, 105-144).  n records of 6 floats (xx, xy, xz, yy,
  * yz, zz) at `stride_floats`, in the order of the last imls_set_target's points (n must equal
  * that call's n; records of points its NaN filter dropped are ignored).  Invalidated by the next
- * imls_set_target.  The _device form takes SoA float32[6][n] in device memory. */
+ * imls_set_target.  The _device form takes SoA float32[6][n] in device memory; after a count-less
+ * (deferred) set_target it is read when the target is built (its first use), so it must stay valid
+ * until then. */
 int imls_set_target_tensors(imls_ctx* ctx, const float* tensors, size_t n, size_t stride_floats);
 int imls_set_target_tensors_device(imls_ctx* ctx, const float* d_ten6, size_t n);
 /* The reference's own tensor encoding of per-point PCA features (CustomTensorVoting::

@@ -71,6 +71,9 @@ struct imls_ctx {
     size_t tf_n = 0, sf_n = 0;
     bool tgt_filter_deferred = false, src_filter_deferred = false;
     size_t last_batch_n = 0;              // frames of the last batch this context was part of
+    const float* ten_src = nullptr;       // tensors set while the target build was pending
+    size_t ten_n = 0;
+    bool ten_pending = false;
     int tgt_slot = -1;                    // timing event slot of the pending target build
     uint32_t* src_kept_out = nullptr;
     // pinned staging of host uploads (0: target / map scans, 1: source), reused once its copy ran
@@ -482,6 +485,8 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
     return IMLS_OK;
 }
 
+int gather_tensors(imls_ctx* c, hipStream_t s, const float* d_ten6, size_t n);
+
 // Phase B of a pending target build (waits for its filter's kept count).
 int finish_target(imls_ctx* c) {
     if (!c->tgt_pending) return IMLS_OK;
@@ -500,6 +505,11 @@ int finish_target(imls_ctx* c) {
     timed_end(c, 1, c->tgt_slot);
     c->tgt_slot = -1;
     c->has_target = rc == IMLS_OK && c->M > 0;
+    if (rc == IMLS_OK && c->ten_pending) {
+        c->ten_pending = false;
+        if (c->has_target) rc = gather_tensors(c, c->stream, c->ten_src, c->ten_n);
+        else c->has_tensors = false;
+    }
     return rc;
 }
 
@@ -638,6 +648,13 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused) {
             who[q].first->Pl = jobs[q].P;
             who[q].first->levels = jobs[q].levels;
         }
+    for (size_t k = 0; k < n; ++k) {          // tensors set while the build was pending (config E)
+        imls_ctx* c = ctxs[k];
+        if (!c->ten_pending) continue;
+        c->ten_pending = false;
+        if (!c->has_target) { c->has_tensors = false; continue; }
+        if (int rc = gather_tensors(c, L->stream, c->ten_src, c->ten_n)) return fail(L, rc, c->err);
+    }
     // every member's later work on its own stream (its frame's launches when the batch is not fused)
     // is ordered after the build (a fused batch orders them after the whole batch instead)
     if (fused) return IMLS_OK;
@@ -662,6 +679,7 @@ int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
     if (!c->ev_tgt && hipEventCreateWithFlags(&c->ev_tgt, hipEventDisableTiming) != hipSuccess)
         return fail(c, IMLS_ERR_DEVICE, "hipEventCreate");
     c->has_tensors = false;
+    c->ten_pending = false;
     c->tgt_pending = false;
     c->tgt_filter_deferred = false;
     timed_begin(c, 1, c->tgt_slot);
@@ -714,13 +732,29 @@ int do_set_source(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept, ui
     return IMLS_OK;
 }
 
+// The target's tensors gathered to Morton order (needs the built target: its kept index and order).
+int gather_tensors(imls_ctx* c, hipStream_t s, const float* d_ten6, size_t n) {
+    if (!grow(c->mten, (size_t)std::max(c->M, 1) * 32)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tensors)");
+    launch_tensor_gather(s, d_ten6, n, (const unsigned*)c->tkept.p, (const float4*)c->mpt.p, c->M, (float4*)c->mten.p);
+    if (hipGetLastError() != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "tensor gather launch failed");
+    return IMLS_OK;
+}
+
+// With the target build still pending (a count-less load) the gather waits for it too: it runs
+// right after the build (alone, or with a batch's builds), reading d_ten6 then.
 int do_set_tensors(imls_ctx* c, const float* d_ten6, size_t n) {
-    if (int rc = ensure_built(c)) return rc;
     if (!c->has_target) return fail(c, IMLS_ERR_STATE, "set_target first");
     if (n != c->n_target_in) return fail(c, IMLS_ERR_ARG, "tensor count must equal the last set_target's point count");
-    if (!grow(c->mten, (size_t)std::max(c->M, 1) * 32)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tensors)");
-    launch_tensor_gather(c->stream, d_ten6, n, (const unsigned*)c->tkept.p, (const float4*)c->mpt.p, c->M, (float4*)c->mten.p);
-    if (hipGetLastError() != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "tensor gather launch failed");
+    if (c->tgt_pending) {
+        c->ten_src = d_ten6;
+        c->ten_n = n;
+        c->ten_pending = true;
+        c->has_tensors = true;
+        return IMLS_OK;
+    }
+    if (!c->has_target) return fail(c, IMLS_ERR_STATE, "set_target first");
+    if (int rc = gather_tensors(c, c->stream, d_ten6, n)) return rc;
+    c->ten_pending = false;
     c->has_tensors = true;
     return IMLS_OK;
 }
