@@ -1447,15 +1447,29 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         return fail(L, IMLS_ERR_DEVICE, "hipEventCreate (batch)");
     hipStream_t s = L->stream;
     L->member_n.assign(n, 0);
+    bool any_nrm = false;
+    int max_m = 0;
     for (size_t k = 0; k < n; ++k) {
         imls_ctx* c = ctxs[k];
         if (int rc = ensure_solve(c, c->N)) return fail(L, rc, c->err);
         if (int rc = ensure_trace(c, iters)) return fail(L, rc, c->err);
         if (!grow(c->stats, 128)) return fail(L, IMLS_ERR_DEVICE, "hipMalloc");
-        if (int rc = ensure_map_normals(c)) return fail(L, rc, c->err);
+        // count-mode map normals (get_normals false): flagged here, computed for all the frames that
+        // need them by one batched launch ahead of the iterations
+        const bool need_nrm = !c->P.get_normals && c->P.recompute_normal_count_mode &&
+                              !(c->rnr_valid && c->rnr_k == c->P.search_number_normal && c->rnr_r == c->P.r_normal);
+        if (need_nrm) {
+            if (!grow(c->rnr, (size_t)std::max(c->M, 1) * 16)) return fail(L, IMLS_ERR_DEVICE, "hipMalloc (normals)");
+            c->rnr_valid = true;
+            c->rnr_k = c->P.search_number_normal;
+            c->rnr_r = c->P.r_normal;
+            any_nrm = true;
+            max_m = std::max(max_m, c->M);
+        }
         if (int rc = check_tv_ready(c)) return fail(L, rc, "context " + std::to_string(k) + ": " + c->err);
         if (int rc = prepare_ransac(c, c->N)) return fail(L, rc, c->err);
         L->tab_h[k] = pair_dev(c);
+        L->tab_h[k].recompute_normals = need_nrm ? 1 : 0;
         L->member_n[k] = c->N;
         if (c != L && hipStreamQuery(c->stream) != hipSuccess) {
             // work of the frame still queued on its own stream (uploads, a counted filter or build):
@@ -1470,6 +1484,8 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
     const PairDev* tab = (const PairDev*)L->tab_d.p;
     hipMemcpyAsync(L->tab_d.p, L->tab_h, n * sizeof(PairDev), hipMemcpyHostToDevice, s);
     k_batch_init<<<(unsigned)n, 64, 0, s>>>(tab, iters);
+    if (any_nrm && launch_map_normals_batch(s, tab, (int)n, max_m, L->P.search_number_normal, L->P.r_normal))
+        return fail(L, IMLS_ERR_DEVICE, "batched map normal launch failed");
     const KParams kp = L->kp;
     const RansacParams rp = ransac_params(L->P);
     const int* nh = L->member_n.data();

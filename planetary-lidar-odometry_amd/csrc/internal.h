@@ -171,6 +171,7 @@ struct PairDev {
     unsigned* fb_list;                 // uncertified queries (exact fallback) + their count
     unsigned* fb_count;
     RansacFrame rf;                    // RANSAC scratch (solve_method RANSAC), else zero
+    int recompute_normals;             // map normals (count mode) to compute into t.mnr before the batch
 };
 
 // index.hip — two phases, so many frames' uploads and filters can be enqueued before one wait:
@@ -259,6 +260,7 @@ void launch_rows_pass1_batch(hipStream_t s, const PairDev* tab, const int* cap_h
 
 // normals.hip — map normals recomputed from the map (get_normals=false, count mode), Morton order
 int launch_map_normals(hipStream_t s, const TreeView& t, int K, double r_normal, float4* out);
+int launch_map_normals_batch(hipStream_t s, const PairDev* tab, int npairs, int maxM, int K, double r_normal);
 
 // tv.hip — tensor voting (VoteForAny, imls_icp.cpp:171-296): the voted normal of every source point
 // at the current pose → tvn[N]; input tensors gathered to Morton order once per target

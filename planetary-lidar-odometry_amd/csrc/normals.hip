@@ -22,10 +22,10 @@ constexpr int kNrmBlock = 128;
 constexpr float kNrmSlack = 1.0f + 2e-6f;
 
 template <int KC>
-__global__ __launch_bounds__(kNrmBlock) void k_map_normals(TreeView t, int K, double r2, float4* __restrict__ out) {
+__device__ __forceinline__ void map_normals_body(const TreeView& t, int K, double r2, float4* __restrict__ out, int bx) {
     __shared__ uint2 stack[kStackDepth][kNrmBlock];
     const int tid = threadIdx.x;
-    const int pos = blockIdx.x * kNrmBlock + tid;
+    const int pos = bx * kNrmBlock + tid;
     if (pos >= t.M) return;
     const float4 q4 = t.mpt[pos];
     const float xf[3] = {q4.x, q4.y, q4.z};
@@ -143,7 +143,31 @@ __global__ __launch_bounds__(kNrmBlock) void k_map_normals(TreeView t, int K, do
     out[pos] = make_float4((float)nr[0], (float)nr[1], (float)nr[2], 0.f);
 }
 
+template <int KC>
+__global__ __launch_bounds__(kNrmBlock) void k_map_normals(TreeView t, int K, double r2, float4* __restrict__ out) {
+    map_normals_body<KC>(t, K, r2, out, (int)blockIdx.x);
+}
+
+// batched (imls_register_frames): the maps of the frames flagged recompute_normals, grid y = frame
+template <int KC>
+__global__ __launch_bounds__(kNrmBlock) void k_map_normals_b(const PairDev* __restrict__ tab, int K, double r2) {
+    const PairDev A = tab[blockIdx.y];
+    if (!A.recompute_normals || (int)blockIdx.x * kNrmBlock >= A.t.M) return;
+    map_normals_body<KC>(A.t, K, r2, const_cast<float4*>(A.t.mnr), (int)blockIdx.x);
+}
+
 }  // namespace
+
+int launch_map_normals_batch(hipStream_t s, const PairDev* tab, int npairs, int maxM, int K, double r_normal) {
+    if (maxM <= 0 || npairs <= 0) return 0;
+    const dim3 g((maxM + kNrmBlock - 1) / kNrmBlock, npairs);
+    const double r2 = r_normal * r_normal;
+    if (K <= 8) k_map_normals_b<8><<<g, kNrmBlock, 0, s>>>(tab, K, r2);
+    else if (K <= 16) k_map_normals_b<16><<<g, kNrmBlock, 0, s>>>(tab, K, r2);
+    else if (K <= 32) k_map_normals_b<32><<<g, kNrmBlock, 0, s>>>(tab, K, r2);
+    else return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_map_normals(hipStream_t s, const TreeView& t, int K, double r_normal, float4* out) {
     if (t.M <= 0) return 0;
