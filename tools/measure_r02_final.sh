@@ -20,6 +20,7 @@ step bench_stream_host 300 python3 bench.py --workload stream --no-cpu --host-in
 step bench_stream_ransac 400 python3 bench.py --workload stream --no-cpu --solver RANSAC_DRPM
 step bench_A 400 python3 bench.py --workload A
 step bench_A_ransac 400 python3 bench.py --workload A --solver RANSAC_DRPM
+step bench_E 500 python3 bench.py --workload E
 step kt_stream 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_stream -o run -- python3 bench.py --workload stream --no-cpu --steps 4 --warmup 1
 step kt_driver 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_driver -o run -- python3 bench.py --no-cpu
 step kt_single 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_single -o run -- python3 bench.py --no-cpu --inflight 1 --no-fuse --steps 5 --warmup 1
