@@ -69,7 +69,6 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
     __shared__ unsigned cp[kTvWaves][kTvCap];             // Morton position
     __shared__ int snode[kTvWaves][kTvStack];
     __shared__ float sdist[kTvWaves][kTvStack];
-    __shared__ double sv[kTvWaves][kTvMaxK][9];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = __builtin_amdgcn_readfirstlane(bx * kTvWaves + wv);
@@ -165,8 +164,8 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
     if (cnt > 0) sort_buffer();
     const int kk = min(cnt, K);
     // voter j = list entry j (lane j): S = w·(R·T)·R' in fp64, the oracle's evaluation order
+    double S[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (lane < kk) {
-        double S[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         const int pos = (int)wp[lane];
         const float4 p4 = t.mpt[pos];
         const double r[3] = {xd[0] - (double)p4.x, xd[1] - (double)p4.y, xd[2] - (double)p4.z};
@@ -213,15 +212,14 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
                     S[a * 3 + b] = w * s;
                 }
         }
-#pragma unroll
-        for (int e = 0; e < 9; ++e) sv[wv][lane][e] = S[e];
     }
-    wave_sync();
-    if (lane != 0) return;
+    // the votes summed in list order (the reference's), read lane by lane (no LDS staging: the
+    // block's LDS then admits a fifth resident wave per SIMD)
     double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < kk; ++j)
 #pragma unroll
-        for (int e = 0; e < 9; ++e) acc[e] += sv[wv][j][e];
+        for (int e = 0; e < 9; ++e) acc[e] += readlane_f64(S[e], j);
+    if (lane != 0) return;
     bool zero = true;
 #pragma unroll
     for (int e = 0; e < 9; ++e) zero = zero && fabs(acc[e]) <= 1e-12;
