@@ -4,7 +4,9 @@
 // `iterations` × {k_project, solve chain} launches are enqueued back to back on the context
 // stream; convergence / too-few-correspondence exits are taken on the device (a `done` flag
 // every later launch checks first), so the host synchronises once per frame.
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -541,12 +543,31 @@ int ensure_built(imls_ctx* c) {
     return finish_source(c);
 }
 
+// IMLS_DEBUG_HOST=1: host-time split of imls_register_frames_async on stderr (diagnostics only)
+struct HostSplit {
+    bool on = std::getenv("IMLS_DEBUG_HOST") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
+    char buf[512];
+    int len = 0;
+    void mark(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        len += std::snprintf(buf + len, sizeof(buf) - (size_t)len, " %s %.2f", what,
+                             std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+    ~HostSplit() {
+        if (on) std::fprintf(stderr, "[imls host ms]%s total %.2f\n", buf,
+                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+
 // The pending builds of a batch's members in ONE launch sequence on the lead's stream (index.hip
 // build_batch: one radix sort for every frame's points): after each member's filter count (one
 // host wait each, all filters already enqueued), the trees and source orders of all of them; the
 // members' streams are then ordered after it.  Members with per-launch timing on keep their own
 // build (its timing events are on their streams).
-int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused) {
+int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused, HostSplit* hs = nullptr) {
     bool any = false, timing = false;
     for (size_t k = 0; k < n; ++k) {
         any |= ctxs[k]->tgt_pending || ctxs[k]->src_pending;
@@ -590,7 +611,9 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused) {
             }
             (void)hipSetDevice(L->device);
             if (int rc = filter_batch(L->stream, fj, L->fscratch, L->ftable, L->h_ftable, L->h_ftable_bytes, L->err)) return rc;
+            if (hs) hs->mark("filter-launch");
             if (hipStreamSynchronize(L->stream) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "batched filter failed");
+            if (hs) hs->mark("filter-wait");
         }
     }
     std::vector<BuildJob> jobs;
@@ -1382,6 +1405,7 @@ PairDev pair_dev(imls_ctx* c) {
 
 int frames_async(imls_ctx* const* ctxs, size_t n) {
     if (!ctxs || n == 0 || !ctxs[0]) return IMLS_ERR_ARG;
+    HostSplit hs;
     imls_ctx* L = ctxs[0];
     if (L->batch_pending) return fail(L, IMLS_ERR_STATE, "a batch led by this context is pending");
     if (int rc = check_device(L)) return rc;
@@ -1400,8 +1424,10 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
     }
     // every member's deferred build: its filter count (one wait each, all filters already enqueued)
     // then all the members' index builds in one launch sequence on the lead's stream
-    if (int rc = batch_builds(L, ctxs, n, batch_fusable(L) && (L->P.solve_method != IMLS_SOLVE_RANSAC || n <= (size_t)kMaxRansacBatch)))
+    hs.mark("checks");
+    if (int rc = batch_builds(L, ctxs, n, batch_fusable(L) && (L->P.solve_method != IMLS_SOLVE_RANSAC || n <= (size_t)kMaxRansacBatch), &hs))
         return rc;
+    hs.mark("filters+builds");
     (void)hipSetDevice(L->device);
     for (size_t k = 0; k < n; ++k) {
         imls_ctx* c = ctxs[k];
@@ -1481,6 +1507,7 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         }
     }
     (void)hipSetDevice(L->device);
+    hs.mark("members");
     const PairDev* tab = (const PairDev*)L->tab_d.p;
     hipMemcpyAsync(L->tab_d.p, L->tab_h, n * sizeof(PairDev), hipMemcpyHostToDevice, s);
     k_batch_init<<<(unsigned)n, 64, 0, s>>>(tab, iters);
@@ -1501,6 +1528,7 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
             launch_solve_batch(s, tab, nh, (int)n, kp, it);
         timed_end(L, 2, slot);
     }
+    hs.mark("iterations");
     k_batch_results<<<(unsigned)std::min<size_t>(n, 1024), 64, 0, s>>>(tab, (int)n, (double*)L->res_d.p, std::max(iters, 0));
     hipMemcpyAsync(L->res_h, L->res_d.p, res_bytes, hipMemcpyDeviceToHost, s);
     L->batch_traces = iters > 0;
