@@ -209,6 +209,8 @@ KParams make_kparams(const imls_params& p) {
     k.tv_k = p.tensor_k;
     k.tv_sigma = p.tensor_sigma;
     k.tv_thr = p.tensor_distance_threshold;
+    k.tv_skin = 0.03f;
+    if (const char* w = std::getenv("IMLS_TV_SKIN")) k.tv_skin = (float)std::atof(w);
     k.cos_thr = std::cos(k.angle_thr_deg * M_PI / 180.0);
     return k;
 }
@@ -247,7 +249,7 @@ int ensure_solve(imls_ctx* c, int N) {
     if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, n * 4 + 256))
         return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
     if (!grow(c->prevnn, prevnn_bytes((int)n))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
-    if (!grow(c->tvn, n * sizeof(double4))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tvn)");
+    if (!grow(c->tvn, n * kTvBytesPerQuery)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tvn)");
     const int pb = std::max(project_blocks((int)n), solve_blocks((int)n)) + 1;
     size_t bytes = 0;
     auto add = [&](size_t b) { size_t o = bytes; bytes += (b + 255) / 256 * 256; return o; };

@@ -63,8 +63,13 @@ struct KParams {
     int tv;                   // tensor-voting normals (use_tensor_voting && !get_normals, IMLS matcher)
     int tv_k;                 // use_tensor_voting.k (≤ kTvMaxK)
     double tv_sigma, tv_thr;  // use_tensor_voting.sigma, .distance_threshold
+    float tv_skin;            // TV ball lists reused while the query moved ≤ skin (m); 0 = every iteration walks the tree
 };
 constexpr int kTvMaxK = 64;    // tensor-voting kNN size handled on device
+constexpr int kTvList = 64;    // TV skin list: ball(ρ + skin) members stored per query (more: not stored)
+// per-query TV state behind TreeView::tvn: voted normal (double4), skin reference (float4: x, count),
+// skin list (kTvList Morton positions)
+constexpr size_t kTvBytesPerQuery = 32 + 16 + 4 * kTvList;
 
 struct TreeView {
     const float4* mpt;        // map points in Morton order, w = original index (bits)
@@ -265,10 +270,11 @@ int launch_map_normals_batch(hipStream_t s, const PairDev* tab, int npairs, int 
 // tv.hip — tensor voting (VoteForAny, imls_icp.cpp:171-296): the voted normal of every source point
 // at the current pose → tvn[N]; input tensors gathered to Morton order once per target
 void launch_tv_vote(hipStream_t s, const TreeView& t, const float4* spt, int N, const double* pose, const int* done,
-                    const KParams& kp, double4* tvn);
+                    const KParams& kp, double4* tvn, int use_prev);
 void launch_tensor_gather(hipStream_t s, const float* ten6_in, size_t n_in, const unsigned* kept, const float4* mpt, int M,
                           float4* mten);
-void launch_tv_vote_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp);
+void launch_tv_vote_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp,
+                          int use_prev);
 
 // ransac.hip — RANSAC (+ final LS / weighted LS / DRPM) and the solve-method dispatcher
 constexpr int kHypMax = 8192;          // hypotheses per chunk (chunks: 16, then up to kHypMax each)

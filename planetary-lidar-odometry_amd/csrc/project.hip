@@ -1440,7 +1440,7 @@ void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     // XCD-grouped frames for batches of many frames (their maps together outgrow the L2s)
     if (kp.xcd < 0) kp.xcd = npairs >= 16 ? 1 : 0;
     // tensor voting: every frame's voted normals at its current pose first (imls_icp.cpp:514-546)
-    if (kp.tv) launch_tv_vote_batch(s, tab, n_host, npairs, kp);
+    if (kp.tv) launch_tv_vote_batch(s, tab, n_host, npairs, kp, use_prev);
     int maxN = 0;
     bool any_small = false, any_large = false;
     for (int k = 0; k < npairs; ++k) {
@@ -1473,7 +1473,7 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
     double* p_fb = partial1 + (size_t)wblocks * kNormEq;
     const int K = kp.K;
     // tensor voting: every source point's voted normal at this pose first (imls_icp.cpp:514-546)
-    if (kp.tv) launch_tv_vote(s, t, spt, N, pose, done, kp, const_cast<double4*>(t.tvn));
+    if (kp.tv) launch_tv_vote(s, t, spt, N, pose, done, kp, const_cast<double4*>(t.tvn), use_prev);
     if (lane_mode || kp.proj) {
         // reference mode: every query through the exact per-lane kernel (grid-stride over the
         // fallback slabs); the wave slabs are zeroed

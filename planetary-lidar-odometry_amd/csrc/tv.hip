@@ -60,9 +60,15 @@ __device__ void wave_bitonic(unsigned long long* k, unsigned* ix, unsigned* ps, 
         }
 }
 
+// fp32 screen distance (the one definition every ball test uses)
+__device__ __forceinline__ float screen_d2(const float4& p4, const float* xf) {
+    const float ex = p4.x - xf[0], ey = p4.y - xf[1], ez = p4.z - xf[2];
+    return __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+}
+
 __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __restrict__ spt, int N,
                                              const double* __restrict__ pose, const int* __restrict__ done,
-                                             const KParams& kp, double4* __restrict__ tvn, int bx) {
+                                             const KParams& kp, double4* __restrict__ tvn, int use_prev, int bx) {
     if (done && *done) return;
     __shared__ unsigned long long ck[kTvWaves][kTvCap];   // exact d² bits (positive doubles order as integers)
     __shared__ unsigned ci[kTvWaves][kTvCap];             // filtered target index (the tie order)
@@ -97,8 +103,78 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
         wave_sync();
         wave_bitonic(wk, wi, wp, n, lane);
     };
+    // skin lists (Verlet): a walk stores every point of the ball of radius ρ' + skin around x (ρ' the
+    // screen radius) when they fit kTvList; while the query stays within skin of that x the ball of
+    // x is a subset of the stored set, so the stored set screened at x gives the same members as a
+    // walk — bit-identical lists, no tree descent.  Margins (1e-5) cover the fp32 screens.
+    const float skin = kp.tv_skin;
+    float4* tref = reinterpret_cast<float4*>(tvn + N);
+    unsigned* tlist = reinterpret_cast<unsigned*>(tref + N) + (size_t)q * kTvList;
+    bool reuse = false;
+    int nst = 0;
+    if (use_prev && skin > 0.f) {
+        const float4 xr = tref[q];
+        const float dx = xf[0] - xr.x, dy = xf[1] - xr.y, dz = xf[2] - xr.z;
+        reuse = xr.w >= 0.f && dx * dx + dy * dy + dz * dz <= skin * skin * (1.0f - 1e-4f);
+        nst = (int)xr.w;
+    }
+    bool wide = !reuse && skin > 0.f;   // this walk collects the skin ball (self matches included)
+    if (wide) {
+        const float rs = sqrtf(r2s) * (1.0f + 1e-5f) + skin;
+        bnd = rs * rs * (1.0f + 1e-5f);
+    }
+    // keep only the screened ball members proper (d32 ≤ r2s, no self match), in buffer order
+    auto compact_ball = [&]() {
+        int nc = 0;
+        for (int a0 = 0; a0 < cnt; a0 += 64) {
+            const int a = a0 + lane;
+            bool keep = false;
+            unsigned long long k0 = 0ull;
+            unsigned i0 = 0u, p0 = 0u;
+            if (a < cnt) {
+                k0 = wk[a];
+                i0 = wi[a];
+                p0 = wp[a];
+                keep = screen_d2(t.mpt[p0], xf) <= r2s && __longlong_as_double((long long)k0) > DBL_EPSILON;
+            }
+            const unsigned long long mk = __ballot(keep);
+            wave_sync();
+            if (keep) {
+                const int at = nc + __popcll(mk & ((1ull << lane) - 1ull));
+                wk[at] = k0;
+                wi[at] = i0;
+                wp[at] = p0;
+            }
+            nc += __popcll(mk);
+            wave_sync();
+        }
+        cnt = nc;
+    };
     const int P = t.P, B = t.B, M = t.M;
-    int node = 1, sp = 0;
+    int node = reuse ? 0 : 1, sp = 0;
+    if (reuse) {
+        bool pass = false;
+        unsigned long long key = 0ull;
+        unsigned oi = 0u, pos = 0u;
+        if (lane < nst) {
+            pos = tlist[lane];
+            const float4 p4 = t.mpt[pos];
+            if (screen_d2(p4, xf) <= r2s) {
+                const double d2 = exact_d2(xd, p4.x, p4.y, p4.z);
+                key = (unsigned long long)__double_as_longlong(d2);
+                oi = __float_as_uint(p4.w);
+                pass = d2 > DBL_EPSILON;
+            }
+        }
+        const unsigned long long m = __ballot(pass);
+        if (pass) {
+            const int at = __popcll(m & ((1ull << lane) - 1ull));
+            wk[at] = key;
+            wi[at] = oi;
+            wp[at] = pos;
+        }
+        cnt = __popcll(m);
+    }
     while (node) {
         if (node < P) {
             const float4* rec = t.nodes + 3 * (size_t)node;
@@ -122,18 +198,26 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
             bool pass = false;
             unsigned long long key = 0ull;
             unsigned oi = 0u;
+            float d32 = __builtin_inff();
             if (lane < cl) {
                 const float4 p4 = t.mpt[base + lane];
-                const float ex = p4.x - xf[0], ey = p4.y - xf[1], ez = p4.z - xf[2];
-                const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                d32 = screen_d2(p4, xf);
                 if (d32 <= bnd) {
                     const double d2 = exact_d2(xd, p4.x, p4.y, p4.z);
                     key = (unsigned long long)__double_as_longlong(d2);
                     oi = __float_as_uint(p4.w);
-                    pass = d2 > DBL_EPSILON && (key < bk || (key == bk && oi < bi));   // no self match (197)
+                    pass = (wide || d2 > DBL_EPSILON) && (key < bk || (key == bk && oi < bi));   // no self match (197)
                 }
             }
             unsigned long long m = __ballot(pass);
+            if (wide && cnt + __popcll(m) > kTvCap) {
+                // the skin ball overflows: no list for this query; back to the ball proper
+                wide = false;
+                bnd = r2s;
+                compact_ball();
+                pass = pass && d32 <= r2s && __longlong_as_double((long long)key) > DBL_EPSILON;
+                m = __ballot(pass);
+            }
             if (cnt + __popcll(m) > kTvCap) {
                 // cut to the best k; its k-th entry bounds everything after
                 sort_buffer();
@@ -160,6 +244,15 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
             if (sdist[wv][sp] <= bnd * kTvSlack) { node = snode[wv][sp]; break; }
         }
         node = __builtin_amdgcn_readfirstlane(node);
+    }
+    if (wide) {
+        // the walk's skin ball: stored when it fits, then cut to the ball proper
+        const bool fits = cnt <= kTvList;
+        if (fits && lane < cnt) tlist[lane] = wp[lane];
+        if (lane == 0) tref[q] = make_float4(xf[0], xf[1], xf[2], fits ? (float)cnt : -1.f);
+        compact_ball();
+    } else if (!reuse && skin > 0.f && lane == 0) {
+        tref[q] = make_float4(0.f, 0.f, 0.f, -1.f);
     }
     if (cnt > 0) sort_buffer();
     const int kk = min(cnt, K);
@@ -241,15 +334,15 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
 // Input tensors [6][n_in] (input order) → Morton order, 2 float4 per point.
 __global__ __launch_bounds__(kTvBlock) void k_tv_vote(TreeView t, const float4* __restrict__ spt, int N,
                                                       const double* __restrict__ pose, const int* __restrict__ done,
-                                                      KParams kp, double4* __restrict__ tvn) {
-    tv_vote_body(t, spt, N, pose, done, kp, tvn, (int)blockIdx.x);
+                                                      KParams kp, double4* __restrict__ tvn, int use_prev) {
+    tv_vote_body(t, spt, N, pose, done, kp, tvn, use_prev, (int)blockIdx.x);
 }
 
 // batched (imls_register_frames): frame = tab[blockIdx.y], the same body
-__global__ __launch_bounds__(kTvBlock) void k_tv_vote_b(const PairDev* __restrict__ tab, KParams kp) {
+__global__ __launch_bounds__(kTvBlock) void k_tv_vote_b(const PairDev* __restrict__ tab, KParams kp, int use_prev) {
     const PairDev A = tab[blockIdx.y];
     if (A.t.M <= 0 || (int)blockIdx.x * kTvWaves >= A.N) return;
-    tv_vote_body(A.t, A.spt, A.N, A.st.pose, A.st.done, kp, const_cast<double4*>(A.t.tvn), (int)blockIdx.x);
+    tv_vote_body(A.t, A.spt, A.N, A.st.pose, A.st.done, kp, const_cast<double4*>(A.t.tvn), use_prev, (int)blockIdx.x);
 }
 
 __global__ void k_tensor_gather(const float* __restrict__ ten6, size_t n_in, const unsigned* __restrict__ kept,
@@ -264,16 +357,17 @@ __global__ void k_tensor_gather(const float* __restrict__ ten6, size_t n_in, con
 }  // namespace
 
 void launch_tv_vote(hipStream_t s, const TreeView& t, const float4* spt, int N, const double* pose, const int* done,
-                    const KParams& kp, double4* tvn) {
+                    const KParams& kp, double4* tvn, int use_prev) {
     if (N <= 0 || t.M <= 0) return;
-    k_tv_vote<<<(N + kTvWaves - 1) / kTvWaves, kTvBlock, 0, s>>>(t, spt, N, pose, done, kp, tvn);
+    k_tv_vote<<<(N + kTvWaves - 1) / kTvWaves, kTvBlock, 0, s>>>(t, spt, N, pose, done, kp, tvn, use_prev);
 }
 
-void launch_tv_vote_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp) {
+void launch_tv_vote_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp,
+                          int use_prev) {
     int maxN = 0;
     for (int k = 0; k < npairs; ++k) maxN = std::max(maxN, n_host[k]);
     if (maxN <= 0) return;
-    k_tv_vote_b<<<dim3((maxN + kTvWaves - 1) / kTvWaves, npairs), kTvBlock, 0, s>>>(tab, kp);
+    k_tv_vote_b<<<dim3((maxN + kTvWaves - 1) / kTvWaves, npairs), kTvBlock, 0, s>>>(tab, kp, use_prev);
 }
 
 void launch_tensor_gather(hipStream_t s, const float* ten6_in, size_t n_in, const unsigned* kept, const float4* mpt, int M,

@@ -165,3 +165,44 @@ def test_tv_frames_one_launch(g):
         assert (r["iters"], r["status"]) == (iters[k], status[k]), k
         for a, b in zip(r["trace"], traces[k]):
             assert list(a.delta) == list(b.delta) and list(a.reject) == list(b.reject) and a.n_valid == b.n_valid
+
+
+@pytest.mark.parametrize("skin", ["0.01", "0.03", "0.3"])
+def test_tv_skin_lists_bit_identical(g, monkeypatch, skin):
+    """Skin lists (a walk stores the ball of ρ + skin; later iterations screen the stored set while
+    the query moved ≤ skin) must not change a single bit: register_frame and the batched frames
+    path with lists on equal the walk-every-iteration run (IMLS_TV_SKIN=0).  0.3 m overflows the
+    64-entry lists for most queries (the no-list path)."""
+    p = tv_params()
+    src = rows(g["src"])
+    sources = [src, src[::2].copy()]
+
+    def run(sk):
+        monkeypatch.setenv("IMLS_TV_SKIN", sk)
+        out = []
+        with imls_icp.ImlsContext(p) as c:
+            for s in sources:
+                c.set_target(rows(g["tgt"]))
+                c.set_target_tensors(rows(g["ten"]))
+                c.set_source(s)
+                out.append(c.register_frame())
+        ctxs = [imls_icp.ImlsContext(p) for _ in sources]
+        try:
+            for c, s in zip(ctxs, sources):
+                c.set_target(rows(g["tgt"]))
+                c.set_target_tensors(rows(g["ten"]))
+                c.set_source(s)
+            batch = imls_icp.register_frames(ctxs)
+        finally:
+            for c in ctxs:
+                c.close()
+        return out, batch
+
+    ref, ref_b = run("0")
+    got, got_b = run(skin)
+    for a, b in zip(ref, got):
+        assert np.array_equal(a["pose"], b["pose"]) and (a["iters"], a["status"]) == (b["iters"], b["status"])
+        for ta, tb in zip(a["trace"], b["trace"]):
+            assert list(ta.delta) == list(tb.delta) and list(ta.reject) == list(tb.reject) and ta.n_valid == tb.n_valid
+    assert all(np.array_equal(x, y) for x, y in zip(ref_b[0], got_b[0]))
+    assert list(ref_b[1]) == list(got_b[1]) and list(ref_b[2]) == list(got_b[2])
