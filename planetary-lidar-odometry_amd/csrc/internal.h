@@ -67,9 +67,9 @@ struct KParams {
 };
 constexpr int kTvMaxK = 64;    // tensor-voting kNN size handled on device
 constexpr int kTvList = 64;    // TV skin list: ball(ρ + skin) members stored per query (more: not stored)
-// per-query TV state behind TreeView::tvn: voted normal (double4), skin reference (float4: x, count),
-// skin list (kTvList Morton positions)
-constexpr size_t kTvBytesPerQuery = 32 + 16 + 4 * kTvList;
+// per-query TV state behind TreeView::tvn, arrays of N: voted normal (double4), skin reference
+// (float4: x, count), skin list (kTvList Morton positions), summed tensor (9 doubles)
+constexpr size_t kTvBytesPerQuery = 32 + 16 + 4 * kTvList + 72;
 
 struct TreeView {
     const float4* mpt;        // map points in Morton order, w = original index (bits)

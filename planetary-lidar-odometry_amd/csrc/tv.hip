@@ -16,8 +16,9 @@
 // point per lane, ball members (fp32 screen with slack, exact fp64 libnabo metric, self match
 // excluded by d² > DBL_EPSILON) are appended to an LDS buffer by ballot; a full buffer is sorted
 // and cut to the best k (the k-th entry then bounds the search).  Finally the buffer is sorted by
-// (d², index), lane j < k computes voter j's S in fp64, lane 0 sums them in list order (the
-// reference's order) and runs the shared 3×3 Jacobi eigensolver.
+// (d², index), lane j < k computes voter j's S in fp64, lanes 0..8 sum one component each in list
+// order (the reference's order) through LDS, and k_tv_tangent runs the shared 3×3 Jacobi
+// eigensolver with one thread per query.  Skin lists (below) let later ICP iterations skip the walk.
 #include <algorithm>
 #include <cfloat>
 
@@ -60,6 +61,12 @@ __device__ void wave_bitonic(unsigned long long* k, unsigned* ix, unsigned* ps, 
         }
 }
 
+// the summed tensors (9 doubles per query) behind the voted normals, skin references and lists
+__device__ __forceinline__ double* tv_acc(double4* tvn, int N) {
+    return reinterpret_cast<double*>(reinterpret_cast<unsigned*>(reinterpret_cast<float4*>(tvn + N) + N) +
+                                     (size_t)N * kTvList);
+}
+
 // fp32 screen distance (the one definition every ball test uses)
 __device__ __forceinline__ float screen_d2(const float4& p4, const float* xf) {
     const float ex = p4.x - xf[0], ey = p4.y - xf[1], ez = p4.z - xf[2];
@@ -75,6 +82,7 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
     __shared__ unsigned cp[kTvWaves][kTvCap];             // Morton position
     __shared__ int snode[kTvWaves][kTvStack];
     __shared__ float sdist[kTvWaves][kTvStack];
+    __shared__ double sx[kTvWaves][64];                   // the vote sum's ninth component
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = __builtin_amdgcn_readfirstlane(bx * kTvWaves + wv);
@@ -110,6 +118,7 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
     const float skin = kp.tv_skin;
     float4* tref = reinterpret_cast<float4*>(tvn + N);
     unsigned* tlist = reinterpret_cast<unsigned*>(tref + N) + (size_t)q * kTvList;
+    double* tacc = tv_acc(tvn, N);
     bool reuse = false;
     int nst = 0;
     if (use_prev && skin > 0.f) {
@@ -306,22 +315,54 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
                 }
         }
     }
-    // the votes summed in list order (the reference's), read lane by lane (no LDS staging: the
-    // block's LDS then admits a fifth resident wave per SIMD)
-    double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int j = 0; j < kk; ++j)
+    // the votes summed in list order (the reference's): the wave's S staged in its (now free) LDS
+    // buffers, component-major, and lane e < 9 runs component e's chain of adds — 9 chains side by
+    // side instead of 9·k wave-wide adds of lane-broadcast values
+    wave_sync();   // every lane has read its wp entry
+    double* sk = reinterpret_cast<double*>(wk);
+    if (lane < kk) {
 #pragma unroll
-        for (int e = 0; e < 9; ++e) acc[e] += readlane_f64(S[e], j);
-    if (lane != 0) return;
+        for (int e = 0; e < 4; ++e) sk[e * 64 + lane] = S[e];
+#pragma unroll
+        for (int e = 4; e < 8; ++e) {
+            const unsigned long long b = (unsigned long long)__double_as_longlong(S[e]);
+            wi[(e - 4) * 64 + lane] = (unsigned)b;
+            wp[(e - 4) * 64 + lane] = (unsigned)(b >> 32);
+        }
+        sx[wv][lane] = S[8];
+    }
+    wave_sync();
+    if (lane >= 9) return;
+    const unsigned* lo;
+    const unsigned* hi;
+    int st;
+    if (lane < 4) { lo = reinterpret_cast<const unsigned*>(sk + lane * 64); hi = lo + 1; st = 2; }
+    else if (lane < 8) { lo = wi + (lane - 4) * 64; hi = wp + (lane - 4) * 64; st = 1; }
+    else { lo = reinterpret_cast<const unsigned*>(sx[wv]); hi = lo + 1; st = 2; }
+    double acc = 0.0;
+    for (int j = 0; j < kk; ++j)
+        acc += __longlong_as_double((long long)(((unsigned long long)hi[j * st] << 32) | lo[j * st]));
+    tacc[(size_t)q * 9 + lane] = acc;
+}
+
+// The summed tensor's tangent, one thread per query (the serial 3×3 Jacobi of 64 queries shares the
+// wave's instructions): Eigen isZero (|coeff| ≤ 1e-12) → no normal; else the eigenvector of the
+// smallest |λ| of the lower triangle, flipped to +z (imls_icp.cpp:245, 272-278).
+__device__ __forceinline__ void tv_tangent_body(int N, const int* __restrict__ done, double4* __restrict__ tvn, int q) {
+    if (q >= N || (done && *done)) return;
+    const double* acc = tv_acc(tvn, N) + (size_t)q * 9;
+    double a9[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) a9[e] = acc[e];
     bool zero = true;
 #pragma unroll
-    for (int e = 0; e < 9; ++e) zero = zero && fabs(acc[e]) <= 1e-12;
+    for (int e = 0; e < 9; ++e) zero = zero && fabs(a9[e]) <= 1e-12;
     if (zero) { tvn[q] = make_double4(0.0, 0.0, 0.0, 0.0); return; }
     double A[9], ev[3], U[9];
 #pragma unroll
     for (int a = 0; a < 3; ++a)
 #pragma unroll
-        for (int b = 0; b < 3; ++b) A[a * 3 + b] = a >= b ? acc[a * 3 + b] : acc[b * 3 + a];
+        for (int b = 0; b < 3; ++b) A[a * 3 + b] = a >= b ? a9[a * 3 + b] : a9[b * 3 + a];
     sym_eig<3>(A, ev, U);
     int mi = 0;
     if (fabs(ev[1]) < fabs(ev[mi])) mi = 1;
@@ -329,6 +370,16 @@ __device__ __forceinline__ void tv_vote_body(const TreeView& t, const float4* __
     double n0 = U[mi * 3], n1 = U[mi * 3 + 1], n2 = U[mi * 3 + 2];
     if (n2 < 0) { n0 = -n0; n1 = -n1; n2 = -n2; }
     tvn[q] = make_double4(n0, n1, n2, 1.0);
+}
+
+__global__ __launch_bounds__(256) void k_tv_tangent(int N, const int* __restrict__ done, double4* __restrict__ tvn) {
+    tv_tangent_body(N, done, tvn, (int)(blockIdx.x * blockDim.x + threadIdx.x));
+}
+
+__global__ __launch_bounds__(256) void k_tv_tangent_b(const PairDev* __restrict__ tab) {
+    const PairDev A = tab[blockIdx.y];
+    if (A.t.M <= 0) return;
+    tv_tangent_body(A.N, A.st.done, const_cast<double4*>(A.t.tvn), (int)(blockIdx.x * blockDim.x + threadIdx.x));
 }
 
 // Input tensors [6][n_in] (input order) → Morton order, 2 float4 per point.
@@ -360,6 +411,7 @@ void launch_tv_vote(hipStream_t s, const TreeView& t, const float4* spt, int N, 
                     const KParams& kp, double4* tvn, int use_prev) {
     if (N <= 0 || t.M <= 0) return;
     k_tv_vote<<<(N + kTvWaves - 1) / kTvWaves, kTvBlock, 0, s>>>(t, spt, N, pose, done, kp, tvn, use_prev);
+    k_tv_tangent<<<(N + 255) / 256, 256, 0, s>>>(N, done, tvn);
 }
 
 void launch_tv_vote_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp,
@@ -368,6 +420,7 @@ void launch_tv_vote_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     for (int k = 0; k < npairs; ++k) maxN = std::max(maxN, n_host[k]);
     if (maxN <= 0) return;
     k_tv_vote_b<<<dim3((maxN + kTvWaves - 1) / kTvWaves, npairs), kTvBlock, 0, s>>>(tab, kp, use_prev);
+    k_tv_tangent_b<<<dim3((maxN + 255) / 256, npairs), 256, 0, s>>>(tab);
 }
 
 void launch_tensor_gather(hipStream_t s, const float* ten6_in, size_t n_in, const unsigned* kept, const float4* mpt, int M,
