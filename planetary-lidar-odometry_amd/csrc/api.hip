@@ -185,6 +185,18 @@ KParams make_kparams(const imls_params& p) {
     k.reseed = 0.25f;
     k.sparse_lanes = 32;
     if (const char* w = std::getenv("IMLS_SPARSE")) k.sparse_lanes = std::atoi(w);
+    k.packet = 64;
+    // one frame alone on the GPU (imls_register_frame): its first ICP iteration, where every lane
+    // seeds, traverses in 32-query packets (the launch lasts as long as its slowest wave; measured
+    // on config B, one pair: k_knn_wave 240 -> 229 us per launch, 8.35 -> 8.14 ms per pair).
+    // Batched launches keep 64 (with 4 pairs in flight 32 measured 295 vs 305 pairs/s: the GPU is
+    // then throughput-bound and the idle half-waves cost more than the shorter tail saves).
+    k.pk_small = 32;
+    k.pk_iters = 1;
+    k.pk_batch = 0;
+    if (const char* w = std::getenv("IMLS_PACKET")) k.pk_small = std::atoi(w) == 16 ? 16 : std::atoi(w) == 32 ? 32 : 64;
+    if (const char* w = std::getenv("IMLS_PACKET_ITERS")) k.pk_iters = std::atoi(w);
+    if (const char* w = std::getenv("IMLS_PACKET_BATCH")) k.pk_batch = std::atoi(w);
     k.qwave = -1;   // auto
     if (const char* w = std::getenv("IMLS_QWAVE")) k.qwave = std::atoi(w);
     if (const char* w = std::getenv("IMLS_SEED_HALF")) k.seed_half = std::atoi(w);
@@ -1293,7 +1305,7 @@ int imls_register_frame_async(imls_ctx* c) {
         hipEvent_t marks[3];
         timed_begin(c, 0, slot);
         launch_project(c->stream, tv, (const float4*)c->spt.p, (const float4*)c->snr.p, (const unsigned*)c->qperm.p, c->N,
-                       c->st.pose, c->st.done, c->kp, (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p,
+                       c->st.pose, c->st.done, kp_at(c->kp, it), (float4*)c->cs.p, (float4*)c->cd.p, (float4*)c->cn.p,
                        c->st.partial1, tr + it, stats_ptr(c), fb_list(c), fb_count(c), c->lane_mode,
                        c->st.delta, (int*)c->prevnn.p, it > 0 && c->temporal_seed, project_marks(c, marks));
         timed_end(c, 0, slot);

@@ -53,6 +53,9 @@ struct KParams {
     float reseed;             // temporal seed unless displacement² > reseed · previous worst key
     int sparse_lanes;         // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
     int qwave;                // traversal: 0 = packets of 64 queries per wave, 1 = one wave per query
+    int packet;               // packet traversal: queries per wave in this launch (64, or 32 / 16: see pk_small)
+    int pk_small, pk_iters;   // the first pk_iters ICP iterations (mostly seeding lanes) use pk_small-query packets
+    int pk_batch;             // … in batched launches too (imls_register_frames; off: measured slower there)
     int wide;                 // packet traversal: binary levels descended per step (1..3)
     int verlet;               // reuse a query's list without traversal while its certification holds
     int qverlet;              // the same for the wave-per-query traversal (off by default: measured slower)
@@ -65,6 +68,12 @@ struct KParams {
     double tv_sigma, tv_thr;  // use_tensor_voting.sigma, .distance_threshold
     float tv_skin;            // TV ball lists reused while the query moved ≤ skin (m); 0 = every iteration walks the tree
 };
+// the parameters of ICP iteration `it`'s projection launch (packet size of the traversal)
+inline KParams kp_at(const KParams& k, int it) {
+    KParams r = k;
+    r.packet = it >= 0 && it < k.pk_iters ? k.pk_small : 64;
+    return r;
+}
 constexpr int kTvMaxK = 64;    // tensor-voting kNN size handled on device
 constexpr int kTvList = 64;    // TV skin list: ball(ρ + skin) members stored per query (more: not stored)
 // per-query TV state behind TreeView::tvn, arrays of N: voted normal (double4), skin reference

@@ -329,8 +329,12 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     __shared__ float4 sleaf[kWaveBlock / 64][64];   // the current leaf's points (lockstep insertion)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int slot = bx * kWaveBlock + tid;
-    const bool active = slot < N;
+    // a wave owns kp.packet Morton-consecutive queries (64; 32 or 16 in the first iterations, where
+    // most lanes seed: a smaller packet's union of neighbourhoods is smaller, and the launch lasts
+    // as long as its slowest wave); lanes past the packet idle
+    const int qp = kp.packet;
+    const int slot = (bx * (kWaveBlock / 64) + wv) * qp + lane;
+    const bool active = lane < qp && slot < N;
     float xf[3] = {0.f, 0.f, 0.f};
     if (active) {
         double ns[3];
@@ -1299,6 +1303,11 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(
 }
 
 __device__ __forceinline__ int wave_blocks_of(int N) { return (N + kWaveBlock - 1) / kWaveBlock; }
+// traversal blocks for packets of qp queries per wave
+__host__ __device__ __forceinline__ int knn_blocks_of(int N, int qp) {
+    const int per = qp * (kWaveBlock / 64);
+    return (N + per - 1) / per;
+}
 // traversal choice (launch_wave): one wave per query for sparse query sets, packets otherwise
 __host__ __device__ __forceinline__ bool use_qwave(const KParams& kp, int N) {
     return kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN);
@@ -1334,7 +1343,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const P
     batch_block(kp.xcd, f, bx);
     if (f >= npairs) return;
     const PairDev A = tab[f];
-    if (use_qwave(kp, A.N) || bx >= wave_blocks_of(A.N)) return;
+    if (use_qwave(kp, A.N) || bx >= knn_blocks_of(A.N, kp.packet)) return;
     float4* xref = xref_dev(A.lists, A.N);
     knn_wave_body<KL, LOCKSTEP>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
                                 wlist_of<KL>(A.lists, A.N), xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats,
@@ -1384,8 +1393,9 @@ void launch_wave_batch(hipStream_t s, const PairDev* tab, int npairs, int maxN, 
         k_knn_qwave_b<KL><<<dim3((n + kWaveBlock / 64 - 1) / (kWaveBlock / 64), gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
     }
     if (any_large) {
-        if (kp.lockstep) k_knn_wave_b<KL, true><<<dim3(wb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
-        else k_knn_wave_b<KL, false><<<dim3(wb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        const int kb = knn_blocks_of(maxN, kp.packet);
+        if (kp.lockstep) k_knn_wave_b<KL, true><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        else k_knn_wave_b<KL, false><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
     }
     k_finish_b<KL><<<dim3(wb, gy), kWaveBlock, 0, s>>>(tab, kp, it, npairs);
 }
@@ -1415,10 +1425,10 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
                                                                                           delta, lists, wlist, xref, nref, use_prev, stats,
                                                                                           fb_count);
     else if (kp.lockstep)
-        k_knn_wave<KL, true><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
+        k_knn_wave<KL, true><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
                                                           nref, use_prev, stats, fb_count);
     else
-        k_knn_wave<KL, false><<<blocks, kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
+        k_knn_wave<KL, false><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
                                                            nref, use_prev, stats, fb_count);
     if (marks) (void)hipEventRecord(marks[1], s);
     k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,
@@ -1433,7 +1443,7 @@ void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     // auto traversal choice for a batch: the wave-per-query kernel wins on one small frame (latency:
     // few waves), packets win once the batch's queries fill the GPU (measured on the config-C-like
     // stream, 32 frames of ~1900 queries per launch: 546 → 320 µs).  Either gives the exact answer.
-    KParams kp = kp0;
+    KParams kp = kp_at(kp0, kp0.pk_batch ? it : -1);
     long long total = 0;
     for (int k = 0; k < npairs; ++k) total += n_host[k];
     if (kp.qwave < 0 && total > kQwaveAutoN) kp.qwave = 0;
