@@ -28,4 +28,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
   step pmc_$c 300 rocprofv3 --kernel-trace --kernel-include-regex 'k_knn_wave|k_finish' --output-format csv \
       --pmc $c -d $O/pmc_$c -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --inflight 1 --no-fuse --latency-pairs 3
 done
+# the driver's N>1 launch shape at N=1 (torch.distributed.run, RCCL init, max-over-ranks timing)
+step dist1 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu
 echo done
