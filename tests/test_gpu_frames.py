@@ -293,3 +293,22 @@ class _DevSoa:
     def free(self):
         import ctypes
         self.hip.hipFree(ctypes.c_void_p(self.ptr))
+
+
+@pytest.mark.parametrize("packet,iters", [(16, 20), (32, 3)])
+def test_traversal_packet_sizes_in_batches(hdl_pair, monkeypatch, packet, iters):
+    """The traversal packet size (queries per wave, IMLS_PACKET / IMLS_PACKET_ITERS; batched
+    launches too with IMLS_PACKET_BATCH) only changes which waves walk which queries: the lists it
+    hands k_finish are certified there, so every frame's pose, iterations and trace stay bit-equal
+    to the default single-frame path (32-query packets in iteration 0 only)."""
+    frames = [(hdl_pair.source, hdl_pair.target),
+              (synth.fps_subsample(hdl_pair.source, 40000, seed=11), hdl_pair.target)]
+    ref = _single(_params(6), frames)
+    monkeypatch.setenv("IMLS_PACKET", str(packet))
+    monkeypatch.setenv("IMLS_PACKET_ITERS", str(iters))
+    monkeypatch.setenv("IMLS_PACKET_BATCH", "1")
+    poses, its, status, traces = _batched(_params(6), frames)
+    for k, r in enumerate(ref):
+        assert np.array_equal(r["pose"], poses[k]), (k, np.abs(r["pose"] - poses[k]).max())
+        assert (r["iters"], r["status"]) == (its[k], status[k]), k
+        assert all(_trace_equal(a, b) for a, b in zip(r["trace"], traces[k])), k
