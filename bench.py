@@ -106,15 +106,18 @@ def timed_steps(step, steps: int, world: int, dev, sync=None):
     return elapsed, per, out
 
 
-def exchange_poses(local_poses, world: int):
-    """The one collective: all-gather of every rank's relative poses (unit order = rank-major blocks,
-    sequences.shard_range) and the chained trajectory nowPose_k = prevLaserPose·rPose_k."""
-    local_poses = np.asarray(local_poses, dtype=np.float64).reshape(-1, 4, 4)
-    if world == 1:
-        allp = local_poses
-    else:
-        allp = sequences.gather_relative_poses(local_poses, world * len(local_poses))
-    return allp, sequences.chain_trajectory(allp)
+def exchange_poses(results, world: int, rank: int = 0):
+    """The one collective: all-gather of every rank's (sequence, frame order, relative pose) records
+    and each sequence's trajectory nowPose_k = prevLaserPose·rPose_k chained on its own
+    (laser_odometry.cpp:652-655; config D: 8 independent sequences, never one trajectory).
+    results: [(seq, order, pose 4×4)], seq ids local to the rank (made global as rank·2^20 + seq).
+    Returns (records (seq, order, pose) of every rank, {seq: (orders, trajectory)})."""
+    seq = np.array([rank * (1 << 20) + int(r[0]) for r in results], dtype=np.int64)
+    order = np.array([int(r[1]) for r in results], dtype=np.int64)
+    poses = np.asarray([r[2] for r in results], dtype=np.float64).reshape(-1, 4, 4)
+    if world > 1:
+        seq, order, poses = sequences.gather_tagged_poses(seq, order, poses)
+    return (seq, order, poses), sequences.chain_per_sequence(seq, order, poses)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -147,53 +150,83 @@ class _Pinned:
         os.sched_setaffinity(0, self.prev)
 
 
-def cpu_baseline(src, tgt, p, label: str, min_seconds: float = 10.0, max_pairs: int = 4, faithful_iters: int = 2,
-                 tensors=None):
-    """The oracle on the same pair (same parameters): (1) "efficient" port, 1 thread pinned: whole
-    registrations repeated to >= min_seconds (<= max_pairs); (2) "faithful": the reference's
-    container costs (erase per rejection, AoS copies, per-query heap vectors), 1 thread pinned, on
-    the first `faithful_iters` ICP iterations, extrapolated per pair; (3) all cores: the per-query
-    loop on every CPU this process may use (OpenMP)."""
+def cpu_baseline(src, tgt, p, label: str, min_seconds: float = 10.0, max_pairs: int = 4, tensors=None,
+                 faithful: bool = True):
+    """The oracle on the same pair (same parameters).  Returns (baseline dict, the oracle's first
+    result — the parity reference of that pair).
+      (1) "efficient" port, 1 thread pinned: whole registrations repeated to >= min_seconds;
+      (2) "faithful": the reference's container costs (erase per rejection, AoS copies, per-query heap
+          vectors), 1 thread pinned, one whole registration (every ICP iteration);
+      (3) "host_share": the per-query loop OpenMP over this process's CPU share (OMP_NUM_THREADS on
+          the GPU box: 16 of its 256 CPUs per GPU — the box's rule for worker pools), plus the
+          perfect-scaling bound of the 1-thread figure over every CPU the process may run on (an
+          upper bound for the whole socket pair: the index build and solver are sequential)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle_ctypes as oc
     info = host_info()
     iters = p.iterations
+    first = None
     with _Pinned() as pin:
         total, n, t_idx = 0.0, 0, 0.0
         while n < max_pairs and (n == 0 or total < min_seconds):
             r = oc.register_frame(src, tgt, p, tensors=tensors)
+            first = first or r
             total += r["seconds_total"]
             t_idx += r["seconds_index"]
             n += 1
-        pf = _abi.ImlsParams.from_buffer_copy(p)
-        pf.iterations = min(faithful_iters, iters)
-        oc.set_faithful(True)
-        try:
-            rf = oc.register_frame(src, tgt, pf, tensors=tensors)
-        finally:
-            oc.set_faithful(False)
-    t_iter_f = (rf["seconds_total"] - rf["seconds_index"]) / max(rf["iters"], 1)
-    faithful_pair = rf["seconds_index"] + iters * t_iter_f
+        rf = None
+        if faithful:
+            oc.set_faithful(True)
+            try:
+                rf = oc.register_frame(src, tgt, p, tensors=tensors)
+            finally:
+                oc.set_faithful(False)
     threads = max(1, min(info["affinity_cpus"], int(os.environ.get("OMP_NUM_THREADS") or 10 ** 6)))
     oc.set_threads(threads)
     try:
         r2 = oc.register_frame(src, tgt, p, tensors=tensors)
     finally:
         oc.set_threads(1)
-    return dict(
-        value=n / total, unit="scan-pairs/s", cores=1, kind="port",
+    one = n / total
+    out = dict(
+        value=one, unit="scan-pairs/s", cores=1, kind="port",
         sample=f"{n} whole registration(s) of the {label} pair ({src.shape[1]} queries vs {tgt.shape[1]}-pt map, "
                f"{r['iters']} ICP iterations each) in {total:.1f} s, index build {t_idx / n:.2f} s/pair; "
                f"oracle/imls_oracle.cpp -O3 (efficient port: stable compaction), 1 thread pinned to CPU {pin.cpu}",
         seconds_per_pair=total / n,
-        faithful={"value": 1.0 / faithful_pair, "cores": 1, "seconds_per_pair": faithful_pair,
-                  "sample": f"index build + {rf['iters']} of {iters} ICP iterations with the reference's container "
-                            f"costs (erase per rejected point, AoS copy per iteration, per-query heap vectors), "
-                            f"{rf['seconds_total']:.1f} s, extrapolated to {iters} iterations"},
-        all_cores={"value": 1.0 / r2["seconds_total"], "cores": threads,
-                   "sample": f"1 whole registration, per-query projection loop OpenMP over {threads} threads "
-                             f"(index build and solver sequential)"},
+        host_share={"value": 1.0 / r2["seconds_total"], "cores": threads,
+                    "sample": f"1 whole registration, per-query projection loop OpenMP over {threads} threads "
+                              f"(this process's CPU share; index build and solver sequential)"},
+        all_cpus_linear_bound={"value": one * info["affinity_cpus"], "cores": info["affinity_cpus"],
+                               "sample": "1-thread value x every CPU in sched_getaffinity (perfect scaling: an "
+                                         "upper bound, not a measurement)"},
         host=info)
+    if rf is not None:
+        out["faithful"] = {"value": 1.0 / rf["seconds_total"], "cores": 1, "seconds_per_pair": rf["seconds_total"],
+                           "sample": f"1 whole registration (index build + all {rf['iters']} ICP iterations) with the "
+                                     f"reference's container costs (erase per rejected point, AoS copy per iteration, "
+                                     f"per-query heap vectors), {rf['seconds_total']:.1f} s"}
+    return out, first
+
+
+def parity_vs_oracle(got: dict, want: dict, truth=None) -> dict:
+    """The GPU's single-frame result of a pair against the oracle's (DESIGN §3 contract: iterations,
+    status, per-iteration valid counts and reject counters exact; pose within 1e-6 (1e-5 through
+    DRPM's device erfc)).  truth: the synthetic relative pose — both results' translation error
+    against it shows whether a large error is the algorithm's (shared) or the kernels'."""
+    tg, tw = got["trace"], want["trace"]
+    d = {
+        "max_pose_diff_vs_oracle": float(np.abs(np.asarray(got["pose"]) - np.asarray(want["pose"])).max()),
+        "iters_equal": int(got["iters"]) == int(want["iters"]),
+        "status_equal": int(got["status"]) == int(want["status"]),
+        "n_valid_equal": len(tg) == len(tw) and all(a.n_valid == b.n_valid for a, b in zip(tg, tw)),
+        "rejects_equal": len(tg) == len(tw) and all(list(a.reject) == list(b.reject) for a, b in zip(tg, tw)),
+        "iters": int(got["iters"]),
+    }
+    if truth is not None:
+        d["gpu_truth_err_cm"] = float(np.linalg.norm(np.asarray(got["pose"])[:3, 3] - truth[:3, 3]) * 100)
+        d["oracle_truth_err_cm"] = float(np.linalg.norm(np.asarray(want["pose"])[:3, 3] - truth[:3, 3]) * 100)
+    return d
 
 
 # ------------------------------------------------------------------------------------------------
@@ -204,11 +237,13 @@ def soa_tensor(cloud, dev):
     return torch.from_numpy(np.ascontiguousarray(synth.soa(cloud))).to(dev).contiguous()
 
 
-def algorithmic_bytes_per_launch(stats: dict, trace, iters: int) -> float:
-    """B_q = 24 (query xyz+n) + 24·[NN found] + 24·k_q + 40·[valid], summed over
-    the queries of one projection launch (k_q from the kernel's own counts)."""
-    n_valid = float(np.mean([t.n_valid for t in trace])) if trace else 0.0
-    return 24.0 * stats["queries"] + 24.0 * stats["nn_found"] / iters + 24.0 * stats["sum_kq"] / iters + 40.0 * n_valid
+def frame_bytes(stats: dict, n_queries: int, trace) -> float:
+    """SURVEY §8(d) algorithmic bytes of one frame's projections, summed over the iterations it ran:
+    Σ_it Σ_q [24 (query xyz+n) + 24·[NN found] + 24·k_q + 40·[valid]] (k_q and NN-found from the
+    kernels' own counters, accumulated over the frame)."""
+    its = len(trace)
+    return (24.0 * n_queries * its + 24.0 * stats["nn_found"] + 24.0 * stats["sum_kq"]
+            + 40.0 * float(sum(t.n_valid for t in trace)))
 
 
 def solver_params(solver: str, iters: int) -> _abi.ImlsParams:
@@ -222,13 +257,13 @@ def solver_params(solver: str, iters: int) -> _abi.ImlsParams:
 
 class Pipeline:
     """Fused steps: the contexts are split into `groups` parts, each registered as ONE launch
-    sequence (register_frames_async).  A part is re-loaded (deferred uploads and NaN filters: no
-    host wait, enqueued behind its running batch), collected and launched again while the other
-    parts' batches still run, so batches
-    overlap on the GPU (one fills another's tail) and the host work hides behind them (groups = 1:
-    one batch per step, collected at the next step).  A step registers every context once and
-    returns the results collected during it; the batches launched last stay in flight into the
-    next step (the timed region's device-wide synchronize on both sides covers them)."""
+    sequence (register_frames_async).  A part is re-loaded (count-less uploads: no host wait,
+    enqueued behind its running batch), collected and launched again while the other parts' batches
+    still run, so batches overlap on the GPU (one fills another's tail) and the host work hides
+    behind them (groups = 1: one batch per step, collected at the next step).  A step registers
+    every context once and returns the results collected during it, tagged with the context index:
+    (k, pose, iterations, status, trace); the batches launched last stay in flight into the next
+    step (the timed region's device-wide synchronize on both sides covers them)."""
 
     def __init__(self, ctxs, prep, groups=2):
         g = max(1, min(groups, len(ctxs)))
@@ -244,9 +279,9 @@ class Pipeline:
             return []
         self.inflight[h] = False
         t0 = time.perf_counter()
-        poses, iters, st, _ = imls_icp.register_frames_result(self.halves[h])
+        poses, iters, st, tr = imls_icp.register_frames_result(self.halves[h])
         self.t_wait += time.perf_counter() - t0
-        return list(zip(poses, iters, st))
+        return [(self.offs[h] + j, poses[j], int(iters[j]), int(st[j]), tr[j]) for j in range(len(poses))]
 
     def step(self):
         out = []
@@ -270,13 +305,16 @@ class Pipeline:
 
 
 class PairRunner:
-    """Configs A / B: independent pairs, inputs resident in HBM, one context per pair.  fuse: the
-    step's pairs are registered as ONE launch sequence (imls_register_frames); else one launch
-    sequence per pair, each on its context's stream."""
+    """Configs A / B / E: independent pairs, inputs resident in HBM, one context per pair.  fuse:
+    the step's pairs are registered as `groups` launch sequences in flight (Pipeline); else one
+    launch sequence per pair, each on its context's stream.  RANSAC: every registration starts its
+    context's rand() stream from params.ransac_seed (each pair is an independent registration, the
+    reference's first frame), so a result depends on its pair alone."""
 
     def __init__(self, pairs, p, dev, local, fuse=True, groups=2, tensors=False):
         self.fuse = fuse
         self.pairs = pairs
+        self.ransac = p.solve_method == _abi.IMLS_SOLVE_RANSAC
         self.s_dev = [soa_tensor(q.source, dev) for q in pairs]
         self.t_dev = [soa_tensor(q.target, dev) for q in pairs]
         # config E: the targets' tensor-voting input tensors, SoA (6, M) in HBM
@@ -285,38 +323,50 @@ class PairRunner:
             import torch
             self.ten_dev = [torch.from_numpy(np.ascontiguousarray(q.meta["tensors"].T)).to(dev).contiguous() for q in pairs]
         self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in pairs]
+        self.seed_state = self.ctxs[0].rng_state()        # a fresh context's stream (params.ransac_seed)
+        # deferred reads of the count-less device loads: a large batch filters all its members in
+        # three launches (the inputs stay resident and unchanged for the whole run)
+        per_group = len(pairs) / max(1, groups)
+        for c in self.ctxs:
+            c.set_defer(fuse and per_group >= 8)
         self.pipe = Pipeline(self.ctxs, self._prep, groups) if fuse else None
+
+    def _load(self, c, k, count):
+        q = self.pairs[k]
+        if self.ransac:
+            c.set_rng_state(self.seed_state)
+        c.set_target_device(self.t_dev[k].data_ptr(), q.target.size, count=count)
+        if self.ten_dev:
+            c.set_target_tensors_device(self.ten_dev[k].data_ptr(), q.target.size)
+        c.set_source_device(self.s_dev[k].data_ptr(), q.source.size, count=count)
 
     def _prep(self, idx):
         for k in idx:
-            q, c = self.pairs[k], self.ctxs[k]
-            c.set_target_device(self.t_dev[k].data_ptr(), q.target.size, count=False)
-            if self.ten_dev:
-                c.set_target_tensors_device(self.ten_dev[k].data_ptr(), q.target.size)
-            c.set_source_device(self.s_dev[k].data_ptr(), q.source.size, count=False)
+            self._load(self.ctxs[k], k, False)
 
-    def step(self, ctxs=None, idx=None, fuse=None):
-        fuse = self.fuse if fuse is None else fuse
-        if fuse and ctxs is None:
+    def step(self):
+        if self.fuse:
             return self.pipe.step()
-        ctxs = ctxs or self.ctxs
-        idx = idx if idx is not None else range(len(self.pairs))
-        for c, k in zip(ctxs, idx):
-            q = self.pairs[k]
-            c.set_target_device(self.t_dev[k].data_ptr(), q.target.size)
-            if self.ten_dev:
-                c.set_target_tensors_device(self.ten_dev[k].data_ptr(), q.target.size)
-            c.set_source_device(self.s_dev[k].data_ptr(), q.source.size)
-            if not fuse:
-                c.register_frame_async()
-        if fuse:
-            poses, iters, st, _ = imls_icp.register_frames(ctxs)
-            return list(zip(poses, iters, st))
-        return [c.register_frame_result() for c in ctxs]
+        return self.single()
+
+    def single(self, idx=None):
+        """Each pair (or pairs idx) registered alone, one launch sequence per pair on its own
+        context's stream (imls_register_frame: the single-frame kernels), tagged like Pipeline."""
+        idx = list(range(len(self.pairs)) if idx is None else idx)
+        for k in idx:
+            self._load(self.ctxs[k], k, True)
+            self.ctxs[k].register_frame_async()
+        out = []
+        for k in idx:
+            pose, it, st = self.ctxs[k].register_frame_result()
+            out.append((k, pose, it, st, self.ctxs[k].last_trace))
+        return out
+
+    def drain(self):
+        return self.pipe.drain() if self.pipe else []
 
     def close(self):
-        if self.pipe:
-            self.pipe.drain()
+        self.drain()
         for c in self.ctxs:
             c.close()
 
@@ -324,12 +374,15 @@ class PairRunner:
 class StreamRunner:
     """Config C/D-like: `n_seq` independent sequences (one context each); each step processes one
     frame per sequence exactly as LaserOdometry.process does (map_push of the previous filtered
-    scan, set_source of the flat cloud, register), host buffers in.  A sequence ping-pongs over its
-    F produced frames (0 … F−1 … 0 …) so every step registers two adjacent frames."""
+    scan, set_source of the flat cloud, register).  A sequence ping-pongs over its F produced frames
+    (0 … F−1 … 0 …) so every step registers two adjacent frames.  Results are tagged with the
+    context index; self.last[q] = (map frame, source frame) of the frame most recently loaded."""
 
     def __init__(self, n_seq, p, local, rank, frames_per_seq=5, fuse=True, unique=8, dev=None, resident=True, groups=2):
         from planetary_lidar_odometry_amd import producer
         self.fuse = fuse
+        self.p = p
+        self.local = local
         sm = synth.hdl64()
         self.seqs = []
         with imls_icp.ImlsContext(device=local) as pctx:
@@ -346,6 +399,7 @@ class StreamRunner:
         # sequences beyond `unique` replay the produced ones (each still its own context and map
         # FIFO, at its own phase): producing every HDL-64 sweep on the host would dominate set-up
         u = len(self.seqs)
+        self.unique_seqs = u
         # resident: every produced cloud already in HBM as SoA6 (the timed region starts with the
         # inputs resident, like config B; a step pushes / loads them device-to-device); else host
         # buffers cross PCIe inside the timed region (the reference's host-side hand-over)
@@ -355,23 +409,30 @@ class StreamRunner:
         self.seqs = [self.seqs[q % u] for q in range(n_seq)]
         self.dseq = [q % u for q in range(n_seq)]
         self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in range(n_seq)]
+        for c in self.ctxs:
+            c.set_defer(fuse and n_seq / max(1, groups) >= 8)
+        self.seed_state = self.ctxs[0].rng_state()
+        self.ransac = p.solve_method == _abi.IMLS_SOLVE_RANSAC
         self.pos = [(q // u) % frames_per_seq for q in range(n_seq)]
         self.dir = [1] * n_seq
         # frame 0 only seeds the map (Q13); afterwards each registered frame's filtered scan joins
         # the FIFO at the start of that sequence's next step, as LaserOdometry.process orders it
         self.pending = [fr[self.pos[q]][0] for q, fr in enumerate(self.seqs)]
         self.pending_k = list(self.pos)
+        self.last = [None] * n_seq
         self.t_prep = self.t_reg = 0.0        # host time in the per-frame uploads / in registration
         self.pipe = Pipeline(self.ctxs, self._prep, groups) if fuse else None
 
     def _prep(self, idx):
         """One frame of each sequence in idx, as LaserOdometry.process orders it: the previous
         filtered scan joins the device map FIFO (only it crosses PCIe), the flat cloud is loaded;
-        deferred (no host wait for the NaN-filtered counts)."""
+        count-less (no host wait for the NaN-filtered counts)."""
         t0 = time.perf_counter()
         for q in idx:
             c = self.ctxs[q]
             k = self._advance(q)
+            if self.ransac:
+                c.set_rng_state(self.seed_state)
             if self.resident:
                 filt, _ = self.dev_frames[self.dseq[q]][self.pending_k[q]]
                 _, flat = self.dev_frames[self.dseq[q]][k]
@@ -380,6 +441,7 @@ class StreamRunner:
             else:
                 c.map_push(self.pending[q], count=False)
                 c.set_source(self.seqs[q][k][1], count=False)
+            self.last[q] = (self.pending_k[q], k)
             self.pending[q] = self.seqs[q][k][0]
             self.pending_k[q] = k
             self.pos[q] = k
@@ -404,9 +466,22 @@ class StreamRunner:
         t1 = time.perf_counter()
         for c in self.ctxs:
             c.register_frame_async()
-        out = [c.register_frame_result() for c in self.ctxs]
+        out = []
+        for q, c in enumerate(self.ctxs):
+            pose, it, st = c.register_frame_result()
+            out.append((q, pose, it, st, c.last_trace))
         self.t_reg += time.perf_counter() - t1
         return out
+
+    def single(self, q, frames):
+        """Frame (map frame m, source frame k) of sequence q registered alone on a fresh context
+        (set_target of the map scan — max_queue_size 1 — + set_source + register_frame)."""
+        m, k = frames
+        fr = self.seqs[q]
+        with imls_icp.ImlsContext(self.p, device=self.local) as c:
+            c.set_target(fr[m][0])
+            c.set_source(fr[k][1])
+            return c.register_frame()
 
     @property
     def queries(self):
@@ -416,9 +491,11 @@ class StreamRunner:
     def map_points(self):
         return int(np.mean([len(f[0]) for s in self.seqs for f in s]))
 
+    def drain(self):
+        return self.pipe.drain() if self.pipe else []
+
     def close(self):
-        if self.pipe:
-            self.pipe.drain()
+        self.drain()
         for c in self.ctxs:
             c.close()
 
@@ -433,11 +510,6 @@ def latency_probe(run_one, ctx, n_pairs: int, iters: int):
         run_one()
         lat.append(time.perf_counter() - t)
     ctx.enable_timing(False)
-    # one more pair with the traversal / neighbour counters on (Σk_q, NN found: the algorithmic
-    # bytes) — counted apart from the timed pairs, whose kernels then carry no counter atomics
-    ctx.enable_stats(True)
-    run_one()
-    ctx.enable_stats(False)
     k = {name: ctx.kernel_timing(i) for i, name in enumerate(("projection", "index", "solve", "k_knn_wave", "k_finish"))}
     lat = np.array(lat) * 1e3
     idx_ms = k["index"][0] / max(k["index"][1], 1)
@@ -445,6 +517,73 @@ def latency_probe(run_one, ctx, n_pairs: int, iters: int):
                 ms_per_iteration=float((np.median(lat) - idx_ms) / iters),
                 kernel_avg_ms={n: v[0] / max(v[1], 1) for n, v in k.items()},
                 launches={n: int(v[1]) for n, v in k.items()})
+
+
+def same_result(a, b) -> bool:
+    """Bit equality of two tagged results (pose, iterations, status, every trace record)."""
+    if not (np.array_equal(np.asarray(a[1]), np.asarray(b[1])) and a[2] == b[2] and a[3] == b[3]):
+        return False
+    ta, tb = a[4], b[4]
+    return len(ta) == len(tb) and all(
+        list(x.delta) == list(y.delta) and list(x.pose) == list(y.pose) and list(x.reject) == list(y.reject)
+        and x.n_valid == y.n_valid and x.n_kept == y.n_kept for x, y in zip(ta, tb))
+
+
+def union_ms(iv) -> float:
+    """Length of the union of [start, end) intervals (ms)."""
+    if len(iv) == 0:
+        return 0.0
+    iv = sorted(map(tuple, iv))
+    busy, cs, ce = 0.0, iv[0][0], iv[0][1]
+    for s, e in iv[1:]:
+        if s > ce:
+            busy += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    return busy + ce - cs
+
+
+def busy_pass(runner, steps: int, sync):
+    """A second timed pass with light HIP-event timing (projection and solve launches only, every
+    launch sequence's own stream; imls_enable_timing 2) on one device-wide clock: returns its wall
+    time and the union of the projection / solve intervals — the time the GPU spent with at least
+    one projection (or solve) kernel running, the denominator of roofline.frac."""
+    ctxs = runner.ctxs
+    runner.drain()
+    sync()
+    for c in ctxs:
+        c.reset_timing()
+        c.enable_timing(2)
+    ctxs[0].timing_origin()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        runner.step()
+    runner.drain()
+    sync()
+    wall = time.perf_counter() - t0
+    proj = np.concatenate([c.timing_intervals(0) for c in ctxs] + [np.zeros((0, 2))])
+    solve = np.concatenate([c.timing_intervals(2) for c in ctxs] + [np.zeros((0, 2))])
+    for c in ctxs:
+        c.enable_timing(0)
+    return dict(wall_ms=wall * 1e3, projection_busy_ms=union_ms(proj), solve_busy_ms=union_ms(solve),
+                any_busy_ms=union_ms(np.concatenate([proj, solve])), projection_launches=int(len(proj)))
+
+
+def stats_pass(runner):
+    """One step with the neighbour counters on for every context (then off): each frame's
+    algorithmic bytes (frame_bytes).  Returns {context: bytes}."""
+    runner.drain()
+    for c in runner.ctxs:
+        c.enable_stats(True)
+    res = runner.step() + runner.drain()
+    out = {}
+    for k, pose, it, st, tr in res:
+        c = runner.ctxs[k]
+        out[k] = frame_bytes(c.index_stats(), c.index_stats()["queries"], tr)
+    for c in runner.ctxs:
+        c.enable_stats(False)
+    return out
 
 
 def main():
@@ -465,7 +604,9 @@ def main():
     ap.add_argument("--host-inputs", action="store_true",
                     help="stream: frames handed over in host memory (PCIe inside the timed region)")
     ap.add_argument("--latency-pairs", type=int, default=50, help="single-pair latency / roofline probe size")
+    ap.add_argument("--busy-steps", type=int, default=5, help="steps of the HIP-event busy-time pass (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
+    ap.add_argument("--no-verify", action="store_true", help="skip the bit-equality check of the timed results")
     ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     ap.add_argument("--workload", choices=["B", "stream", "A", "E"], default="B")
@@ -475,14 +616,11 @@ def main():
     import torch
     import torch.distributed as dist
     world, rank, local, dev = dist_setup(args.backend)
-    # config B: each pair already fills the GPU; 4 in flight as 4 one-pair launch sequences measured
-    # best (pairs per sequence × sequences: 1×4 264.7, 2×2 252.4, 2×4 255.7, 3×2 237.2, 4×2 231,
-    # 8×2 205 pairs/s: more per launch only adds cache pressure).  The ~1900-query stream frames
-    # need many per launch: 64 per sequence × 2 → 2819 frames/s (32 × 4: 1841)
     # measured (profiles/r02_final): B pairs fill the GPU alone and run best as 4 one-pair launch
-    # sequences in flight; the small A / stream frames run best as ONE large batch per step (two
-    # half batches in flight share hardware queues, so a filter of one half can wait behind the
-    # other half's launch sequence)
+    # sequences in flight (1x4 264.7, 2x2 252.4, 2x4 255.7, 4x2 231, 8x2 205 pairs/s: more per launch
+    # only adds cache pressure); the small A / stream frames run best as ONE large batch per step
+    # (two half batches in flight share hardware queues, so a filter of one half can wait behind
+    # the other half's launch sequence)
     P = args.inflight if args.inflight > 0 else {"B": 4, "A": 256, "stream": 1024, "E": 256}[args.workload]
     if args.groups <= 0:
         args.groups = {"B": 4, "A": 1, "stream": 1, "E": 1}[args.workload]
@@ -494,12 +632,11 @@ def main():
         p.get_normals, p.recompute_normal_count_mode = 0, 1
         p.use_tensor_voting, p.tensor_k, p.tensor_sigma, p.tensor_distance_threshold = 1, 50, 0.2, 0.6
     t0 = time.time()
-    if args.workload == "stream":
+    stream = args.workload == "stream"
+    if stream:
         runner = StreamRunner(P, p, local, rank, fuse=fuse, unique=args.unique_seqs, dev=dev,
                               resident=not args.host_inputs, groups=args.groups)
-        probe_ctx = runner.ctxs[0]
         queries, map_points = runner.queries, runner.map_points
-        single = None
     else:
         if args.workload == "E":
             # sparse VLP-16 scans over the planetary heightfield (synth.make_planetary_pair: ~10 s of
@@ -514,46 +651,92 @@ def main():
             pairs = [synth.Pair(synth.fps_subsample(q.source, args.queries, seed=rank), q.target, q.true_pose, q.meta)
                      for q in pairs]
         runner = PairRunner(pairs, p, dev, local, fuse=fuse, groups=args.groups, tensors=args.workload == "E")
-        probe_ctx = runner.ctxs[0]
         queries, map_points = pairs[0].source.size, pairs[0].target.size
-        # the probe runs the one-frame launch sequence: its events separate k_knn_wave and k_finish
-        single = lambda: runner.step([probe_ctx], [0], fuse=False)   # noqa: E731
+    probe_ctx = runner.ctxs[0]
     log(f"[rank {rank}] workload {args.workload} set up in {time.time() - t0:.1f}s: {P} in flight, "
         f"~{queries} queries vs ~{map_points}-pt maps, solver {args.solver}")
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        res = runner.step()
-    if args.workload != "stream":
-        if runner.pipe:                  # pipelined results arrive out of pair order: check one plain pass
-            runner.pipe.drain()
-            res = runner.step(runner.ctxs, range(P), fuse=False)
-        errs = [np.linalg.norm(r[0][:3, 3] - q.true_pose[:3, 3]) for r, q in zip(res, runner.pairs)]
-        log(f"[rank {rank}] warmup done; max pose error vs truth {max(errs) * 100:.2f} cm")
+        runner.step()
+    runner.drain()
 
     if hasattr(runner, "t_prep"):
         runner.t_prep = runner.t_reg = 0.0
     if getattr(runner, "pipe", None):
         runner.pipe.t_wait = runner.pipe.t_launch = 0.0
+    # the stream's frame of each result: the (map, source) frames loaded when its batch was prepared
+    frames_at_launch = {}
+    if stream:
+        orig_prep = runner._prep
+
+        def tagging_prep(idx):
+            orig_prep(idx)
+            for q in idx:
+                frames_at_launch.setdefault(q, []).append(runner.last[q])
+        runner._prep = tagging_prep
+        if runner.pipe:
+            runner.pipe.prep = tagging_prep
     elapsed, per_step, res = timed_steps(runner.step, args.steps, world, dev, torch.cuda.synchronize)
-    if getattr(runner, "pipe", None):
-        res += runner.pipe.drain()        # the batches still in flight (already finished: synchronized)
+    res += runner.drain()                 # the batches still in flight (already finished: synchronized)
+    if stream:
+        runner._prep = orig_prep
+        if runner.pipe:
+            runner.pipe.prep = orig_prep
     if hasattr(runner, "t_prep"):
         log(f"[rank {rank}] host time per step: uploads (+ filters) {runner.t_prep / args.steps * 1e3:.2f} ms, "
             f"rest (builds, launches, waits) {runner.t_reg / args.steps * 1e3:.2f} ms")
     if getattr(runner, "pipe", None):
         log(f"[rank {rank}] pipeline host time per step: result waits {runner.pipe.t_wait / args.steps * 1e3:.2f} ms, "
             f"register_frames_async (builds + launches) {runner.pipe.t_launch / args.steps * 1e3:.2f} ms")
-    poses = [r[0] for r in res]
-    allp, traj = exchange_poses(poses, world)          # the one RCCL exchange (trajectory chaining)
     n_pairs = args.steps * P
     value = world * n_pairs / elapsed
 
-    # single-pair latency + serialised per-launch kernel durations (roofline), outside the timed region
-    probe = latency_probe(single, probe_ctx, args.latency_pairs, args.iters) if single else None
-    stats = probe_ctx.index_stats()
+    # ---- outside the timed region -------------------------------------------------------------
+    # (1) every timed result bit-equal to its pair registered alone (single-frame kernels)
+    verify = None
+    if stream:
+        # each context's results in launch order ↔ the frames loaded for those launches (the warm-up
+        # launches were drained before the timed region: the first result per context is the first
+        # timed launch); a sample of sequences is re-registered alone on fresh contexts
+        seen = {}
+        checked = mism = 0
+        for k, pose, it, st, tr in res:
+            j = seen.get(k, 0)
+            seen[k] = j + 1
+            if not args.no_verify and k < 8 and j < 2:
+                ref = runner.single(k, frames_at_launch[k][j])
+                ok = same_result((k, pose, it, st, tr), (k, ref["pose"], ref["iters"], ref["status"], ref["trace"]))
+                checked += 1
+                mism += 0 if ok else 1
+        verify = dict(timed_results=len(res), checked=checked, mismatches=mism,
+                      rule="sequences 0-7, first two timed frames each, vs a fresh context registering that frame alone")
+    else:
+        ref = {r[0]: r for r in runner.single()}
+        mism = 0 if args.no_verify else sum(0 if same_result(r, ref[r[0]]) else 1 for r in res)
+        verify = dict(timed_results=len(res), checked=0 if args.no_verify else len(res), mismatches=mism,
+                      rule="every timed result vs its pair registered alone (single-frame kernels), bit for bit")
+        errs = [np.linalg.norm(ref[k][1][:3, 3] - q.true_pose[:3, 3]) for k, q in enumerate(runner.pairs)]
+        log(f"[rank {rank}] max pose error vs synthetic truth {max(errs) * 100:.2f} cm")
+    log(f"[rank {rank}] timed results checked {verify['checked']}, mismatches {verify['mismatches']}")
+    if verify["mismatches"]:
+        raise SystemExit(f"bench: {verify['mismatches']} timed result(s) differ from the single-frame path")
+
+    # (2) per-sequence trajectories (one all-gather of tagged relative poses)
+    if stream:
+        tags = [(k, j, r[1]) for j, r in enumerate(res) for k in [r[0]]]
+    else:
+        tags = [(0, r[0], r[1]) for r in res[-P:]] if len(res) >= P else []   # the last step: pairs 0..P-1 in order
+    allp, trajs = exchange_poses(tags, world, rank)
+
+    # (3) single-pair latency + serialised per-launch kernel durations, algorithmic bytes, busy time
+    probe = None
+    if not stream:
+        probe = latency_probe(lambda: runner.single([0]), probe_ctx, args.latency_pairs, args.iters)
+    fb = stats_pass(runner)
+    bytes_per_step = float(sum(fb.values())) if not stream else float(np.mean(list(fb.values()))) * P
+    busy = busy_pass(runner, args.busy_steps, torch.cuda.synchronize) if args.busy_steps > 0 else None
     trav = probe_ctx.traversal_stats()
-    bytes_launch = algorithmic_bytes_per_launch(stats, probe_ctx.last_trace, args.iters)
 
     if rank != 0:
         runner.close()
@@ -563,44 +746,81 @@ def main():
 
     traffic = None
     tj = pathlib.Path(args.traffic_json)
+    stats0 = probe_ctx.index_stats()
     if tj.exists() and args.workload == "B":
         try:
             tdat = json.loads(tj.read_text())
-            if tdat.get("queries") == stats["queries"] and tdat.get("iters") == args.iters:
+            if tdat.get("queries") == stats0["queries"] and tdat.get("iters") == args.iters:
                 traffic = tdat.get("bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
 
-    cpu = None
-    if world == 1 and not args.no_cpu and args.workload != "stream":
+    # (4) CPU baseline + parity of one pair (frame) vs the oracle
+    cpu = parity = None
+    if world == 1 and not args.no_cpu:
         log("[rank 0] CPU baseline (oracle) ...")
-        q0 = runner.pairs[0]
-        cpu = cpu_baseline(synth.soa(q0.source), synth.soa(q0.target), p, f"config {args.workload}",
-                           tensors=np.ascontiguousarray(q0.meta["tensors"].T) if args.workload == "E" else None)
+        if stream:
+            m, k = frames_at_launch[0][0]
+            fr = runner.seqs[0]
+            src, tgt, ten, truth = synth.soa(fr[k][1]), synth.soa(fr[m][0]), None, None
+            got = runner.single(0, (m, k))
+            label = f"stream (sequence 0, frame {k} vs frame {m}'s filtered scan)"
+        else:
+            q0 = runner.pairs[0]
+            src, tgt, truth = synth.soa(q0.source), synth.soa(q0.target), q0.true_pose
+            ten = np.ascontiguousarray(q0.meta["tensors"].T) if args.workload == "E" else None
+            k0, pose0, it0, st0, tr0 = runner.single([0])[0]
+            got = dict(pose=pose0, iters=it0, status=st0, trace=tr0)
+            label = f"config {args.workload}"
+        cpu, want = cpu_baseline(src, tgt, p, label, tensors=ten, faithful=True)
+        parity = parity_vs_oracle(got, want, truth)
+        parity["pair"] = label
         log(f"[rank 0] CPU baseline {cpu['value']:.4f} pairs/s (faithful {cpu['faithful']['value']:.4f}, "
-            f"{cpu['all_cores']['cores']} cores {cpu['all_cores']['value']:.3f})")
+            f"{cpu['host_share']['cores']} cores {cpu['host_share']['value']:.3f}); parity {parity}")
+        if stream:
+            cpu["unit"] = "frames/s"
 
+    # (5) roofline of the projection step (HBM-bound by the survey's accounting)
     roof = None
+    ms_step = elapsed / args.steps * 1e3
+    agg = bytes_per_step / (ms_step / 1e3) / 1e9
+    roof = {
+        "bound": "hbm",
+        "kernel": "projection step = k_knn_wave (packet traversal) + k_finish (exact re-rank, gates, IMLS, pass-1 "
+                  "normal equations) [+ k_project_lane fallback]: algorithmic bytes of every projection launch of a "
+                  "step / the time at least one projection kernel ran (union of HIP-event intervals of all launch "
+                  "sequences on one device clock, busy pass)",
+        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "traffic": traffic,
+        "algorithmic_bytes_per_step": bytes_per_step,
+        "aggregate_GBps": agg,
+        "aggregate_frac": agg / HBM_PEAK_GBS,
+    }
+    if busy:
+        bsteps = args.busy_steps
+        busy_step = busy["projection_busy_ms"] / bsteps
+        roof.update(achieved=bytes_per_step / (busy_step / 1e3) / 1e9 if busy_step > 0 else 0.0,
+                    busy_projection_ms_per_step=busy_step,
+                    busy_solve_ms_per_step=busy["solve_busy_ms"] / bsteps,
+                    busy_any_ms_per_step=busy["any_busy_ms"] / bsteps,
+                    busy_pass_ms_per_step=busy["wall_ms"] / bsteps,
+                    busy_pass_launches_per_step=busy["projection_launches"] / bsteps)
+        roof["frac"] = roof["achieved"] / HBM_PEAK_GBS
+    else:
+        roof.update(achieved=agg, frac=agg / HBM_PEAK_GBS)
     if probe:
         kd = probe["kernel_avg_ms"]
         dom_ms = kd["k_knn_wave"] + kd["k_finish"]
-        achieved = bytes_launch / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
-        roof = {
-            "bound": "hbm",
-            "kernel": "projection step = k_knn_wave (packet traversal) + k_finish (exact re-rank, gates, IMLS, "
-                      "pass-1 normal equations); serialised per-launch HIP-event duration, one pair in flight",
-            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": bytes_launch,
-            "avg_launch_ms": dom_ms,
-            "kernel_avg_ms": kd,
-            "aggregate_algorithmic_GBps": bytes_launch * args.iters * n_pairs * world / elapsed / 1e9,
-            "aggregate_frac": bytes_launch * args.iters * n_pairs * world / elapsed / 1e9 / HBM_PEAK_GBS,
-        }
+        b_launch = fb[0] / max(args.iters, 1)
+        roof["serialised_single_pair"] = {
+            "avg_launch_ms": dom_ms, "kernel_avg_ms": kd, "algorithmic_bytes_per_launch": b_launch,
+            "achieved": b_launch / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0,
+            "frac": b_launch / (dom_ms / 1e3) / 1e9 / HBM_PEAK_GBS if dom_ms > 0 else 0.0}
+
     solver_txt = "LS (trimmed, t=0.02)" if args.solver == "LS" else "RANSAC -> DRPM (shipped config.json solver)"
     if args.workload == "B":
         metric = "IMLS-ICP scan-pairs/s (HDL-64 ~120k-pt scan vs 10-scan map, 20 ICP iterations)"
-        workload = f"config B: HDL-64 scan vs 10-scan local map; a step = {P} independent scan pairs" + (" in one launch sequence" if fuse else " in flight, one stream each")
+        workload = f"config B: HDL-64 scan vs 10-scan local map; a step = {P} independent scan pairs" + (f" as {args.groups} launch sequences in flight" if fuse else " in flight, one stream each")
         unit = "scan-pairs/s"
     elif args.workload == "E":
         metric = ("IMLS-ICP scan-pairs/s (config E: tensor-voting normals + IMLS on sparse VLP-16 planetary scans, "
@@ -619,6 +839,7 @@ def main():
         workload = f"config C/D-like: {P} independent sequences, one frame each per step" + (" in one launch sequence" if fuse else ", one stream each")
         unit = "frames/s"
     per = np.array(per_step) * 1e3
+    first_traj = next(iter(trajs.values()), None)
     out = {
         "metric": metric,
         "value": value,
@@ -626,7 +847,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": ms_step,
         "ms_per_step_median": float(np.median(per)),
         "ms_per_step_p90": float(np.percentile(per, 90)),
         "ms_per_pair": elapsed / n_pairs * 1e3,
@@ -640,8 +861,8 @@ def main():
         "data": "synthetic (seeded HDL-64 / VLP-16 ray-cast urban scene, planetary-lidar-odometry_amd/synth.py)",
         "config": {
             "workload": workload,
-            "queries": int(stats["queries"]) if args.workload != "stream" else queries,
-            "map_points": int(stats["points"]) if args.workload != "stream" else map_points,
+            "queries": int(stats0["queries"]) if not stream else queries,
+            "map_points": int(stats0["points"]) if not stream else map_points,
             "icp_iterations": args.iters,
             "solver": solver_txt,
             "search_number": p.search_number,
@@ -649,9 +870,13 @@ def main():
             "launch_groups": args.groups if fuse else P,
             "parallelism": f"independent pairs per GPU over {world} GPU(s), RCCL pose all-gather" if world > 1 else "1 GPU",
         },
+        "verify": verify,
+        "parity": parity,
         "roofline": roof,
+        "busy_pass": busy,
         "traversal_per_launch": {k: v / args.iters for k, v in trav.items()},
-        "trajectory_end": traj[-1][:3, 3].tolist() if len(traj) else None,
+        "sequences": len(trajs),
+        "trajectory_end_seq0": first_traj[1][-1][:3, 3].tolist() if first_traj is not None and len(first_traj[1]) else None,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -180,8 +180,10 @@ int imls_synchronize(imls_ctx* ctx);
  * consume it.  imls_seed_rng restarts it (= srand(seed)); imls_get_rng_state / imls_set_rng_state
  * (the glibc TYPE_3 state: 31 words, front index, rear index, 0) hand one stream from a context to
  * another, e.g. when a caller creates a fresh context per frame as the reference creates a fresh
- * matcher (laser_odometry.cpp:489).  Contexts used concurrently (imls_register_batch) each run
- * their own stream. */
+ * matcher (laser_odometry.cpp:489).  Contexts used concurrently each run their own stream;
+ * imls_register_batch restarts a context's stream from params.ransac_seed before every pair, so its
+ * pairs are independent of the `streams` count and of the order they are given in.  imls_seed_rng
+ * leaves params.ransac_seed unchanged (contexts seeded differently still batch together). */
 int imls_seed_rng(imls_ctx* ctx, uint32_t seed);
 int imls_get_rng_state(imls_ctx* ctx, int32_t state[34]);
 int imls_set_rng_state(imls_ctx* ctx, const int32_t state[34]);
@@ -199,14 +201,22 @@ int imls_set_source(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n,
                     size_t stride_floats, size_t* n_kept, uint32_t* kept_index);
 /* Same, for clouds already resident in device memory as SoA float32[6][n]
  * (x[], y[], z[], nx[], ny[], nz[]) — inputs stay in HBM, no PCIe in the hot loop.
- * Deferred mode (n_kept NULL, and no kept_index): the call returns at once; the index build runs
+ * Count-less mode (n_kept NULL, and no kept_index): the call returns at once; the index build runs
  * at the first use of the cloud (a registration, a projection, or all the frames of an
- * imls_register_frames batch together, in one launch sequence), and when the context was last
- * registered in a batch of 8 or more frames the NaN filter waits for that first use too, reading
- * d_soa6 THEN — so the device buffer must stay valid and unchanged until that first use.
+ * imls_register_frames batch together, in one launch sequence).  When d_soa6 is read depends only on
+ * imls_set_defer: off (the default) — the NaN filter reads it on the context's stream right after
+ * the call (the buffer may be rewritten by work ordered after the context's stream has passed the
+ * call, e.g. after imls_synchronize or the next registration's result); on — the filter reads it at
+ * the first use, so it must stay valid and unchanged until that first use has run (e.g. the
+ * registration's result is collected).  Once filtered, the context works on its own copy.
  * Host-pointer calls copy their input at the call, so their buffers are free on return. */
 int imls_set_target_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
 int imls_set_source_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_kept);
+/* Deferred reads of count-less device loads (see above): with it on, the NaN filters of the frames
+ * of one imls_register_frames batch run together in three launches (a caller that loads hundreds of
+ * small frames per batch).  Default off.  Applies to imls_set_target_device, imls_set_source_device
+ * and imls_map_push_device (and to the owned upload buffers of the host-pointer forms). */
+int imls_set_defer(imls_ctx* ctx, int on);
 
 /* Map FIFO kept in HBM: replaces accumulateTargetCloud(newCloud, max_queue_size, ...)
  * (laser_odometry.cpp:116-136, called at 663-664) followed by the next frame's
@@ -221,7 +231,7 @@ int imls_map_push(imls_ctx* ctx, const float* xyz, const float* nrm, size_t n, s
                   size_t* n_map);
 /* Device-resident scan (SoA6 floats in HBM).  With max_queue_size 1 the map is this scan alone and
  * is indexed in place (no FIFO copy): the buffer must then stay valid until the map's first use
- * (deferred mode, n_map NULL) or until the context's stream has passed the push; raising
+ * (count-less with imls_set_defer on) or until the context's stream has passed the push; raising
  * max_queue_size afterwards needs a fresh push.  Larger FIFOs copy the scan into a FIFO slot. */
 int imls_map_push_device(imls_ctx* ctx, const float* d_soa6, size_t n, size_t* n_map);
 int imls_map_clear(imls_ctx* ctx);
@@ -280,6 +290,15 @@ int imls_register_frame(imls_ctx* ctx, double pose_out[16], int* iters_run, int*
 int imls_register_frame_async(imls_ctx* ctx);
 int imls_register_frame_result(imls_ctx* ctx, double pose_out[16], int* iters_run, int* status,
                                imls_iter_trace* trace);
+/* Per-iteration correspondences of imls_register_frame, for the reference's per-iteration outputs
+ * (saveMatchedPointsToFile of in_cloud_vec / ref_cloud_vec into matched_points/<ts>_<i>.txt,
+ * laser_odometry.cpp:621-623; saver.cpp:113-133).  While on, each iteration's correspondences are
+ * kept on the device (48 B per source point per iteration); after the frame's result,
+ * imls_captured_correspondences(iter) returns iteration `iter` (< iters_run) compacted in source
+ * order exactly as imls_project does (capacity: the kept source points). */
+int imls_capture_correspondences(imls_ctx* ctx, int on);
+int imls_captured_correspondences(imls_ctx* ctx, int iter, float* x_out, float* y_out, float* n_out,
+                                  uint32_t* src_index_out, size_t* n_valid);
 
 /* ---- many frames in one launch sequence (configs C/D: many sequences per GPU) ------------ */
 /* Registers the frames already loaded into ctxs[0..n) (each by imls_set_target / imls_map_push +
@@ -321,7 +340,7 @@ imls_batch* imls_batch_create(int device, const imls_params* p, int32_t streams)
 void imls_batch_destroy(imls_batch* b);
 const char* imls_batch_last_error(const imls_batch* b);
 /* Registers pairs[0..n_pairs) (each exactly as imls_set_target + imls_set_source +
- * imls_register_frame would); poses_out[16·i] (row-major), iters_out[i] and status_out[i]
+ * imls_register_frame would on a context freshly seeded with params.ransac_seed); poses_out[16·i] (row-major), iters_out[i] and status_out[i]
  * (imls_frame_status; each nullable) receive pair i's result.  Returns the first error (the
  * message names the pair); the pairs in flight are drained before returning. */
 int imls_register_batch(imls_batch* b, size_t n_pairs, const imls_pair_input* pairs, double* poses_out,
@@ -441,8 +460,17 @@ int imls_sample_point_cloud(imls_ctx* ctx, const imls_sample_params* p, const fl
  * the last reset.  kernel: 0 = projection (all its kernels), 1 = index build (all its kernels),
  * 2 = solve chain, 3 = k_knn_wave (packet traversal) alone, 4 = k_finish (exact stage) alone,
  * 5 = k_ring_pca (imls_ring_normals_pca), 6 = k_major_avg (imls_sample_point_cloud, major_axis),
- * 7 = imls_scan_front_end (all its kernels). */
+ * 7 = imls_scan_front_end (all its kernels).  enable: 0 off, 1 every kind above (the members of
+ * an imls_register_frames batch then build their indices one by one, each inside its events),
+ * 2 light — only the projection (0) and solve-chain (2) events of the iterations, the launch
+ * sequence otherwise unchanged (for timing a concurrent workload). */
 int imls_enable_timing(imls_ctx* ctx, int enable);
+/* Records a process-wide origin event on ctx's stream (and waits for it).  Afterwards every
+ * harvested timing pair of every context on that device is also kept as an interval (start, end)
+ * in ms since the origin: imls_timing_intervals copies up to `cap` of them (out[2k], out[2k+1]) and
+ * returns their count in *n — the union over contexts is the busy time of concurrent work. */
+int imls_timing_origin(imls_ctx* ctx);
+int imls_timing_intervals(imls_ctx* ctx, int kernel, double* out, size_t cap, size_t* n);
 /* Traversal / neighbour counters (imls_traversal_stats, and the sum_kq / nn_found fields of
  * imls_index_stats) are collected only while enabled (default off: they are device-scope atomics
  * onto a few shared words from every wave, ~60 µs per projection at config B). */

@@ -105,12 +105,24 @@ inline bool strided_view(const PointCloud2& m, StridedCloud* out) {
     return true;
 }
 
+// A message holds n = width·height records of point_step bytes: its data must cover them.
+inline bool msg_covers(const PointCloud2& m) {
+    const size_t n = (size_t)m.width * m.height;
+    return m.point_step == 0 ? n == 0 : m.data.size() / m.point_step >= n;
+}
+
 // pcl::fromROSMsg into 48-byte PointXYZINormal records (12 floats each): fields matched by name,
-// FLOAT32 only; a field the message lacks stays 0.
-inline void xyzinormal_from_msg(const PointCloud2& m, float* records) {
+// FLOAT32 only; a field the message lacks stays 0.  Returns false (records untouched) for a
+// malformed message: data shorter than width·height·point_step, or a field not inside point_step.
+inline bool xyzinormal_from_msg(const PointCloud2& m, float* records) {
     static const char* names[8] = {"x", "y", "z", "intensity", "normal_x", "normal_y", "normal_z", "curvature"};
     static const uint32_t dst[8] = {0, 1, 2, 8, 4, 5, 6, 9};
     const size_t n = (size_t)m.width * m.height;
+    if (!msg_covers(m)) return false;
+    for (int k = 0; k < 8; ++k) {
+        const PointField* f = find_field(m, names[k]);
+        if (f && f->datatype == FLOAT32 && (size_t)f->offset + 4 > m.point_step) return false;
+    }
     std::memset(records, 0, n * kXYZINormalStep);
     for (int k = 0; k < 8; ++k) {
         const PointField* f = find_field(m, names[k]);
@@ -118,6 +130,7 @@ inline void xyzinormal_from_msg(const PointCloud2& m, float* records) {
         for (size_t i = 0; i < n; ++i)
             std::memcpy(records + 12 * i + dst[k], m.data.data() + i * m.point_step + f->offset, 4);
     }
+    return true;
 }
 
 // ---- (2) libpointmatcher DataPoints -----------------------------------------------------------
@@ -191,11 +204,16 @@ inline PointCloud2 dp_to_msg(const DPCloud& dp, const std::string& frame_id, dou
 
 // rosMsgToLibPointMatcherCloud (saver.cpp:224-306): fixed labels, fields read by position.
 // Times are allocated (one "time" row) and left 0.  Returns false (empty cloud) for a message
-// without fields, or one with fewer than the 12 fields it reads.
+// without fields, one with fewer than the 12 fields it reads, or a malformed one (see msg_covers).
 inline bool dp_from_msg(const PointCloud2& m, DPCloud* dp) {
     *dp = DPCloud{};
     if (m.fields.empty()) return false;
     if (m.fields.size() < 12) return false;
+    // malformed: data shorter than width·height·point_step, or a read past point_step
+    static const uint32_t span_of[12] = {1, 1, 1, 1, 1, 1, 3, 3, 1, 4, 7, 1};
+    if (!msg_covers(m)) return false;
+    for (int k = 0; k < 12; ++k)
+        if ((size_t)m.fields[k].offset + 4 * (size_t)span_of[k] > m.point_step) return false;
     dp->feature_labels = {{"x", 1}, {"y", 1}, {"z", 1}, {"pad", 1}};
     dp->descriptor_labels = dp_descriptor_labels();
     dp->time_labels = {{"time", 1}};

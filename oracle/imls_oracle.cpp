@@ -17,6 +17,7 @@
 #include <cstring>
 #include <limits>
 #include <numeric>
+#include <sstream>
 #include <vector>
 
 namespace {
@@ -1234,6 +1235,21 @@ void oracle_chain_pose(const double prev[16], const double rel[16], double out[1
 // savePoseToFile (saver.cpp:46-54): Eigen::Quaterniond(Matrix3d) (Eigen's quaternionbase_assign_impl
 // for a 3x3: trace branch, else the largest-diagonal branch with strict '>'), then
 // `std::fixed << std::setprecision(6)`: ts tx ty tz qx qy qz qw.  Returns the line length.
+// saveMatchedPointsToFile (saver.cpp:113-133): `sx sy sz yx yy yz` per correspondence, the doubles
+// of Eigen::Vector3d built from the float clouds, default std::ostream formatting.  x3 / y3: [n][3].
+// Returns the byte count written (or needed, when it exceeds cap).
+size_t oracle_format_matched(const float* x3, const float* y3, size_t n, char* buf, size_t cap) {
+    std::ostringstream file;
+    for (size_t i = 0; i < n; ++i) {
+        const double s0 = x3[3 * i], s1 = x3[3 * i + 1], s2 = x3[3 * i + 2];
+        const double m0 = y3[3 * i], m1 = y3[3 * i + 1], m2 = y3[3 * i + 2];
+        file << s0 << " " << s1 << " " << s2 << " " << m0 << " " << m1 << " " << m2 << "\n";
+    }
+    const std::string t = file.str();
+    if (buf && t.size() < cap) std::memcpy(buf, t.c_str(), t.size() + 1);
+    return t.size();
+}
+
 int oracle_format_pose(const double P[16], const char* timestamp, char* buf, size_t cap) {
     auto m = [&](int r, int c) { return P[r * 4 + c]; };
     double q[4];   // x y z w

@@ -82,6 +82,7 @@ int oracle_register_frame_rs(const float* src6, size_t N, const float* tgt6, siz
  * (saver.cpp:46-54, Eigen quaternion + fixed/6) into buf; returns its length. */
 void oracle_chain_pose(const double prev[16], const double rel[16], double out[16]);
 int oracle_format_pose(const double pose[16], const char* timestamp, char* buf, size_t cap);
+size_t oracle_format_matched(const float* x3, const float* y3, size_t n, char* buf, size_t cap);
 
 /* CPU-baseline modes (bench.py only): threads of the per-query projection loop, and the
  * "faithful" container costs of the reference (AoS copy per iteration, erase per rejected point,

@@ -47,6 +47,8 @@ def lib():
                                                VP, C.c_int, VP, P(SZ), P(C.c_double), P(C.c_double)]
         L.oracle_chain_pose.argtypes = [VP, VP, VP]
         L.oracle_format_pose.argtypes = [VP, C.c_char_p, C.c_char_p, SZ]
+        L.oracle_format_matched.argtypes = [VP, VP, SZ, C.c_char_p, SZ]
+        L.oracle_format_matched.restype = SZ
         L.oracle_tv_normals.argtypes = [VP, SZ, VP, VP, SZ, P(abi.ImlsParams), VP, VP, VP]
         L.oracle_rand_seed.argtypes = [VP, C.c_uint32]
         L.oracle_rand_next.argtypes = [VP]
@@ -177,6 +179,16 @@ def format_pose(pose, timestamp: str) -> str:
     buf = C.create_string_buffer(512)
     n = lib().oracle_format_pose(_ptr(P), timestamp.encode(), buf, 512)
     assert 0 < n < 512
+    return buf.value.decode()
+
+
+def format_matched(x3, y3) -> str:
+    """saveMatchedPointsToFile's text (saver.cpp:113-133) for float (n, 3) clouds."""
+    x3 = np.ascontiguousarray(x3, dtype=np.float32).reshape(-1, 3)
+    y3 = np.ascontiguousarray(y3, dtype=np.float32).reshape(-1, 3)
+    need = lib().oracle_format_matched(_ptr(x3), _ptr(y3), len(x3), None, 0)
+    buf = C.create_string_buffer(need + 1)
+    lib().oracle_format_matched(_ptr(x3), _ptr(y3), len(x3), buf, need + 1)
     return buf.value.decode()
 
 

@@ -210,6 +210,11 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_map_push_device": (C.c_int, [VP, VP, SZ, P(SZ)]),
         "imls_map_clear": (C.c_int, [VP]),
         "imls_map_size": (C.c_int, [VP, P(SZ), P(SZ)]),
+        "imls_set_defer": (C.c_int, [VP, C.c_int]),
+        "imls_capture_correspondences": (C.c_int, [VP, C.c_int]),
+        "imls_captured_correspondences": (C.c_int, [VP, C.c_int, VP, VP, VP, VP, P(SZ)]),
+        "imls_timing_origin": (C.c_int, [VP]),
+        "imls_timing_intervals": (C.c_int, [VP, C.c_int, VP, SZ, P(SZ)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -230,7 +235,9 @@ ABI_SYMBOLS = (
     "imls_batch_last_error", "imls_register_batch", "imls_seed_rng", "imls_get_rng_state",
     "imls_set_rng_state", "imls_map_push", "imls_map_push_device", "imls_map_clear", "imls_map_size",
     "imls_register_frames", "imls_register_frames_async", "imls_register_frames_result",
-    "imls_default_front_params", "imls_scan_front_end", "imls_enable_stats",
+    "imls_default_front_params", "imls_scan_front_end", "imls_enable_stats", "imls_set_defer",
+    "imls_timing_origin", "imls_timing_intervals", "imls_capture_correspondences",
+    "imls_captured_correspondences",
 )
 
 _LIB = None

@@ -72,7 +72,7 @@ struct imls_ctx {
     const float* sf_soa = nullptr;
     size_t tf_n = 0, sf_n = 0;
     bool tgt_filter_deferred = false, src_filter_deferred = false;
-    size_t last_batch_n = 0;              // frames of the last batch this context was part of
+    bool defer = false;                   // imls_set_defer: count-less loads read their input at first use
     const float* ten_src = nullptr;       // tensors set while the target build was pending
     size_t ten_n = 0;
     bool ten_pending = false;
@@ -85,12 +85,19 @@ struct imls_ctx {
     // correspondences + solver state
     DevBuf cs, cd, cn, solve_mem, trace_mem, stats, rows_d, pose_tmp;
     DevBuf ransac_mem, rng;               // RANSAC scratch + the glibc rand() state (34 words)
-    int rng_seed_state[34] = {};          // host copy of the seeded state (source of the async upload)
+    int rng_seed_state[34] = {};          // host copy of the seeded state
     bool rng_dirty = true;                // upload rng_seed_state to the device before its next use
+    int* h_rng = nullptr;                 // pinned source of that upload (rewritten after ev_rng)
+    hipEvent_t ev_rng = nullptr;
     bool rng_init = false;                // seeded from params.ransac_seed (first imls_set_params)
     SolveState st{};
     int st_N = -1, trace_cap = 0;
     bool has_corr = false;
+    // per-iteration correspondences of imls_register_frame (imls_capture_correspondences): slot it =
+    // cs / cd / cn (float4 [N] each) after iteration it's projection
+    bool capture = false;
+    DevBuf cap_mem;
+    int cap_iters = 0, cap_N = 0;
     // async frame results
     imls_iter_trace* h_trace = nullptr;   // pinned
     double* h_misc = nullptr;             // pinned: pose[16], iters, status
@@ -118,8 +125,11 @@ struct imls_ctx {
     // traversal / neighbour counters (imls_traversal_stats): off by default — their per-wave
     // device-scope atomics onto a few shared words cost ~60 µs per projection at config B
     bool collect_stats = false;
-    // timing
-    bool timing = false;
+    // timing: 0 off, 1 every launch kind (a batch's members then build one by one, each inside its
+    // own events), 2 light — the projection / solve events of the iterations only (builds unchanged),
+    // kept as intervals on a process-wide clock (imls_timing_intervals: busy time of concurrent work)
+    int timing = 0;
+    std::vector<std::pair<double, double>> iv[kTimingKinds];
     std::vector<hipEvent_t> ev;
     int ev_used = 0;
     std::vector<std::pair<int, int>> ev_pairs[kTimingKinds];
@@ -322,10 +332,16 @@ RansacParams ransac_params(const imls_params& p) {
 int sync_rng(imls_ctx* c) {
     if (!grow(c->rng, 34 * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (rand state)");
     if (!c->rng_dirty) return IMLS_OK;
-    if (hipMemcpyAsync(c->rng.p, c->rng_seed_state, 34 * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    // pinned source, rewritten only after its previous copy ran (ev_rng): no host wait on the stream
+    // (a caller that reseeds before every frame keeps its frames in flight)
+    if (!c->h_rng && hipHostMalloc((void**)&c->h_rng, 34 * 4) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipHostMalloc (rand state)");
+    if (!c->ev_rng && hipEventCreateWithFlags(&c->ev_rng, hipEventDisableTiming) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "hipEventCreate (rand state)");
+    if (hipEventSynchronize(c->ev_rng) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "rand state upload");
+    std::memcpy(c->h_rng, c->rng_seed_state, 34 * 4);
+    if (hipMemcpyAsync(c->rng.p, c->h_rng, 34 * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipEventRecord(c->ev_rng, c->stream) != hipSuccess)
         return fail(c, IMLS_ERR_DEVICE, "rand state upload");
-    // the source must stay valid until the copy ran: wait (seeding is rare)
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "rand state upload");
     c->rng_dirty = false;
     return IMLS_OK;
 }
@@ -443,13 +459,23 @@ hipEvent_t* project_marks(imls_ctx* c, hipEvent_t marks[3]) {
     return marks;
 }
 
+// Process-wide origin of the timing intervals (imls_timing_origin): one clock for every context
+// of the device, so the busy time of concurrent launch sequences is the union of their intervals.
+hipEvent_t g_origin = nullptr;
+int g_origin_device = -1;
+
 void harvest_timing(imls_ctx* c) {
+    const bool iv = g_origin && g_origin_device == c->device;
     for (int k = 0; k < kTimingKinds; ++k) {
         for (auto& pr : c->ev_pairs[k]) {
             float ms = 0;
             if (hipEventElapsedTime(&ms, c->ev[pr.first], c->ev[pr.second]) == hipSuccess) {
                 c->t_ms[k] += ms;
                 c->t_n[k] += 1;
+                float a = 0, b = 0;
+                if (iv && hipEventElapsedTime(&a, g_origin, c->ev[pr.first]) == hipSuccess &&
+                    hipEventElapsedTime(&b, g_origin, c->ev[pr.second]) == hipSuccess)
+                    c->iv[k].push_back({a, b});
             }
         }
         c->ev_pairs[k].clear();
@@ -585,7 +611,7 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused, HostS
     bool any = false, timing = false;
     for (size_t k = 0; k < n; ++k) {
         any |= ctxs[k]->tgt_pending || ctxs[k]->src_pending;
-        timing |= ctxs[k]->timing;
+        timing |= ctxs[k]->timing == 1;
     }
     if (!any) return IMLS_OK;
     if (timing) {
@@ -704,11 +730,11 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused, HostS
     return IMLS_OK;
 }
 
-// A count-less load defers its NaN filter to the first use when the context was last registered
-// in a batch of ≥ kDeferBatch frames (the batch then filters all its members in three launches);
-// otherwise the filter is enqueued at once, behind the context's running work, so it overlaps it.
-constexpr size_t kDeferBatch = 8;
-bool defer_filter(const imls_ctx* c) { return c->last_batch_n >= kDeferBatch; }
+// A count-less load defers its NaN filter to the first use only when the caller asked for deferred
+// reads (imls_set_defer: a batch then filters all its members in three launches); otherwise the
+// filter is enqueued at once, behind the context's running work, so it overlaps it.  Either way
+// the rule the caller sees depends on that switch alone, never on the context's history.
+bool defer_filter(const imls_ctx* c) { return c->defer; }
 
 int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
     if (n == 0 || n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "target size out of range");
@@ -894,7 +920,7 @@ void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->front_mem, &c->sample_mem, &c->pca_mem, &c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
+    DevBuf* bufs[] = {&c->cap_mem, &c->front_mem, &c->sample_mem, &c->pca_mem, &c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
                       &c->upload_t, &c->spt, &c->snr, &c->sscratch,
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
@@ -906,6 +932,8 @@ void imls_destroy(imls_ctx* c) {
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->h_trace) (void)hipHostFree(c->h_trace);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
+    if (c->h_rng) (void)hipHostFree(c->h_rng);
+    if (c->ev_rng) (void)hipEventDestroy(c->ev_rng);
     if (c->tab_h) (void)hipHostFree(c->tab_h);
     if (c->h_cnt) (void)hipHostFree(c->h_cnt);
     for (int k = 0; k < 2; ++k) {
@@ -947,7 +975,8 @@ const char* imls_last_error(const imls_ctx* c) { return c ? c->err.c_str() : "nu
 
 int imls_seed_rng(imls_ctx* c, uint32_t seed) {
     if (!c) return IMLS_ERR_ARG;
-    c->P.ransac_seed = seed;
+    // the stream restarts; params.ransac_seed is left as set (contexts seeded differently still
+    // batch together: frames_async compares the params without it)
     ransac_seed_host(seed, c->rng_seed_state);
     c->rng_dirty = true;
     return IMLS_OK;
@@ -1300,6 +1329,12 @@ int imls_register_frame_async(imls_ctx* c) {
     if (int rc = ensure_map_normals(c)) return rc;
     const TreeView tv = tree_view(c);
     if (int rc = prepare_ransac(c, c->N)) return rc;
+    c->cap_iters = 0;
+    if (c->capture && iters > 0) {
+        if (!grow(c->cap_mem, (size_t)iters * c->N * 48)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (capture)");
+        c->cap_iters = iters;
+        c->cap_N = c->N;
+    }
     for (int it = 0; it < iters; ++it) {
         int slot;
         hipEvent_t marks[3];
@@ -1309,6 +1344,12 @@ int imls_register_frame_async(imls_ctx* c) {
                        c->st.partial1, tr + it, stats_ptr(c), fb_list(c), fb_count(c), c->lane_mode,
                        c->st.delta, (int*)c->prevnn.p, it > 0 && c->temporal_seed, project_marks(c, marks));
         timed_end(c, 0, slot);
+        if (c->cap_iters) {   // this iteration's correspondences (stale, and never read, once the frame stopped)
+            char* dst = (char*)c->cap_mem.p + (size_t)it * c->N * 48;
+            hipMemcpyAsync(dst, c->cs.p, (size_t)c->N * 16, hipMemcpyDeviceToDevice, c->stream);
+            hipMemcpyAsync(dst + (size_t)c->N * 16, c->cd.p, (size_t)c->N * 16, hipMemcpyDeviceToDevice, c->stream);
+            hipMemcpyAsync(dst + (size_t)c->N * 32, c->cn.p, (size_t)c->N * 16, hipMemcpyDeviceToDevice, c->stream);
+        }
         timed_begin(c, 2, slot);
         launch_solve(c->stream, solve_launch(c, tr + it, 1));
         timed_end(c, 2, slot);
@@ -1429,7 +1470,9 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         for (size_t j = 0; j < k; ++j)
             if (ctxs[j] == c) return fail(L, IMLS_ERR_ARG, "a context appears twice in the batch");
         if (c->device != L->device) return fail(L, IMLS_ERR_ARG, "batch contexts must share one device");
-        if (std::memcmp(&c->P, &L->P, sizeof(imls_params)) != 0)
+        imls_params pc = c->P, pl = L->P;
+        pc.ransac_seed = pl.ransac_seed = 0;    // each context runs its own rand() stream
+        if (std::memcmp(&pc, &pl, sizeof(imls_params)) != 0)
             return fail(L, IMLS_ERR_ARG, "batch contexts must share their params (context " + std::to_string(k) + ")");
         if (c->lane_mode != L->lane_mode || c->temporal_seed != L->temporal_seed || c->B != L->B)
             return fail(L, IMLS_ERR_ARG, "batch contexts must share their traversal settings");
@@ -1449,7 +1492,6 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
             return fail(L, IMLS_ERR_STATE, "context " + std::to_string(k) + ": set_target and set_source first");
     }
     L->members.assign(ctxs, ctxs + n);
-    for (size_t k = 0; k < n; ++k) ctxs[k]->last_batch_n = n;
     L->batch_fused = batch_fusable(L) && (L->P.solve_method != IMLS_SOLVE_RANSAC || n <= (size_t)kMaxRansacBatch);
     if (!L->batch_fused) {
         // one launch sequence per frame, each on its own context stream
@@ -1536,9 +1578,10 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         launch_project_batch(s, tab, nh, (int)n, kp, it, it > 0 && L->temporal_seed);
         timed_end(L, 0, slot);
         timed_begin(L, 2, slot);
-        if (kp.solve_method == IMLS_SOLVE_RANSAC)
-            launch_ransac_batch(s, tab, nh, (int)n, kp, rp, it);
-        else
+        if (kp.solve_method == IMLS_SOLVE_RANSAC) {
+            if (launch_ransac_batch(s, tab, nh, (int)n, kp, rp, it))
+                return fail(L, IMLS_ERR_CAPACITY, "RANSAC batch larger than kMaxRansacBatch frames");
+        } else
             launch_solve_batch(s, tab, nh, (int)n, kp, it);
         timed_end(L, 2, slot);
     }
@@ -1656,6 +1699,11 @@ int imls_register_batch(imls_batch* b, size_t n_pairs, const imls_pair_input* pa
         for (size_t k = 0; k < m; ++k) {
             imls_ctx* c = b->ctx[k];
             const imls_pair_input& q = pairs[g + k];
+            // independent pairs: each starts the RANSAC rand() stream from params.ransac_seed (as the
+            // reference's process does for its first frame), so a pair's result does not depend on
+            // `streams` or on the pairs its context handled before
+            ransac_seed_host(c->P.ransac_seed, c->rng_seed_state);
+            c->rng_dirty = true;
             int rc = imls_set_target(c, q.tgt_xyz, q.tgt_nrm, q.n_tgt, q.stride_floats, nullptr);
             if (rc == IMLS_OK) rc = imls_set_source(c, q.src_xyz, q.src_nrm, q.n_src, q.stride_floats, nullptr, nullptr);
             if (rc != IMLS_OK) {
@@ -1791,8 +1839,72 @@ int imls_enable_stats(imls_ctx* c, int enable) {
 }
 
 int imls_enable_timing(imls_ctx* c, int enable) {
+    if (!c || enable < 0 || enable > 2) return IMLS_ERR_ARG;
+    c->timing = enable;
+    return IMLS_OK;
+}
+
+int imls_capture_correspondences(imls_ctx* c, int on) {
     if (!c) return IMLS_ERR_ARG;
-    c->timing = enable != 0;
+    c->capture = on != 0;
+    return IMLS_OK;
+}
+
+int imls_captured_correspondences(imls_ctx* c, int iter, float* x_out, float* y_out, float* n_out,
+                                  uint32_t* src_index_out, size_t* n_valid) {
+    if (!c || !n_valid) return IMLS_ERR_ARG;
+    if (c->pending) return fail(c, IMLS_ERR_STATE, "collect the frame first (imls_register_frame_result)");
+    if (iter < 0 || iter >= c->cap_iters) return fail(c, IMLS_ERR_STATE, "no captured iteration " + std::to_string(iter));
+    if (int rc = check_device(c)) return rc;
+    const size_t N = (size_t)c->cap_N;
+    std::vector<float> h(N * 12);
+    if (hipMemcpy(h.data(), (const char*)c->cap_mem.p + (size_t)iter * N * 48, N * 48, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "capture download");
+    const float *hs = h.data(), *hd = hs + 4 * N, *hn = hs + 8 * N;
+    size_t k = 0;
+    for (size_t i = 0; i < N; ++i) {
+        if (hs[4 * i + 3] == 0.f) continue;   // rejected (erased from in_cloud by the reference)
+        for (int d = 0; d < 3; ++d) {
+            if (x_out) x_out[3 * k + d] = hs[4 * i + d];
+            if (y_out) y_out[3 * k + d] = hd[4 * i + d];
+            if (n_out) n_out[3 * k + d] = hn[4 * i + d];
+        }
+        if (src_index_out) src_index_out[k] = (uint32_t)i;
+        ++k;
+    }
+    *n_valid = k;
+    return IMLS_OK;
+}
+
+int imls_set_defer(imls_ctx* c, int on) {
+    if (!c) return IMLS_ERR_ARG;
+    c->defer = on != 0;
+    return IMLS_OK;
+}
+
+int imls_timing_origin(imls_ctx* c) {
+    if (!c) return IMLS_ERR_ARG;
+    if (int rc = check_device(c)) return rc;
+    if (g_origin && g_origin_device != c->device) {
+        (void)hipEventDestroy(g_origin);
+        g_origin = nullptr;
+    }
+    if (!g_origin && hipEventCreate(&g_origin) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipEventCreate (origin)");
+    g_origin_device = c->device;
+    if (hipEventRecord(g_origin, c->stream) != hipSuccess || hipEventSynchronize(g_origin) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "origin event");
+    for (auto& v : c->iv) v.clear();
+    return IMLS_OK;
+}
+
+int imls_timing_intervals(imls_ctx* c, int kernel, double* out, size_t cap, size_t* n) {
+    if (!c || kernel < 0 || kernel >= kTimingKinds || !n) return IMLS_ERR_ARG;
+    const auto& v = c->iv[kernel];
+    *n = v.size();
+    for (size_t k = 0; k < v.size() && k < cap && out; ++k) {
+        out[2 * k] = v[k].first;
+        out[2 * k + 1] = v[k].second;
+    }
     return IMLS_OK;
 }
 
@@ -1805,7 +1917,7 @@ int imls_kernel_timing(imls_ctx* c, int kernel, double* total_ms, uint64_t* laun
 
 int imls_reset_timing(imls_ctx* c) {
     if (!c) return IMLS_ERR_ARG;
-    for (int k = 0; k < kTimingKinds; ++k) { c->t_ms[k] = 0; c->t_n[k] = 0; c->ev_pairs[k].clear(); }
+    for (int k = 0; k < kTimingKinds; ++k) { c->t_ms[k] = 0; c->t_n[k] = 0; c->ev_pairs[k].clear(); c->iv[k].clear(); }
     c->ev_used = 0;
     return IMLS_OK;
 }

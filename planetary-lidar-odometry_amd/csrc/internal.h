@@ -315,7 +315,7 @@ int ransac_init_tables(int device);    // the rand() jump table on `device` (cur
 constexpr int kMaxRansacBatch = 1024;  // frames per batched RANSAC launch
 // Batched RANSAC (+ final LS / weighted LS / DRPM) for all frames of tab, ICP iteration `it`:
 // one launch per step for the whole batch, every frame at its own count / rand() stream / done flag.
-void launch_ransac_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp,
+int launch_ransac_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp,
                          const RansacParams& rp, int it);
 void ransac_seed_host(uint32_t seed, int st[34]);
 

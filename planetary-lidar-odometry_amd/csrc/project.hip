@@ -84,19 +84,29 @@ __device__ __forceinline__ bool angle_reject(const double ns[3], double n0, doub
     return angle > thr;
 }
 
+// Sorted insertion of (d, pos) into the ascending top-KL list; precondition d < lk[KL−1].  With
+// c[k] = d < lk[k] (old keys; monotone in k, so the first true c is the insertion point) every slot
+// is independent of the others: key k = med3(lk[k−1], d, lk[k]) (= lk[k−1] when c[k−1], else
+// min(d, lk[k]): the keys are sorted and never NaN), position k = c[k−1] ? lp[k−1] : (c[k] ? pos :
+// lp[k]) — one v_med3 + one compare + two selects per slot, none of fminf's canonicalising maxes.
+// Equal keys keep their order (a new key goes after the ones it equals).
 template <int KL>
 __device__ __forceinline__ void insert_top(float (&lk)[KL], int (&lp)[KL], float d, int pos) {
-    bool prev = true;   // prev = d < lk[k] (old value), i.e. the shift decision of slot k+1
+    bool c[KL];
 #pragma unroll
-    for (int k = KL - 1; k >= 0; --k) {
-        const bool sh = (k > 0) ? (d < lk[(k > 0) ? k - 1 : 0]) : false;
-        const float nk = sh ? lk[(k > 0) ? k - 1 : 0] : fminf(d, lk[k]);
-        const int np = sh ? lp[(k > 0) ? k - 1 : 0] : (prev ? pos : lp[k]);
-        lk[k] = nk;
-        lp[k] = np;
-        prev = sh;
+    for (int k = 0; k < KL - 1; ++k) c[k] = d < lk[k];
+    c[KL - 1] = true;
+#pragma unroll
+    for (int k = KL - 1; k >= 1; --k) {
+        lp[k] = c[k - 1] ? lp[k - 1] : (c[k] ? pos : lp[k]);
+        lk[k] = __builtin_amdgcn_fmed3f(lk[k - 1], d, lk[k]);
     }
+    lp[0] = c[0] ? pos : lp[0];
+    lk[0] = c[0] ? d : lk[0];
 }
+
+// min(a, b) of non-NaN floats (a plain select: fminf canonicalises both operands first)
+__device__ __forceinline__ float fmin_nn(float a, float b) { return a < b ? a : b; }
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -405,7 +415,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 }
             }
         }
-        bnd = fminf(r2s, lk[KL - 1]);
+        bnd = fmin_nn(r2s, lk[KL - 1]);
     }
     // leaf scan shared by the seed pass and the traversal: the lanes in `want` test every point of
     // leaf `leaf` against their bound; `listed`: the leaf may hold points already in a lane's
@@ -415,6 +425,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
 #ifdef IMLS_DEBUG_WAVE_TRACE
     unsigned dbg_ev = 0, dbg_ins = 0;
     unsigned dbg_sparse = 0, dbg_bcast = 0, dbg_sparse_lanes = 0, dbg_sparse_ins = 0;
+    unsigned dbg_seed_steps = 0, dbg_seed_pts = 0;   // seed points where any lane inserted / seed points scanned
 #endif
     auto scan_leaf = [&](int leaf, unsigned long long want, bool listed) {
         const int base = leaf * B;
@@ -493,7 +504,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                             ++dbg_ins;
 #endif
                             insert_top<KL>(lk, lp, d32, base + j);
-                            bnd = fminf(r2s, lk[KL - 1]);
+                            bnd = fmin_nn(r2s, lk[KL - 1]);
                         }
                     }
 #ifdef IMLS_DEBUG_WAVE_TRACE
@@ -529,7 +540,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                         ++dbg_sparse_ins;
 #endif
                         insert_top<KL>(lk, lp, dj, base + j);
-                        bnd = fminf(r2s, lk[KL - 1]);
+                        bnd = fmin_nn(r2s, lk[KL - 1]);
                     }
                 }
             }
@@ -549,7 +560,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
 #endif
                 if (ins) {
                     insert_top<KL>(lk, lp, d32, base + j);
-                    bnd = fminf(r2s, lk[KL - 1]);
+                    bnd = fmin_nn(r2s, lk[KL - 1]);
                 }
             }
         }
@@ -601,9 +612,13 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             for (int k = 0; k < kSeedChunk; ++k) {
                 const float ex = qs[k].x - xf[0], ey = qs[k].y - xf[1], ez = qs[k].z - xf[2];
                 const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                dbg_seed_steps += __ballot(p0 + k < pend && d32 <= bnd && d32 < lk[KL - 1]) ? 1 : 0;
+                ++dbg_seed_pts;
+#endif
                 if (p0 + k < pend && d32 <= bnd && d32 < lk[KL - 1]) {
                     insert_top<KL>(lk, lp, d32, p0 + k);
-                    bnd = fminf(r2s, lk[KL - 1]);
+                    bnd = fmin_nn(r2s, lk[KL - 1]);
                 }
             }
 #pragma unroll
@@ -734,6 +749,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 r[2] = n_leaf; r[3] = n_inner; r[4] = dbg_ev; r[5] = dbg_sparse; r[6] = dbg_bcast;
                 r[7] = __popcll(gl); r[8] = __popcll(wi); r[9] = __popcll(w1); r[10] = __float_as_uint(wmax);
                 r[11] = dbg_sparse_lanes; r[12] = sins; r[13] = dbg_ins;
+                r[14] = dbg_seed_steps; r[15] = __builtin_amdgcn_readfirstlane(dbg_seed_pts);
             }
         }
     }

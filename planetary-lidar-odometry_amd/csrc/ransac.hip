@@ -1147,9 +1147,10 @@ RansacFrame ransac_frame(void* scratch, int cap, int* rng) {
     return F;
 }
 
-void launch_ransac_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp,
-                         const RansacParams& rp, int it) {
-    if (npairs <= 0 || npairs > kMaxRansacBatch) return;
+int launch_ransac_batch(hipStream_t s, const PairDev* tab, const int* n_host, int npairs, const KParams& kp,
+                        const RansacParams& rp, int it) {
+    if (npairs <= 0) return 0;
+    if (npairs > kMaxRansacBatch) return -1;   // the select kernels keep one slot per frame in LDS
     std::vector<int> caps((size_t)npairs);
     int maxc = 1;
     for (int k = 0; k < npairs; ++k) {
@@ -1202,6 +1203,7 @@ void launch_ransac_batch(hipStream_t s, const PairDev* tab, const int* n_host, i
             k_drpm_final_b<<<g1, 256, 0, s>>>(tab, fk, rp.drpm_threshold, it);   // + RANSAC's trace record
     }
     if (rp.final_method == IMLS_FINAL_LS || rp.final_method == IMLS_FINAL_WEIGHTED_LS) k_ransac_trace_b<<<g1, 64, 0, s>>>(tab, it);
+    return 0;
 }
 
 int ransac_init_tables(int device) {

@@ -316,7 +316,38 @@ class ImlsContext:
         self._check(self.lib.imls_enable_stats(self.ctx, int(on)))
 
     def enable_timing(self, on=True):
+        """on: False/0 off, True/1 every launch kind, 2 light (projection + solve events only)."""
         self._check(self.lib.imls_enable_timing(self.ctx, int(on)))
+
+    def set_defer(self, on=True):
+        """Count-less device loads read their buffer at first use (imls_set_defer)."""
+        self._check(self.lib.imls_set_defer(self.ctx, int(bool(on))))
+
+    def capture_correspondences(self, on=True):
+        """Keep every iteration's correspondences of register_frame (imls_capture_correspondences)."""
+        self._check(self.lib.imls_capture_correspondences(self.ctx, int(bool(on))))
+
+    def captured(self, it: int):
+        """Iteration `it` of the last register_frame: (x, y, n, source index), source order."""
+        N = max(self.n_source if self.n_source is not None else self.index_stats()["queries"], 1)
+        x = np.zeros((N, 3), np.float32); y = np.zeros((N, 3), np.float32); n = np.zeros((N, 3), np.float32)
+        idx = np.zeros(N, np.uint32); nv = C.c_size_t()
+        self._check(self.lib.imls_captured_correspondences(self.ctx, int(it), _ptr(x), _ptr(y), _ptr(n), _ptr(idx),
+                                                           C.byref(nv)))
+        k = nv.value
+        return x[:k], y[:k], n[:k], idx[:k]
+
+    def timing_origin(self):
+        """Process-wide origin of the timing intervals (imls_timing_origin)."""
+        self._check(self.lib.imls_timing_origin(self.ctx))
+
+    def timing_intervals(self, kernel: int) -> np.ndarray:
+        """(n, 2) ms since the origin of every harvested launch of `kernel` (imls_timing_intervals)."""
+        n = C.c_size_t()
+        self._check(self.lib.imls_timing_intervals(self.ctx, kernel, None, 0, C.byref(n)))
+        out = np.zeros((max(n.value, 1), 2))
+        self._check(self.lib.imls_timing_intervals(self.ctx, kernel, _ptr(out), n.value, C.byref(n)))
+        return out[: n.value]
 
     def reset_timing(self):
         self._check(self.lib.imls_reset_timing(self.ctx))
@@ -606,8 +637,18 @@ class LaserOdometry:
     (accumulateTargetCloud, 663-664).  The FIFO lives in HBM (ImlsContext.map_push): only the new
     scan crosses PCIe each frame.  The context (and its RANSAC rand() stream) persists across frames."""
 
-    def __init__(self, params: Optional[_abi.ImlsParams] = None, device: int = 0, pose_file: Optional[str] = None):
+    def __init__(self, params: Optional[_abi.ImlsParams] = None, device: int = 0, pose_file: Optional[str] = None,
+                 output_dir: Optional[str] = None):
         self.ctx = ImlsContext(params, device)
+        # output_dir (opt-in): the reference's per-iteration outputs (laser_odometry.cpp:621-625) —
+        # matched_points/<ts>_<i>.txt and imls_iter_results.txt under it, from the device trace and
+        # the captured correspondences (the subdirectory is created here; the reference needs it
+        # pre-created, config.json:173-176)
+        self.output_dir = output_dir
+        if output_dir:
+            import os
+            os.makedirs(os.path.join(output_dir, "matched_points"), exist_ok=True)
+            self.ctx.capture_correspondences(True)
         self.prev_pose = np.eye(4)
         self.frame_count = 0
         self.pose_file = pose_file
@@ -633,6 +674,8 @@ class LaserOdometry:
             else:
                 self.ctx.set_source(flat_cloud)
                 result = self.ctx.register_frame()
+                if self.output_dir:
+                    self._save_iterations(result, timestamp)
             now = chain_pose(self.prev_pose, result["pose"])
             self.prev_pose = now
             self.poses.append((timestamp, now))
@@ -642,6 +685,17 @@ class LaserOdometry:
         self.ctx.map_push(filtered_cloud)
         self.frame_count += 1
         return result
+
+    def _save_iterations(self, result, timestamp: str):
+        """laser_odometry.cpp:621-625, for every iteration whose solve succeeded (the reference writes
+        after the solver's flag check, before the convergence test): the correspondences the solver
+        got (in_cloud_vec, ref_cloud_vec) and rPose after `rPose = Δ·rPose`."""
+        import os
+        for i in range(result["iters"]):
+            x, y, _, _ = self.ctx.captured(i)
+            saveMatchedPointsToFile(x, y, os.path.join(self.output_dir, "matched_points", f"{timestamp}_{i}.txt"))
+            savePoseToFile(np.array(result["trace"][i].pose).reshape(4, 4),
+                           os.path.join(self.output_dir, "imls_iter_results.txt"), timestamp)
 
 
 def _quat_xyzw(R) -> tuple:

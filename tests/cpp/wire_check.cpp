@@ -72,5 +72,17 @@ int main() {
     PointCloud2 empty;
     DPCloud de;
     std::printf("dp empty=%d\n", (int)dp_from_msg(empty, &de));
+    // malformed messages are rejected, never read out of bounds
+    PointCloud2 shortm = m;
+    shortm.data.resize(shortm.data.size() - 1);
+    PointCloud2 badoff = m;
+    badoff.fields[0].offset = badoff.point_step - 2;
+    PointCloud2 dshort = d;
+    dshort.data.resize(d.point_step * (n - 1));
+    PointCloud2 doff = d;
+    doff.fields[11].offset = doff.point_step;
+    std::printf("malformed xyzinormal_short=%d xyzinormal_offset=%d dp_short=%d dp_offset=%d\n",
+                (int)xyzinormal_from_msg(shortm, back.data()), (int)xyzinormal_from_msg(badoff, back.data()),
+                (int)dp_from_msg(dshort, &de), (int)dp_from_msg(doff, &de));
     return 0;
 }

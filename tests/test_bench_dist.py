@@ -49,8 +49,9 @@ def _worker(rank, world, port, steps, q):
         return [(res["pose"] @ marker(rank, k), res["iters"], res["status"])]
 
     elapsed, per, out = bench.timed_steps(step, steps, world, dev)
-    allp, traj = bench.exchange_poses([o[0] for o in out], world)
-    q.put((rank, elapsed, sum(per), allp, traj))
+    # this rank's units form one sequence (seq 0 locally), in step order
+    recs, trajs = bench.exchange_poses([(0, k, o[0]) for k, o in enumerate(out)], world, rank)
+    q.put((rank, elapsed, sum(per), recs, {s: (o.tolist(), t) for s, (o, t) in trajs.items()}))
     dist.destroy_process_group()
 
 
@@ -70,15 +71,21 @@ def test_bench_dist_path_gloo_world2():
     from planetary_lidar_odometry_amd import config
     g = dict(np.load(ROOT / "tests" / "golden" / "vlp16_pair.npz"))
     base = oc.register_frame(g["src"], g["tgt"], config.bench_params(2))["pose"]
-    want = np.array([base @ marker(r, k) for r in range(world) for k in range(steps)])   # unit order: rank-major
-    chained = []
-    T = np.eye(4)
-    for d in want:
-        T = T @ d
-        chained.append(T)
+    want = np.array([base @ marker(r, k) for r in range(world) for k in range(steps)])   # rank-major records
     elapsed = [t[1] for t in res]
     assert elapsed[0] == elapsed[1]                          # max over ranks, identical on every rank
     assert all(elapsed[0] >= t[2] for t in res)              # ≥ each rank's own time in its steps
-    for _, _, _, allp, traj in res:
-        assert np.array_equal(allp, want)
-        assert np.allclose(traj, np.array(chained), rtol=0, atol=1e-12)
+    for _, _, _, (seq, order, poses), trajs in res:
+        assert np.array_equal(poses, want)
+        assert list(seq) == [r << 20 for r in range(world) for _ in range(steps)]
+        assert list(order) == [k for _ in range(world) for k in range(steps)]
+        # every rank's sequence chained on its own (laser_odometry.cpp:652-655 per sequence)
+        assert sorted(trajs) == [r << 20 for r in range(world)]
+        for r in range(world):
+            orders, traj = trajs[r << 20]
+            T, chained = np.eye(4), []
+            for k in range(steps):
+                T = T @ want[r * steps + k]
+                chained.append(T)
+            assert orders == list(range(steps))
+            assert np.array_equal(traj, np.array(chained))

@@ -41,3 +41,24 @@ def test_batch_error_names_the_pair(stream_pairs):
             b.register(bad)
         poses, _, _ = b.register(stream_pairs[:2])          # the batch is usable afterwards
         assert np.all(np.isfinite(poses))
+
+
+def test_batch_ransac_independent_of_streams(stream_pairs):
+    """The shipped RANSAC → DRPM solver draws from each context's rand() stream; imls_register_batch
+    restarts it from params.ransac_seed before every pair, so a pair's result is the same whatever
+    `streams` is and whatever its context registered before — equal to a fresh context's
+    register_frame (laser_odometry.cpp:489: a fresh matcher per frame)."""
+    p = config.params_from_config(config.load())          # RANSAC → DRPM
+    p.iterations = 6
+    res = []
+    for streams in (1, 2, 4):
+        with imls_icp.ImlsBatch(p, streams=streams) as b:
+            res.append(b.register(stream_pairs))
+    for k, (src, tgt) in enumerate(stream_pairs):
+        with imls_icp.ImlsContext(p) as c:
+            c.set_target(tgt)
+            c.set_source(src)
+            r = c.register_frame()
+        for poses, iters, status in res:
+            assert np.array_equal(r["pose"], poses[k]), k
+            assert (r["iters"], r["status"]) == (iters[k], status[k]), k

@@ -5,6 +5,8 @@ previous scan(s), laser_odometry.cpp:484-485, 116-136), so the contract is stric
 pose, iteration count, status and per-iteration trace must equal — bit for bit — what
 imls_register_frame gives on that frame alone, whatever else shares the launch (other sizes, other
 traversal / solver paths, frames that stop early)."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -229,10 +231,11 @@ def test_two_batches_in_flight(vlp_pairs):
 
 
 def test_deferred_filters_in_large_batches(vlp_pairs):
-    """After a batch of >= 8 frames a context defers its NaN filter to the first use: the next
-    batch filters and builds all its members in one launch sequence (device inputs, a queue-1 map
-    pushed in place, NaN points in the maps); a member registered alone afterwards filters on its
-    own.  Every result equals a fresh single context fed the same clouds from the host."""
+    """With imls_set_defer on, a context defers its NaN filter to the first use: a batch filters and
+    builds all its members in one launch sequence (device inputs, a queue-1 map pushed in place, NaN
+    points in the maps); a member registered alone afterwards filters on its own.  Round 0 runs with
+    the default (filters at once).  Every result equals a fresh single context fed the same clouds
+    from the host."""
     p = _params(5)
     p.max_queue_size = 1
     frames = []
@@ -248,6 +251,7 @@ def test_deferred_filters_in_large_batches(vlp_pairs):
     try:
         for rnd in range(2):                          # round 0: filters at once; round 1: deferred
             for c, (sd, td) in zip(ctxs, dev):
+                c.set_defer(rnd == 1)
                 c.map_push_device(td.ptr, td.n, count=False)
                 c.set_source_device(sd.ptr, sd.n, count=False)
             poses, iters, status, _ = imls_icp.register_frames(ctxs)
@@ -264,6 +268,53 @@ def test_deferred_filters_in_large_batches(vlp_pairs):
             c.close()
         for a, b in dev:
             a.free()
+            b.free()
+
+
+def test_count_less_buffer_lifetime(vlp_pairs):
+    """The lifetime of a count-less device load's buffer depends on imls_set_defer alone (never on
+    what the context did before): defer off — once the context's stream has passed the call the
+    caller may overwrite the buffer; defer on — after the first use has run (the registration's
+    result) the context works on its own filtered copy.  Both with and without an earlier large
+    batch on the context."""
+    p = _params(5)
+    p.max_queue_size = 1
+    q = vlp_pairs[2]
+    src = synth.fps_subsample(q.source, 1300, seed=41)
+    ref = _single(p, [(src, q.target)])[0]
+    hip = _hip()
+    junk = np.full((6, max(src.size, q.target.size)), np.nan, np.float32)
+    ctxs = [imls_icp.ImlsContext(p) for _ in range(9)]
+    bufs = []
+    try:
+        for history in (False, True):
+            if history:                               # a batch of 9 frames on these contexts first
+                for c in ctxs:
+                    c.set_target(q.target)
+                    c.set_source(src)
+                imls_icp.register_frames(ctxs)
+            c = ctxs[0]
+            for defer in (False, True):
+                c.set_defer(defer)
+                sd, td = _DevSoa(hip, synth.soa(src)), _DevSoa(hip, synth.soa(q.target))
+                bufs += [sd, td]
+                c.map_push_device(td.ptr, td.n, count=False)
+                c.set_source_device(sd.ptr, sd.n, count=False)
+                if not defer:
+                    c.synchronize()                   # the stream has passed the loads
+                    for b in (sd, td):
+                        assert hip.hipMemcpy(C.c_void_p(b.ptr), junk.ctypes.data_as(C.c_void_p), 24 * b.n, 1) == 0
+                r = c.register_frame()
+                assert np.array_equal(r["pose"], ref["pose"]) and r["iters"] == ref["iters"], (history, defer)
+                if defer:                             # first use has run: the context keeps its copy
+                    for b in (sd, td):
+                        assert hip.hipMemcpy(C.c_void_p(b.ptr), junk.ctypes.data_as(C.c_void_p), 24 * b.n, 1) == 0
+                    r = c.register_frame()
+                    assert np.array_equal(r["pose"], ref["pose"]), (history, defer)
+    finally:
+        for c in ctxs:
+            c.close()
+        for b in bufs:
             b.free()
 
 

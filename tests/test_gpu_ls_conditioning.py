@@ -110,10 +110,14 @@ CASES = {
 }
 
 
+# fixed target-noise seed per case (reproducible run to run)
+TARGET_SEEDS = {case: 101 + k for k, case in enumerate(CASES)}
+
+
 @pytest.mark.parametrize("case", list(CASES))
 def test_near_degenerate_ls(ctx, case):
     s, nrm = CASES[case]()
-    d = targets(s, nrm, hash(case) % 1000)
+    d = targets(s, nrm, TARGET_SEEDS[case])
     p = config.bench_params(1)
     ok, D = ctx.solve_correspondences(_abi.IMLS_SOLVE_LS, s, d, nrm)
     okr, Dr = oc.solve(_abi.IMLS_SOLVE_LS, s, d, nrm, p)

@@ -180,3 +180,41 @@ def test_fifo_edge_cases(vlp_frames):
         lo.process(filtered, flat)
         r = lo.process(filtered, flat[:0])
         assert r["status"] == _abi.IMLS_FRAME_TOO_FEW and np.array_equal(r["pose"], np.eye(4))
+
+
+def test_per_iteration_outputs(vlp_frames, tmp_path):
+    """LaserOdometry(output_dir=…): the reference's per-iteration files (laser_odometry.cpp:621-625)
+    — matched_points/<ts>_<i>.txt (saveMatchedPointsToFile, saver.cpp:113-133) and
+    imls_iter_results.txt (savePoseToFile of rPose after each successful solve) — one per
+    iteration that solved.  Bytes: identical to the oracle's C++ formatting of the same values;
+    values: the oracle's own correspondences of that iteration (count and x exact, y within 1e-5)
+    and its per-iteration rPose (within 1e-6)."""
+    p = config.params_from_config(config.load())
+    p.solve_method = _abi.IMLS_SOLVE_LS
+    frames = vlp_frames[:4]
+    out = tmp_path / "out"
+    n_lines = 0
+    with imls_icp.LaserOdometry(p, device=0, output_dir=str(out)) as lo:
+        for k, (filtered, flat) in enumerate(frames):
+            ts = f"{1317384506.0 + 0.1 * k:f}"
+            r = lo.process(filtered, flat, timestamp=ts)
+            if k == 0:
+                continue
+            tgt, src = synth.soa(frames[k - 1][0]), synth.soa(flat)   # max_queue_size 1: previous scan
+            iter_lines = (out / "imls_iter_results.txt").read_text().splitlines(keepends=True)
+            assert len(iter_lines) == n_lines + r["iters"]
+            for i in range(r["iters"]):
+                x, y, _, _ = lo.ctx.captured(i)
+                text = (out / "matched_points" / f"{ts}_{i}.txt").read_text()
+                assert text == oc.format_matched(x, y)             # the reference's formatting, bytes
+                corr = oc.register_frame(src, tgt, p, corr_iter=i)["corr"]
+                assert len(x) == len(corr) and np.array_equal(x, corr[:, :3]), (ts, i)
+                assert np.abs(y.astype(np.float64) - corr[:, 3:6]).max() <= 1e-5, (ts, i)
+                pose_i = np.array(r["trace"][i].pose).reshape(4, 4)
+                assert iter_lines[n_lines + i] == oc.format_pose(pose_i, ts)
+            want = oc.register_frame(src, tgt, p)
+            assert want["iters"] == r["iters"]
+            for i in range(r["iters"]):
+                assert np.abs(np.array(r["trace"][i].pose) - np.array(want["trace"][i].pose)).max() < 1e-6
+            assert not (out / "matched_points" / f"{ts}_{r['iters']}.txt").exists()
+            n_lines += r["iters"]

@@ -96,3 +96,13 @@ def test_dp_roundtrip_and_by_position_reads(cpp_out):
 def test_cpp_roundtrips(cpp_out):
     assert cpp_out("xyzinormal roundtrip") == "xyzinormal roundtrip=1"
     assert cpp_out("dp roundtrip") == "dp roundtrip=1"
+
+
+def test_malformed_messages_rejected(cpp_out):
+    """Truncated data or a field past point_step: the C++ readers return false (no out-of-bounds
+    host read), the Python mirror raises."""
+    assert cpp_out("malformed") == "malformed xyzinormal_short=0 xyzinormal_offset=0 dp_short=0 dp_offset=0"
+    m = wire.xyzinormal_to_msg(_records())
+    m.data = m.data[:-1]
+    with pytest.raises(Exception):
+        wire.xyzinormal_from_msg(m)

@@ -11,7 +11,7 @@ pair = synth.make_pairs(1, "hdl64", map_scans=10, scene_seed=0, traj_seed=2000, 
 sd = torch.from_numpy(np.ascontiguousarray(synth.soa(pair.source))).cuda()
 td = torch.from_numpy(np.ascontiguousarray(synth.soa(pair.target))).cuda()
 cols = ["seed_t", "trav_t", "leaves", "inner", "bc_events", "sparse_lv", "bcast_lv", "greedy", "W_inf", "W>1", "Wmax",
-        "sp_lanes", "sp_ins", "bc_ins"]
+        "sp_lanes", "sp_ins", "bc_ins", "seed_steps", "seed_pts"]
 for iters in [int(a) for a in sys.argv[1:]] or [1]:
     c = imls_icp.ImlsContext(config.bench_params(iters), device=0)
     c.set_target_device(td.data_ptr(), pair.target.size)
@@ -21,7 +21,7 @@ for iters in [int(a) for a in sys.argv[1:]] or [1]:
     nw = (c.N + 63) // 64 if hasattr(c, "N") else 1972
     buf = np.zeros((8192, 16), np.uint32)
     n = c.lib.imls_debug_waves(C.c_void_p(buf.ctypes.data), 8192)
-    a = buf[:1972, :14].astype(np.float64)
+    a = buf[:1972, :16].astype(np.float64)
     a[:, 10] = buf[:1972, 10].view(np.float32)
     t = a[:, 0] + a[:, 1]
     print(f"== launch {iters - 1}: waves {n}; total ticks mean {t.mean():.0f} p50 {np.median(t):.0f} p99 {np.percentile(t, 99):.0f} max {t.max():.0f}")
