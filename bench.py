@@ -311,17 +311,18 @@ class PairRunner:
     context's rand() stream from params.ransac_seed (each pair is an independent registration, the
     reference's first frame), so a result depends on its pair alone."""
 
-    def __init__(self, pairs, p, dev, local, fuse=True, groups=2, tensors=False):
+    def __init__(self, pairs, p, dev, local, fuse=True, groups=2, tensors=False, alloc=None):
         self.fuse = fuse
         self.pairs = pairs
         self.ransac = p.solve_method == _abi.IMLS_SOLVE_RANSAC
-        self.s_dev = [soa_tensor(q.source, dev) for q in pairs]
-        self.t_dev = [soa_tensor(q.target, dev) for q in pairs]
+        # device copies (anything with data_ptr()): torch tensors, or `alloc(float32 array)`
+        to_dev = alloc or (lambda a: __import__("torch").from_numpy(np.ascontiguousarray(a)).to(dev).contiguous())
+        self.s_dev = [to_dev(synth.soa(q.source)) for q in pairs]
+        self.t_dev = [to_dev(synth.soa(q.target)) for q in pairs]
         # config E: the targets' tensor-voting input tensors, SoA (6, M) in HBM
         self.ten_dev = None
         if tensors:
-            import torch
-            self.ten_dev = [torch.from_numpy(np.ascontiguousarray(q.meta["tensors"].T)).to(dev).contiguous() for q in pairs]
+            self.ten_dev = [to_dev(np.ascontiguousarray(q.meta["tensors"].T)) for q in pairs]
         self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in pairs]
         self.seed_state = self.ctxs[0].rng_state()        # a fresh context's stream (params.ransac_seed)
         # deferred reads of the count-less device loads: a large batch filters all its members in

@@ -61,6 +61,8 @@ struct KParams {
     int qverlet;              // the same for the wave-per-query traversal (off by default: measured slower)
     int lockstep;             // packet traversal: per-lane candidate masks, then lockstep insertion
     int bcast_lock;           // … also for broadcast leaves: 0 never, 1 first ICP iteration, 2 always
+    int seed_keys;            // packet traversal: the seed keeps keys only and yields a bound cap; the list refills from empty
+    int kl20;                 // list length (K + slack) used for search_number 17..20: 22 (default), 24 or 26
     int xcd;                  // batched projection: frames grouped per XCD round-robin slot (−1 auto: ≥ 16 frames)
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
     int tv;                   // tensor-voting normals (use_tensor_voting && !get_normals, IMLS matcher)
@@ -112,6 +114,27 @@ __device__ __forceinline__ unsigned long long morton48(float x, float y, float z
     const unsigned qy = (unsigned)fminf(fmaxf((y - qp[1]) * sc, 0.f), qmax);
     const unsigned qz = (unsigned)fminf(fmaxf((z - qp[2]) * sc, 0.f), qmax);
     return spread3_16(qx) | (spread3_16(qy) << 1) | (spread3_16(qz) << 2);
+}
+
+// Sum of v over the wave's 64 lanes, valid in lane 63 only: an inclusive scan of each 16-lane row by
+// DPP row shifts (1, 2, 4, 8), then row_bcast:15 and row_bcast:31 carry the row totals into lane 63 —
+// VALU moves only (a __shfl_xor butterfly is 12 ds_bpermute LDS round trips per fp64 sum).  A fixed
+// association: the same bits on every run and in every kernel that uses it.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_add_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(unsigned long long)b, CTRL, ROWS, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)((unsigned long long)b >> 32), CTRL, ROWS, 0xf, true);
+    return v + __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double wave_total(double v) {
+    v = dpp_add_f64<0x111, 0xf>(v);    // row_shr:1
+    v = dpp_add_f64<0x112, 0xf>(v);    // row_shr:2
+    v = dpp_add_f64<0x114, 0xf>(v);    // row_shr:4
+    v = dpp_add_f64<0x118, 0xf>(v);    // row_shr:8  → lane 15 of each row holds its row's sum
+    v = dpp_add_f64<0x142, 0xa>(v);    // row_bcast:15 into rows 1 and 3
+    v = dpp_add_f64<0x143, 0xc>(v);    // row_bcast:31 into rows 2 and 3 → lane 63 holds the total
+    return v;
 }
 
 // Solver scratch living in device memory (one per context).

@@ -108,10 +108,12 @@ __device__ __forceinline__ void insert_top(float (&lk)[KL], int (&lp)[KL], float
 // min(a, b) of non-NaN floats (a plain select: fminf canonicalises both operands first)
 __device__ __forceinline__ float fmin_nn(float a, float b) { return a < b ? a : b; }
 
-__device__ __forceinline__ double wave_sum(double v) {
+// Keys-only sorted insertion (precondition d < lk[KL−1]): one v_med3 per slot.
+template <int KL>
+__device__ __forceinline__ void insert_key(float (&lk)[KL], float d) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    for (int k = KL - 1; k >= 1; --k) lk[k] = __builtin_amdgcn_fmed3f(lk[k - 1], d, lk[k]);
+    lk[0] = fmin_nn(d, lk[0]);
 }
 
 // Gates + ImplicitMLSFunction + projection for one query given its exact neighbour list
@@ -233,19 +235,19 @@ __device__ void block_normeq(const double a[6], double b, double one, double (*r
     for (int r = 0; r < 6; ++r) {
 #pragma unroll
         for (int c = r; c < 6; ++c) {
-            const double v = wave_sum(a[r] * a[c]);
-            if (lane == 0) red[wv][k] = v;
+            const double v = wave_total(a[r] * a[c]);
+            if (lane == 63) red[wv][k] = v;
             ++k;
         }
     }
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-        const double v = wave_sum(a[r] * b);
-        if (lane == 0) red[wv][21 + r] = v;
+        const double v = wave_total(a[r] * b);
+        if (lane == 63) red[wv][21 + r] = v;
     }
     {
-        const double v = wave_sum(one);
-        if (lane == 0) red[wv][27] = v;
+        const double v = wave_total(one);
+        if (lane == 63) red[wv][27] = v;
     }
     __syncthreads();
     if (threadIdx.x < kNormEq) {
@@ -357,6 +359,9 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     for (int j = 0; j < KL; ++j) { lk[j] = kInfF; lp[j] = -1; }
     const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
     float bnd = active ? r2s : -1.0f;
+    // the lane's bound cap: r2s, or (seed_keys) the seed's KL-th key — a bound the final KL-th key
+    // never exceeds (KL seed points lie within it), kept while the list refills from empty
+    float bcap = r2s;
     const int P = t.P, B = t.B, M = t.M;
 #ifdef IMLS_DEBUG_WAVE_TRACE
     const long long dbg_t0 = wall_clock64();
@@ -415,7 +420,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 }
             }
         }
-        bnd = fmin_nn(r2s, lk[KL - 1]);
+        bnd = fmin_nn(bcap, lk[KL - 1]);
     }
     // leaf scan shared by the seed pass and the traversal: the lanes in `want` test every point of
     // leaf `leaf` against their bound; `listed`: the leaf may hold points already in a lane's
@@ -504,7 +509,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                             ++dbg_ins;
 #endif
                             insert_top<KL>(lk, lp, d32, base + j);
-                            bnd = fmin_nn(r2s, lk[KL - 1]);
+                            bnd = fmin_nn(bcap, lk[KL - 1]);
                         }
                     }
 #ifdef IMLS_DEBUG_WAVE_TRACE
@@ -540,7 +545,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                         ++dbg_sparse_ins;
 #endif
                         insert_top<KL>(lk, lp, dj, base + j);
-                        bnd = fmin_nn(r2s, lk[KL - 1]);
+                        bnd = fmin_nn(bcap, lk[KL - 1]);
                     }
                 }
             }
@@ -560,7 +565,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
 #endif
                 if (ins) {
                     insert_top<KL>(lk, lp, d32, base + j);
-                    bnd = fmin_nn(r2s, lk[KL - 1]);
+                    bnd = fmin_nn(bcap, lk[KL - 1]);
                 }
             }
         }
@@ -585,6 +590,10 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         for (int k = threadIdx.x; k < ntab; k += kWaveBlock) skey[k] = t.lkeys[(size_t)k * S];
         __syncthreads();
     }
+    // seed_keys: the seed keeps keys only (med3 insertion, no positions): its KL-th key becomes the
+    // lane's bound cap and the list restarts empty — the traversal, which visits the seed leaves
+    // anyway, inserts the final members (nothing is listed twice, so no listed-mask is needed)
+    const bool seed_keys = kp.seed_keys != 0;
     if (greedy) {
         const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
         int j = 0, jh = ntab - 1;
@@ -617,12 +626,21 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 ++dbg_seed_pts;
 #endif
                 if (p0 + k < pend && d32 <= bnd && d32 < lk[KL - 1]) {
-                    insert_top<KL>(lk, lp, d32, p0 + k);
-                    bnd = fmin_nn(r2s, lk[KL - 1]);
+                    if (seed_keys) {
+                        insert_key<KL>(lk, d32);
+                    } else {
+                        insert_top<KL>(lk, lp, d32, p0 + k);
+                    }
+                    bnd = fmin_nn(bcap, lk[KL - 1]);
                 }
             }
 #pragma unroll
             for (int k = 0; k < kSeedChunk; ++k) qs[k] = nx[k];
+        }
+        if (seed_keys) {
+            bcap = bnd;
+#pragma unroll
+            for (int j = 0; j < KL; ++j) lk[j] = kInfF;
         }
     }
     unsigned n_inner = 0, n_leaf = 0;
@@ -695,7 +713,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         } else {
             ++n_leaf;
             const int leaf = node - P;
-            scan_leaf(leaf, em, use_prev || gmask);
+            scan_leaf(leaf, em, use_prev || (gmask && !seed_keys));
         }
         // pop: the stacked node's box is in LDS — re-check it against the shrunken lane bounds
         node = 0;
@@ -1477,6 +1495,8 @@ void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     const int K = kp.K;
     if (K <= 8) launch_wave_batch<12>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else if (K <= 16) launch_wave_batch<20>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
+    else if (K <= 20 && kp.kl20 == 24) launch_wave_batch<24>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
+    else if (K <= 20 && kp.kl20 == 26) launch_wave_batch<26>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else if (K <= 20) launch_wave_batch<22>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else launch_wave_batch<36>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     // exact fallback for uncertified queries: every frame's kFallbackBlocks slabs are written, by
@@ -1515,6 +1535,8 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
     else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     // K ≤ 20 (the shipped 20): two slack entries certify every query on config B (KL 21 left a few
     // uncertified → the slow exact fallback, −30 %; KL 22 vs 24 measured +6.7 % pairs/s, 4 in flight)
+    else if (K <= 20 && kp.kl20 == 24) launch_wave<24>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
+    else if (K <= 20 && kp.kl20 == 26) launch_wave<26>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else if (K <= 20) launch_wave<22>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     // exact fallback for uncertified queries (usually none; the launch exits at once then)

@@ -207,6 +207,30 @@ __device__ void bitonic(unsigned long long* k, unsigned* r, int n) {
         }
 }
 
+// The same ascending (key, row) order for n ≤ kRankSortMax pairs by counting ranks: each thread
+// ranks its pairs against all n (LDS broadcast reads) and scatters them to their rank in the upper
+// half of the arrays — two barriers instead of bitonic's log²(n)/2 (a trimmed-LS boundary bin holds
+// ~10-30 candidates).  Keys are distinct as (key, row) pairs.  The sorted pairs are left at k/r[0, n).
+constexpr int kRankSortMax = 512;
+__device__ void rank_sort(unsigned long long* k, unsigned* r, int n) {
+    unsigned long long* sk = k + kRankSortMax;
+    unsigned* sr = r + kRankSortMax;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const unsigned long long ki = k[i];
+        const unsigned ri = r[i];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) rank += (k[j] < ki || (k[j] == ki && r[j] < ri)) ? 1 : 0;
+        sk[rank] = ki;
+        sr[rank] = ri;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        k[i] = sk[i];
+        r[i] = sr[i];
+    }
+    __syncthreads();
+}
+
 // Exact fallback when a boundary bin overflows kCandCap: the (key, row) at global rank `target`
 // by bisection over the key bits then over rows (slow; only for massively tied residuals).
 __device__ void rank_select(const double* keys, int N, long long target, unsigned long long* kout, unsigned* rout,
@@ -264,6 +288,13 @@ __device__ __forceinline__ bool pair_le(unsigned long long ka, unsigned ra, unsi
     return ka < kb || (ka == kb && ra <= rb);
 }
 
+#ifdef IMLS_DEBUG_WAVE_TRACE
+__device__ unsigned long long g_dbg_final[4];
+__device__ unsigned long long g_dbg_fstamp[8];   // k_solve_final phase cycles (thread 0), debug build
+#define FSTAMP(k) do { if (threadIdx.x == 0) { const long long _n = wall_clock64(); g_dbg_fstamp[k] += _n - fst; fst = _n; } } while (0)
+#else
+#define FSTAMP(k) do { } while (0)
+#endif
 // The trimmed second solve (solver.cpp:124-166) by one block of NT threads, after k_collect:
 // boundary candidates sorted by (|r| bits, row), exact ranks kept, interior partials added,
 // solve6, Δ, pose update.  LDS: ck/cr [kCandCap], red [(NT/64)·28], out [28], shc, selk/selr [2].
@@ -272,6 +303,9 @@ __device__ void final_block(const Rows& rows, int N, SolveState st, imls_iter_tr
                             const double* __restrict__ partial2, int nparts, const KParams& kp, int update_pose,
                             unsigned long long* ck, unsigned* cr, double* red, double* out, unsigned long long& shc,
                             unsigned long long* selk, unsigned* selr) {
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    long long fst = wall_clock64();
+#endif
     const int blo = st.sel[0], bhi = st.sel[1];
     const long long clo = st.sel[2], chi = st.sel[3], lo = st.sel[4], hi = st.sel[5];
     const unsigned n_lo = st.cand_count[0], n_hi = st.cand_count[1];
@@ -287,6 +321,14 @@ __device__ void final_block(const Rows& rows, int N, SolveState st, imls_iter_tr
         accA[27] += 1.0;
     };
     const bool overflow = n_lo > (unsigned)kCandCap || n_hi > (unsigned)kCandCap;
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    if (threadIdx.x == 0) {   // boundary-bin candidate counts (debug build): solves, Σ n_lo, Σ n_hi, max
+        atomicAdd(&g_dbg_final[0], 1ull);
+        atomicAdd(&g_dbg_final[1], (unsigned long long)n_lo);
+        atomicAdd(&g_dbg_final[2], (unsigned long long)n_hi);
+        atomicMax(&g_dbg_final[3], (unsigned long long)(n_lo > n_hi ? n_lo : n_hi));
+    }
+#endif
     if (!overflow) {
         for (int which = 0; which < 2; ++which) {
             const unsigned n = which ? n_hi : n_lo;
@@ -301,13 +343,17 @@ __device__ void final_block(const Rows& rows, int N, SolveState st, imls_iter_tr
                 cr[i] = i < (int)n ? gr[i] : ~0u;
             }
             __syncthreads();
-            bitonic(ck, cr, np);
+            FSTAMP(0);
+            if ((int)n <= kRankSortMax) rank_sort(ck, cr, (int)n);
+            else bitonic(ck, cr, np);
+            FSTAMP(1);
             const long long base = which ? chi : clo;
             for (int i = threadIdx.x; i < (int)n; i += NT) {
                 const long long rank = base + i;
                 if (rank >= lo && rank <= hi) add_row(cr[i]);
             }
             __syncthreads();
+            FSTAMP(2);
         }
     } else {
         if (threadIdx.x == 0) shc = 0;
@@ -328,11 +374,15 @@ __device__ void final_block(const Rows& rows, int N, SolveState st, imls_iter_tr
 #pragma unroll
         for (int k = 0; k < kNormEq; ++k) accA[k] += partial2[(size_t)q * kNormEq + k];
     block_sum28<NT>(accA, red, out);
+    FSTAMP(3);
     if (threadIdx.x != 0) return;
     double x[6], D[16];
     solve6(out, x);
+    FSTAMP(4);
     delta_from_x(x, D);
+    FSTAMP(5);
     finish_iteration(st, tr, D, (double)st.sel[6], out[27], update_pose, kp);
+    FSTAMP(6);
 }
 
 // Reduce rows strictly between the boundary bins; collect the boundary rows.
@@ -375,8 +425,8 @@ __device__ __forceinline__ void collect_body(const Rows& rows, int N, const Solv
     // block reduction of the 28 partial sums
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int k = 0; k < kNormEq; ++k) {
-        const double v = wave_sum(acc[k]);
-        if (lane == 0) red[wv * kNormEq + k] = v;
+        const double v = wave_total(acc[k]);
+        if (lane == 63) red[wv * kNormEq + k] = v;
     }
     __syncthreads();
     if (threadIdx.x < kNormEq) {
@@ -704,6 +754,11 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
 #ifdef IMLS_DEBUG_WAVE_TRACE
 extern "C" int imls_debug_solve(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(imlsgpu::g_dbg_solve), 64) == hipSuccess ? 0 : -1;
+}
+extern "C" int imls_debug_final(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(imlsgpu::g_dbg_final), 32) == hipSuccess &&
+                   hipMemcpyFromSymbol(out + 4, HIP_SYMBOL(imlsgpu::g_dbg_fstamp), 64) == hipSuccess
+               ? 0 : -1;
 }
 #endif
 

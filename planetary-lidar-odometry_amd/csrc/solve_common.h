@@ -76,18 +76,18 @@ __device__ void block_normeq(const double a[6], double b, double cnt, double* re
     for (int r = 0; r < 6; ++r)
 #pragma unroll
         for (int c = r; c < 6; ++c) {
-            const double v = wave_sum(a[r] * a[c]);
-            if (lane == 0) red[wv * kNormEq + k] = v;
+            const double v = wave_total(a[r] * a[c]);
+            if (lane == 63) red[wv * kNormEq + k] = v;
             ++k;
         }
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-        const double v = wave_sum(a[r] * b);
-        if (lane == 0) red[wv * kNormEq + 21 + r] = v;
+        const double v = wave_total(a[r] * b);
+        if (lane == 63) red[wv * kNormEq + 21 + r] = v;
     }
     {
-        const double v = wave_sum(cnt);
-        if (lane == 0) red[wv * kNormEq + 27] = v;
+        const double v = wave_total(cnt);
+        if (lane == 63) red[wv * kNormEq + 27] = v;
     }
     __syncthreads();
     if (threadIdx.x < kNormEq) {
@@ -104,8 +104,8 @@ __device__ void block_sum28(const double (&v)[kNormEq], double* red, double* out
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < kNormEq; ++k) {
-        const double s = wave_sum(v[k]);
-        if (lane == 0) red[wv * kNormEq + k] = s;
+        const double s = wave_total(v[k]);
+        if (lane == 63) red[wv * kNormEq + k] = s;
     }
     __syncthreads();
     if (threadIdx.x < kNormEq) {

@@ -49,10 +49,14 @@ def oracle_results(pairs, bench_mod):
 
 @pytest.mark.parametrize("groups", [2, 1], ids=["one_pair_per_sequence", "two_pairs_one_sequence"])
 def test_bench_pipeline_matches_single_and_oracle(bench_mod, pairs, oracle_results, groups):
-    import torch
-    dev = torch.device("cuda", 0)
+    import gpu_mem                                     # device copies on the product's HIP runtime
     p = bench_mod.solver_params("LS", 20)
-    runner = bench_mod.PairRunner(pairs, p, dev, 0, fuse=True, groups=groups)
+    bufs = []
+
+    def alloc(a):
+        bufs.append(gpu_mem.DevSoa(a))
+        return bufs[-1]
+    runner = bench_mod.PairRunner(pairs, p, None, 0, fuse=True, groups=groups, alloc=alloc)
     try:
         res = []
         for _ in range(2):                              # two pipelined steps, as the timed region runs them
@@ -71,3 +75,5 @@ def test_bench_pipeline_matches_single_and_oracle(bench_mod, pairs, oracle_resul
             assert np.abs(pose - want["pose"]).max() < POSE_TOL, np.abs(pose - want["pose"]).max()
     finally:
         runner.close()
+        for b in bufs:
+            b.free()

@@ -319,31 +319,21 @@ def test_count_less_buffer_lifetime(vlp_pairs):
 
 
 def _hip():
-    """The HIP runtime the product library runs on (device buffers for the *_device entry points;
-    no second runtime in the process)."""
-    import ctypes
-    h = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
-    h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
-    h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    h.hipFree.argtypes = [ctypes.c_void_p]
-    return h
+    """The HIP runtime the product library runs on (tests/gpu_mem.py)."""
+    import gpu_mem
+    return gpu_mem.product_hip()
 
 
 class _DevSoa:
-    """A (6, n) float32 SoA cloud copied to device memory."""
+    """A (6, n) float32 SoA cloud copied to device memory (tests/gpu_mem.py)."""
 
     def __init__(self, hip, a):
-        import ctypes
-        a = np.ascontiguousarray(a, np.float32)
-        self.hip, self.n = hip, a.shape[1]
-        p = ctypes.c_void_p()
-        assert hip.hipMalloc(ctypes.byref(p), a.nbytes) == 0
-        assert hip.hipMemcpy(p, a.ctypes.data_as(ctypes.c_void_p), a.nbytes, 1) == 0   # host → device
-        self.ptr = p.value
+        import gpu_mem
+        self._d = gpu_mem.DevSoa(a, hip)
+        self.hip, self.n, self.ptr = hip, self._d.n, self._d.ptr
 
     def free(self):
-        import ctypes
-        self.hip.hipFree(ctypes.c_void_p(self.ptr))
+        self._d.free()
 
 
 @pytest.mark.parametrize("packet,iters", [(16, 20), (32, 3)])

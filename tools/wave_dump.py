@@ -29,3 +29,10 @@ for iters in [int(a) for a in sys.argv[1:]] or [1]:
     for i in np.argsort(-t)[:10]:
         print(f"   w{i:5d}", {k: (round(float(v), 3) if k == 'Wmax' else int(v)) for k, v in zip(cols, a[i])})
     c.close()
+fin = np.zeros(12, np.uint64)
+lib = imls_icp.ImlsContext(config.bench_params(1), device=0).lib
+if lib.imls_debug_final(C.c_void_p(fin.ctypes.data)) == 0 and fin[0]:
+    print(f"== trimmed-LS boundary bins over {int(fin[0])} solves: mean n_lo {fin[1] / fin[0]:.1f}, "
+          f"mean n_hi {fin[2] / fin[0]:.1f}, max {int(fin[3])}")
+    ph = ["load", "bitonic", "add_rows", "partials+sum", "solve6", "delta", "finish"]
+    print("   k_solve_final phases, clock ticks per solve:", {k: round(float(fin[4 + i]) / float(fin[0]), 0) for i, k in enumerate(ph)})
