@@ -229,6 +229,8 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_SEED_KEYS")) k.seed_keys = std::atoi(w);
     k.kl20 = 22;
     if (const char* w = std::getenv("IMLS_KL")) k.kl20 = std::atoi(w);
+    k.lazy_listed = 1;
+    if (const char* w = std::getenv("IMLS_LAZY_LISTED")) k.lazy_listed = std::atoi(w);
     // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
     // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)
     k.tv = (p.use_tensor_voting && !p.get_normals && p.matching_method == IMLS_MATCH_IMLS) ? 1 : 0;

@@ -432,26 +432,42 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     unsigned dbg_sparse = 0, dbg_bcast = 0, dbg_sparse_lanes = 0, dbg_sparse_ins = 0;
     unsigned dbg_seed_steps = 0, dbg_seed_pts = 0;   // seed points where any lane inserted / seed points scanned
 #endif
-    auto scan_leaf = [&](int leaf, unsigned long long want, bool listed) {
+    // mine: lane k's point k of the leaf (loaded by the caller; zero past the leaf's count)
+    auto scan_leaf = [&](int leaf, unsigned long long want, bool listed, float4 mine) {
         const int base = leaf * B;
         const int cnt = min(B, M - base);
-        float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (lane < cnt) mine = t.mpt[base + lane];
         // points of this leaf already in the lane's list, as a bit mask: one lockstep pass over
         // the list instead of a divergent membership test per point
         unsigned long long inl = 0ull;
-        if (listed) {
+        auto listed_mask = [&]() {
 #pragma unroll
             for (int k = 0; k < KL; ++k) {
                 const unsigned rel = (unsigned)(lp[k] - base);
                 inl |= rel < 64u ? (1ull << rel) : 0ull;
             }
-        }
+        };
 #ifdef IMLS_DEBUG_WAVE_TRACE
         if (__popcll(want) <= sparse_thr) { ++dbg_sparse; dbg_sparse_lanes += __popcll(want); } else { ++dbg_bcast; }
 #endif
         const bool sparse = __popcll(want) <= sparse_thr;
-        if (LOCKSTEP && (sparse || bcast_lock)) {
+        // lockstep paths: only the NUMBER of listed points in the leaf per lane up front (3 ops per
+        // list slot instead of 7).  Every listed point of the leaf is a candidate of its lane (its
+        // key, recomputed here bit for bit, is ≤ the lane's bound: bnd = min(cap, KL-th key) and
+        // listed keys are ≤ both), so a lane with exactly that many candidates has no new one; the
+        // mask itself is built only when some lane has more (a leaf with new points).
+        const bool lock_path = LOCKSTEP && (sparse || bcast_lock);
+        int nin = 0;
+        bool have_inl = !listed;
+        if (listed) {
+            if (lock_path && kp.lazy_listed) {
+#pragma unroll
+                for (int k = 0; k < KL; ++k) nin += (unsigned)(lp[k] - base) < 64u ? 1 : 0;
+            } else {
+                listed_mask();
+                have_inl = true;
+            }
+        }
+        if (lock_path) {
             // few lanes want this leaf (spread-out queries in a dense region): per wanting lane,
             // all leaf points are measured at once (one per lane) and the ones under that lane's
             // bound and not yet listed become its candidate mask; then the lanes insert their own
@@ -473,6 +489,11 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                     const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
                     cm |= (wants && d32 <= bnd) ? (1ull << j) : 0ull;
                 }
+                if (!have_inl) {
+                    const bool more = __popcll(cm) > nin;
+                    if (__ballot(more)) listed_mask();
+                    cm = more ? cm : 0ull;
+                }
                 cm &= ~inl;
             } else {
                 unsigned long long m = want;
@@ -483,12 +504,24 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                     const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[1]), q));
                     const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[2]), q));
                     const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bnd), q));
-                    const unsigned long long inq =
-                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(inl >> 32), q) << 32) |
-                        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)inl, q);
                     const float ex = mine.x - qx, ey = mine.y - qy, ez = mine.z - qz;
                     const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                    const unsigned long long pm = __ballot(lane < cnt && d32 <= qb) & ~inq;
+                    unsigned long long pm = __ballot(lane < cnt && d32 <= qb);
+                    if (!have_inl) {
+                        const int nq = __builtin_amdgcn_readlane(nin, q);
+                        if (__popcll(pm) > nq) {
+                            listed_mask();
+                            have_inl = true;
+                        } else {
+                            pm = 0ull;
+                        }
+                    }
+                    if (pm) {
+                        const unsigned long long inq =
+                            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(inl >> 32), q) << 32) |
+                            (unsigned)__builtin_amdgcn_readlane((int)(unsigned)inl, q);
+                        pm &= ~inq;
+                    }
                     if (lane == q) cm = pm;
                 }
             }
@@ -713,7 +746,9 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         } else {
             ++n_leaf;
             const int leaf = node - P;
-            scan_leaf(leaf, em, use_prev || (gmask && !seed_keys));
+            float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (lane < min(B, M - leaf * B)) mine = t.mpt[leaf * B + lane];
+            scan_leaf(leaf, em, use_prev || (gmask && !seed_keys), mine);
         }
         // pop: the stacked node's box is in LDS — re-check it against the shrunken lane bounds
         node = 0;
