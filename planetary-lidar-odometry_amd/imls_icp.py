@@ -387,14 +387,41 @@ def register_frames_async(contexts):
     lead._check(lead.lib.imls_register_frames_async(_ctx_array(contexts), len(contexts)))
 
 
+class TraceView:
+    """One frame's iteration records inside a batch's result array, read on access: a batch of
+    1024 frames × 20 iterations would otherwise build 20k ctypes records in Python before the
+    caller can enqueue its next batch (measured: ~16 ms of GPU idle per stream step)."""
+
+    __slots__ = ("_arr", "_off", "_n")
+
+    def __init__(self, arr, off: int, n: int):
+        self._arr, self._off, self._n = arr, off, n
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, j):
+        if isinstance(j, slice):
+            return [self[k] for k in range(*j.indices(self._n))]
+        if j < 0:
+            j += self._n
+        if not 0 <= j < self._n:
+            raise IndexError(j)
+        return self._arr[self._off + j]
+
+    def __iter__(self):
+        return (self._arr[self._off + j] for j in range(self._n))
+
+
 def register_frames_result(contexts):
-    """(poses (n,4,4), iterations (n,), statuses (n,), traces [n lists of ImlsIterTrace])."""
+    """(poses (n,4,4), iterations (n,), statuses (n,), traces [n sequences of ImlsIterTrace]).  The
+    per-frame trace sequences are views into the batch's result array (records built on access)."""
     lead, n = contexts[0], len(contexts)
     it = max(lead.params.iterations, 1)
     poses = np.zeros((n, 16)); iters = np.zeros(n, np.int32); st = np.zeros(n, np.int32)
     tr = (_abi.ImlsIterTrace * (it * n))()
     lead._check(lead.lib.imls_register_frames_result(lead.ctx, _ptr(poses), _ptr(iters), _ptr(st), tr))
-    traces = [[tr[k * it + j] for j in range(int(iters[k]))] for k in range(n)]
+    traces = [TraceView(tr, k * it, int(iters[k])) for k in range(n)]
     for c, t in zip(contexts, traces):
         c.last_trace = t
     return poses.reshape(n, 4, 4), iters, st, traces

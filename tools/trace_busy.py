@@ -34,3 +34,17 @@ for s, e, n in iv:
     cat[n][1] += 1
 for n, (t, c) in sorted(cat.items(), key=lambda x: -x[1][0])[:25]:
     print(f"  {n:32s} {t/1e6:9.2f} ms  {c:6d} calls  {t/c/1e3:8.1f} us")
+# the largest idle gaps between consecutive busy intervals, with the kernels on either side
+if len(sys.argv) > 3:
+    ngap = int(sys.argv[3])
+    gaps, cur_e, last = [], None, None
+    for s, e, n in iv:
+        if cur_e is not None and s > cur_e:
+            gaps.append((s - cur_e, last, n, cur_e))
+        if cur_e is None or e > cur_e:
+            cur_e, last = e, n
+    short = lambda n: re.sub(r"^void ", "", re.sub(r"imlsgpu::\(anonymous namespace\)::", "", n)).split("(")[0][:40]
+    tot = sum(g[0] for g in gaps)
+    print(f"idle gaps: {len(gaps)}, total {tot/1e6:.2f} ms; largest:")
+    for g, a, b, t in sorted(gaps, reverse=True)[:ngap]:
+        print(f"  {g/1e6:8.3f} ms at +{(t - iv[0][0])/1e6:9.2f} ms  after {short(a):40s} before {short(b)}")
