@@ -8,6 +8,11 @@ O=gpurun_out/${OUT:-ab}
 mkdir -p $O
 export TMPDIR=/tmp
 V=planetary-lidar-odometry_amd/csrc/variant/libimls_gpu.so
+if [ "${PRODUCT_TESTS:-0}" = 1 ]; then
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_verlet.py tests/test_gpu_plane_icp.py \
+      tests/test_gpu_tv.py tests/test_gpu_bench_path.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/product_tests.log 2>&1
+  rc=$?; echo "product tests rc=$rc"; tail -2 $O/product_tests.log; [ $rc -eq 0 ] || exit $rc
+fi
 if [ "${VARIANT_TESTS:-0}" = 1 ]; then
   IMLS_LIB_PATH=$V timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_verlet.py tests/test_gpu_plane_icp.py \
       tests/test_gpu_tv.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
@@ -21,6 +26,10 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   show $O/base_$r.json "base $r"
   IMLS_LIB_PATH=$V timeout -k 10 300 python3 bench.py --no-cpu --steps 8 --latency-pairs 10 ${BENCH_ARGS:-} > $O/var_$r.json 2> $O/var_$r.err || { tail -5 $O/var_$r.err; exit 1; }
   show $O/var_$r.json "variant $r"
+done
+for k in ${KNOBS:-}; do   # product library with NAME=VALUE knobs (several joined by '+')
+  timeout -k 10 300 env ${k//+/ } python3 bench.py --no-cpu --steps 8 --latency-pairs 10 ${BENCH_ARGS:-} > $O/knob_$k.json 2> $O/knob_$k.err || { tail -5 $O/knob_$k.err; exit 1; }
+  show $O/knob_$k.json "$k"
 done
 if [ "${SKIP_DUMP:-0}" != 1 ]; then
   IMLS_LIB_PATH=planetary-lidar-odometry_amd/csrc/debug/libimls_gpu.so timeout -k 10 300 python3 tools/wave_dump.py 1 2 3 6 > $O/wave_dump.txt 2> $O/wave_dump.err
