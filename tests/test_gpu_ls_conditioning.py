@@ -127,7 +127,10 @@ def test_near_degenerate_ls(ctx, case):
     err_ora = np.abs(x_from_delta(Dr) - xe).max()
     diff = np.abs(D - Dr).max()
     print(f"{case}: |gpu-oracle| {diff:.3e}  gpu err {err_gpu:.3e}  oracle err {err_ora:.3e}")
-    assert diff < POSE_TOL or err_gpu <= 10 * err_ora + 1e-12, (diff, err_gpu, err_ora)
+    # both bounds hold together: Δ equal to the oracle's, and the GPU's distance to the exact trimmed
+    # solution no worse than twice the oracle's (measured on MI355X, profiles/r03_experiments: at
+    # most 1.23× — corridor tilt 1e-5 — with |gpu − oracle| ≤ 9.1e-13 over every case)
+    assert diff < POSE_TOL and err_gpu <= 2 * err_ora + 1e-14, (diff, err_gpu, err_ora)
 
 
 def test_exactly_degenerate_corridor(ctx):

@@ -27,9 +27,11 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   IMLS_LIB_PATH=$V timeout -k 10 300 python3 bench.py --no-cpu --steps 8 --latency-pairs 10 ${BENCH_ARGS:-} > $O/var_$r.json 2> $O/var_$r.err || { tail -5 $O/var_$r.err; exit 1; }
   show $O/var_$r.json "variant $r"
 done
+kn=0
 for k in ${KNOBS:-}; do   # product library with NAME=VALUE knobs (several joined by '+')
-  timeout -k 10 300 env ${k//+/ } python3 bench.py --no-cpu --steps 8 --latency-pairs 10 ${BENCH_ARGS:-} > $O/knob_$k.json 2> $O/knob_$k.err || { tail -5 $O/knob_$k.err; exit 1; }
-  show $O/knob_$k.json "$k"
+  f=$O/knob_$(echo "$k" | tr '/' '_')_$((++kn))
+  timeout -k 10 300 env ${k//+/ } python3 bench.py --no-cpu --steps 8 --latency-pairs 10 ${BENCH_ARGS:-} > $f.json 2> $f.err || { tail -5 $f.err; exit 1; }
+  show $f.json "$k"
 done
 if [ "${SKIP_DUMP:-0}" != 1 ]; then
   IMLS_LIB_PATH=planetary-lidar-odometry_amd/csrc/debug/libimls_gpu.so timeout -k 10 300 python3 tools/wave_dump.py 1 2 3 6 > $O/wave_dump.txt 2> $O/wave_dump.err
