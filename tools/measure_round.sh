@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 measurement set (outputs under gpurun_out/${OUT:-final}/): full GPU suite + smoke, the
+# Round measurement set (outputs under gpurun_out/${OUT:-final}/): full GPU suite + smoke, the
 # headline bench (driver command, CPU baselines), the stream / A / shipped-solver legs, a kernel
 # trace of the driver command and of a one-pair-in-flight run (the roofline probe's regime), and
 # the PMC traffic passes (FETCH_SIZE, WRITE_SIZE: separate runs, --kernel-trace only).
@@ -23,6 +23,9 @@ step bench_A_ransac 400 python3 bench.py --workload A --solver RANSAC_DRPM
 step bench_E 500 python3 bench.py --workload E
 step kt_stream 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_stream -o run -- python3 bench.py --workload stream --no-cpu --steps 4 --warmup 1
 step kt_driver 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_driver -o run -- python3 bench.py --no-cpu
+# the roofline fraction recomputed from the driver command's own kernel trace (tools/trace_frac.py)
+f=$(find $O/kt_driver -name '*kernel_trace.csv' | head -1)
+python3 tools/trace_frac.py $f $O/kt_driver.out > $O/kt_driver_frac.json && cat $O/kt_driver_frac.json
 step kt_single 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_single -o run -- python3 bench.py --no-cpu --inflight 1 --no-fuse --steps 5 --warmup 1
 for c in FETCH_SIZE WRITE_SIZE; do
   step pmc_$c 300 rocprofv3 --kernel-trace --kernel-include-regex 'k_knn_wave|k_finish' --output-format csv \
