@@ -12,10 +12,15 @@ step() {  # name, timeout, command...
   timeout -k 10 $to "$@" > $O/$name.out 2> $O/$name.err
   local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/$name.err; exit $rc; }
 }
+# PART=1: tests, smoke, the B and stream lines; PART=2: everything else (two gpurun calls); default both
+P1=1; P2=1; [ "${PART:-0}" = 1 ] && P2=0; [ "${PART:-0}" = 2 ] && P1=0
+if [ $P1 = 1 ]; then
 [ "${SKIP_TESTS:-0}" = 1 ] || step gpu_tests 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
 [ "${SKIP_TESTS:-0}" = 1 ] || step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step bench_B 600 python3 bench.py
-step bench_stream 300 python3 bench.py --workload stream --no-cpu
+step bench_stream 300 python3 bench.py --workload stream
+fi
+if [ $P2 = 1 ]; then
 step bench_stream_host 300 python3 bench.py --workload stream --no-cpu --host-inputs
 step bench_stream_ransac 400 python3 bench.py --workload stream --no-cpu --solver RANSAC_DRPM
 step bench_A 400 python3 bench.py --workload A
@@ -34,4 +39,5 @@ done
 # the driver's N>1 launch shape at N=1 (torch.distributed.run, RCCL init, max-over-ranks timing)
 step dist1 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
     --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu
+fi
 echo done
