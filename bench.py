@@ -273,6 +273,7 @@ class Pipeline:
         self.offs = bounds[:g]
         self.inflight = [False] * len(self.halves)
         self.t_wait = self.t_launch = 0.0   # host time in result waits / in register_frames_async
+        self.t_prep = self.t_tag = 0.0      # host time in the parts' input loads / in tagging the results
 
     def _order(self, h):
         """Part h's contexts in the order handed to register_frames_async: rotated by h, so that the
@@ -299,8 +300,14 @@ class Pipeline:
             # the part's next inputs are enqueued while its previous batch still runs (each
             # context's stream is ordered after the batch: set_target / map_push / set_source
             # touch nothing the batch reads before it ends), then its results are collected
+            t0 = time.perf_counter()
             self.prep(range(self.offs[h], self.offs[h] + len(half)))
-            out += self._collect(h)
+            t1 = time.perf_counter()
+            self.t_prep += t1 - t0
+            got = self._collect(h)
+            t2 = time.perf_counter()
+            out += got
+            self.t_tag += time.perf_counter() - t2
             t0 = time.perf_counter()
             imls_icp.register_frames_async(self._order(h))   # builds (after the filter counts) + the batch's launches
             self.t_launch += time.perf_counter() - t0
@@ -675,7 +682,7 @@ def main():
     if hasattr(runner, "t_prep"):
         runner.t_prep = runner.t_reg = 0.0
     if getattr(runner, "pipe", None):
-        runner.pipe.t_wait = runner.pipe.t_launch = 0.0
+        runner.pipe.t_wait = runner.pipe.t_launch = runner.pipe.t_prep = runner.pipe.t_tag = 0.0
     # the stream's frame of each result: the (map, source) frames loaded when its batch was prepared
     frames_at_launch = {}
     if stream:
@@ -699,7 +706,9 @@ def main():
             f"rest (builds, launches, waits) {runner.t_reg / args.steps * 1e3:.2f} ms")
     if getattr(runner, "pipe", None):
         log(f"[rank {rank}] pipeline host time per step: result waits {runner.pipe.t_wait / args.steps * 1e3:.2f} ms, "
-            f"register_frames_async (builds + launches) {runner.pipe.t_launch / args.steps * 1e3:.2f} ms")
+            f"register_frames_async (builds + launches) {runner.pipe.t_launch / args.steps * 1e3:.2f} ms, "
+            f"input loads {runner.pipe.t_prep / args.steps * 1e3:.2f} ms, result tagging {runner.pipe.t_tag / args.steps * 1e3:.2f} ms, "
+            f"rest {(elapsed - runner.pipe.t_wait - runner.pipe.t_launch - runner.pipe.t_prep - runner.pipe.t_tag) / args.steps * 1e3:.2f} ms")
     n_pairs = args.steps * P
     value = world * n_pairs / elapsed
 

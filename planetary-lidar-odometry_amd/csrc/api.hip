@@ -4,6 +4,7 @@
 // `iterations` × {k_project, solve chain} launches are enqueued back to back on the context
 // stream; convergence / too-few-correspondence exits are taken on the device (a `done` flag
 // every later launch checks first), so the host synchronises once per frame.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -1473,8 +1474,6 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
     for (size_t k = 0; k < n; ++k) {
         imls_ctx* c = ctxs[k];
         if (!c) return fail(L, IMLS_ERR_ARG, "null context in the batch");
-        for (size_t j = 0; j < k; ++j)
-            if (ctxs[j] == c) return fail(L, IMLS_ERR_ARG, "a context appears twice in the batch");
         if (c->device != L->device) return fail(L, IMLS_ERR_ARG, "batch contexts must share one device");
         imls_params pc = c->P, pl = L->P;
         pc.ransac_seed = pl.ransac_seed = 0;    // each context runs its own rand() stream
@@ -1484,6 +1483,12 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
             return fail(L, IMLS_ERR_ARG, "batch contexts must share their traversal settings");
         if (c->pending || c->batch_member || (k > 0 && c->batch_pending))
             return fail(L, IMLS_ERR_STATE, "context " + std::to_string(k) + " has a frame pending");
+    }
+    {   // no context twice (sorted copy: O(n log n) for batches of thousands of frames)
+        std::vector<imls_ctx*> sorted(ctxs, ctxs + n);
+        std::sort(sorted.begin(), sorted.end());
+        if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
+            return fail(L, IMLS_ERR_ARG, "a context appears twice in the batch");
     }
     // every member's deferred build: its filter count (one wait each, all filters already enqueued)
     // then all the members' index builds in one launch sequence on the lead's stream
