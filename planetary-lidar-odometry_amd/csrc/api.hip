@@ -220,6 +220,8 @@ KParams make_kparams(const imls_params& p) {
     k.verlet = 1;
     k.qverlet = 0;
     if (const char* w = std::getenv("IMLS_VERLET")) k.verlet = k.qverlet = std::atoi(w);
+    k.verlet2 = k.verlet;
+    if (const char* w = std::getenv("IMLS_VERLET2")) k.verlet2 = std::atoi(w);
     k.lockstep = 1;
     if (const char* w = std::getenv("IMLS_LOCKSTEP")) k.lockstep = std::atoi(w);
     k.bcast_lock = 0;

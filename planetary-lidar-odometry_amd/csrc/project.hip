@@ -288,11 +288,15 @@ __device__ unsigned g_dbg_wave[kDbgWaves][16];
 // so the list — unchanged, not even re-read — still holds the exact answer when U < W'.
 // fp32 keys carry ≤ 3.1e-7 relative error and D ≤ 3e-7: the 1e-6 factors and the 1e-5 margin
 // cover both; k_finish re-certifies in fp64 against W' (a failure there only costs the exact
-// fallback).  Returns true when the traversal can be skipped; w_out = W'.
-__device__ __forceinline__ bool verlet_skip(float4 xr, float nr, const float xf[3], float r2s, float& w_out) {
+// fallback).  Returns true when the traversal can be skipped; w_out = W' (also when the stale
+// bound U fails: w_low = W' whenever it is positive, else −1 — the prefilled list, re-measured at x,
+// may still certify itself against it, see knn_wave_body).
+__device__ __forceinline__ bool verlet_skip(float4 xr, float nr, const float xf[3], float r2s, float& w_out,
+                                            float& w_low) {
     const float dx = xf[0] - xr.x, dy = xf[1] - xr.y, dz = xf[2] - xr.z;
     const float D = sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz))) * (1.0f + 1e-6f) + 1e-6f;
     const float g = sqrtf(xr.w) * (1.0f - 1e-6f) - D;
+    w_low = g > 0.f ? fminf(g * g, r2s) : -1.0f;
     if (!(g > 0.f) || !(nr < kInfF)) return false;
     const float u = sqrtf(nr) * (1.0f + 1e-6f) + D;
     const float w = fminf(g * g, r2s);
@@ -384,7 +388,8 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
         greedy = disp * disp > kp.reseed * wlist[slot];
     }
-    if (active && !greedy && kp.verlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip);
+    float wlow = -1.0f;              // W' of the stored list at xf (prefill certificate below)
+    if (active && !greedy && kp.verlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip, wlow);
     if (active && !greedy && !skip) {
         // prefill from the previous iteration's list re-measured at the new pose: all positions,
         // then all points are loaded before any is consumed (two memory round trips, not 2·KL),
@@ -421,6 +426,15 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             }
         }
         bnd = fmin_nn(bcap, lk[KL - 1]);
+        // prefill certificate: the stored list re-measured at xf holds its answer when the key that
+        // answer relies on (max(K-th key within r, NN-1 key), need_key) is below W' — every point
+        // outside the list is at least √W' away (verlet_skip) — so the traversal is skipped exactly
+        // as for a Verlet reuse; the stale bound √nr + D there is the worst case of this re-measured
+        // key.  (fp32 slack as in verlet_skip; k_finish re-certifies the list in fp64 against W'.)
+        if (kp.verlet2 && wlow > 0.f) {
+            const float nk = need_key<KL>(lk, (float)kp.r2, kp.K);
+            if (nk < kInfF && nk * (1.0f + 1e-5f) < wlow) { skip = true; wskip = wlow; }
+        }
     }
     // leaf scan shared by the seed pass and the traversal: the lanes in `want` test every point of
     // leaf `leaf` against their bound; `listed`: the leaf may hold points already in a lane's
@@ -887,7 +901,8 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
         greedy = disp * disp > kp.reseed * wlist[slot];
     }
-    if (!greedy && kp.qverlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip);
+    float wlow = -1.0f;
+    if (!greedy && kp.qverlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip, wlow);
     if (skip) {
         // the list stays in place
     } else if (!greedy) {

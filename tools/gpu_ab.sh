@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 V=planetary-lidar-odometry_amd/csrc/variant/libimls_gpu.so
 if [ "${PRODUCT_TESTS:-0}" = 1 ]; then
   timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_verlet.py tests/test_gpu_plane_icp.py \
-      tests/test_gpu_tv.py tests/test_gpu_bench_path.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/product_tests.log 2>&1
+      tests/test_gpu_tv.py tests/test_gpu_bench_path.py ${PRODUCT_TESTS_EXTRA:-} -m gpu -x -q --timeout 120 --timeout-method thread > $O/product_tests.log 2>&1
   rc=$?; echo "product tests rc=$rc"; tail -2 $O/product_tests.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "${VARIANT_TESTS:-0}" = 1 ]; then
