@@ -222,6 +222,8 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_VERLET")) k.verlet = k.qverlet = std::atoi(w);
     k.verlet2 = k.verlet;
     if (const char* w = std::getenv("IMLS_VERLET2")) k.verlet2 = std::atoi(w);
+    k.force_fb = 0;
+    if (const char* w = std::getenv("IMLS_FORCE_FALLBACK")) k.force_fb = std::max(0, std::atoi(w));
     k.lockstep = 1;
     if (const char* w = std::getenv("IMLS_LOCKSTEP")) k.lockstep = std::atoi(w);
     k.bcast_lock = 0;

@@ -59,6 +59,7 @@ struct KParams {
     int wide;                 // packet traversal: binary levels descended per step (1..3)
     int verlet;               // reuse a query's list without traversal while its certification holds
     int verlet2;              // … or while the re-measured prefilled list certifies itself (packet traversal)
+    int force_fb;             // test hook: every force_fb-th query slot deferred to the exact fallback (0 off)
     int qverlet;              // the same for the wave-per-query traversal (off by default: measured slower)
     int lockstep;             // packet traversal: per-lane candidate masks, then lockstep insertion
     int bcast_lock;           // … also for broadcast leaves: 0 never, 1 first ICP iteration, 2 always

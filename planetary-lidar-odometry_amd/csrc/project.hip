@@ -1149,10 +1149,16 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
             else need = fmax(need, d1);
             cert = cert && (need < (double)W / kCertSlack);
         }
+        if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_FORCE_FALLBACK)
         if (!cert) {
             const unsigned pos = atomicAdd(fb_count, 1u);
             fb_list[pos] = (unsigned)i;
             cat = -3;                                         // deferred to k_project_lane
+            // the list's own bound for the exact re-run: its points are real, so the exact answer
+            // needs no point beyond max(K-th listed key within r, listed NN-1) (r² when either is
+            // missing) — the fallback's search ball, instead of the whole radius r
+            const double lb = i1 < 0 ? r2 : fmax(cnt_r >= K ? dK : r2, d1);
+            cs[i] = make_float4(0.f, 0.f, 0.f, (float)(fmin(lb, r2) * (1.0 + 1e-6)));
         } else {
             cat = kp.matcher ? finish_plane(xf, ns, p1, t, kp, yf, nf)
                              : finish_query<KL>(xf, ns, ed, ep, 0, min(K, cnt_r), d1, p1, t, kp, yf, nf, kq, i);
@@ -1228,7 +1234,9 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
             // the projected distance — the tree only bounds the ‖p−x‖ ball, the list key is proj
             const bool proj = kp.proj != 0;
             const double r2 = proj ? kp.gate_dist * kp.gate_dist : kp.r2;
-            float bf = (float)r2 * kBoxSlack + 1e-30f;
+            // a query deferred by k_finish carries its list's bound in cs[i].w (the search ball cap)
+            const double cap = (qlist && !proj) ? fmin(r2, (double)cs[i].w) : r2;
+            float bf = (float)cap * kBoxSlack + 1e-30f;
             int node = 1, sp = 0;
             const int P = t.P, B = t.B, M = t.M;
             while (true) {
@@ -1292,7 +1300,7 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
                             }
                             changed = true;
                         }
-                        if (changed) bf = (float)fmin(r2, fmax(ld[KCAP - 1], d1)) * kBoxSlack + 1e-30f;
+                        if (changed) bf = (float)fmin(cap, fmax(ld[KCAP - 1], d1)) * kBoxSlack + 1e-30f;
                     }
                     node = 0;
                 }

@@ -106,3 +106,26 @@ def test_config_b_frame_matches_oracle(ctx, config_b, monkeypatch):
         assert tg.n_valid == tw.n_valid
         assert list(tg.reject) == list(tw.reject)
     assert np.abs(got["pose"] - want["pose"]).max() < POSE_TOL
+
+
+@pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair", "config_b"])
+def test_forced_fallback_same_correspondences(ctx, config_b, name, monkeypatch):
+    """Every 3rd query deferred to the exact fallback kernel (test hook IMLS_FORCE_FALLBACK), which
+    searches the ball its k_finish list bounds (max(K-th listed key, listed NN-1)) instead of the
+    whole radius: the same correspondences — valid counts and reject counters exact per iteration —
+    and poses within 1e-12 of the run without deferrals (the fallback's rows sum in other slabs)."""
+    monkeypatch.delenv("IMLS_QWAVE", raising=False)
+    if name == "config_b":
+        ctx.set_target(config_b.target)
+        ctx.set_source(config_b.source)
+    else:
+        g = dict(np.load(GOLDEN / f"{name}.npz"))
+        ctx.set_target(np.ascontiguousarray(g["tgt"].T))
+        ctx.set_source(np.ascontiguousarray(g["src"].T))
+    p = _params(10, shipped_thresholds=False)
+    monkeypatch.setenv("IMLS_FORCE_FALLBACK", "3")
+    forced = _frame(ctx, p, True, monkeypatch)
+    monkeypatch.delenv("IMLS_FORCE_FALLBACK")
+    plain = _frame(ctx, p, True, monkeypatch)
+    _same_frame(forced, plain)
+    assert forced["stats"]["uncertified"] > 0.3 * 10 * (config_b.source.size if name == "config_b" else 1), forced["stats"]
