@@ -61,9 +61,13 @@ def log(*a):
 # distributed plumbing (shared with tests/test_bench_dist.py, which runs it on gloo)
 # ------------------------------------------------------------------------------------------------
 def dist_setup(backend: str = "auto"):
-    """(world, rank, local_rank, torch device); initialises the process group when WORLD_SIZE > 1."""
+    """(world, rank, local_rank, torch device).  Under a launcher (torch.distributed.run sets
+    WORLD_SIZE, even at N = 1) the process group is initialised, so the launched bench always runs
+    its collectives — barrier, max-over-ranks timing, the pose all-gather — over RCCL (nccl) or gloo;
+    a plain `python bench.py` (no WORLD_SIZE) stays single-process without a group."""
     import torch
     import torch.distributed as dist
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -73,7 +77,7 @@ def dist_setup(backend: str = "auto"):
     if use_cuda:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local) if use_cuda else torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (launched or world > 1) and not dist.is_initialized():
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -81,12 +85,18 @@ def dist_setup(backend: str = "auto"):
     return world, rank, local, dev
 
 
+def _grouped() -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def timed_steps(step, steps: int, world: int, dev, sync=None):
     """Run `steps` calls of step() between barrier + sync on both sides.  Returns (elapsed = max over
     ranks, per-step seconds of this rank, the concatenated per-step results)."""
     import torch.distributed as dist
     sync = sync or (lambda: None)
-    if world > 1:
+    grouped = _grouped()
+    if grouped:
         dist.barrier()
     sync()
     per, out = [], []
@@ -97,7 +107,7 @@ def timed_steps(step, steps: int, world: int, dev, sync=None):
         per.append(time.perf_counter() - ts)
     sync()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if grouped:
         import torch
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -115,7 +125,7 @@ def exchange_poses(results, world: int, rank: int = 0):
     seq = np.array([rank * (1 << 20) + int(r[0]) for r in results], dtype=np.int64)
     order = np.array([int(r[1]) for r in results], dtype=np.int64)
     poses = np.asarray([r[2] for r in results], dtype=np.float64).reshape(-1, 4, 4)
-    if world > 1:
+    if world > 1 or _grouped():           # over the process group whenever there is one (RCCL on GPU)
         seq, order, poses = sequences.gather_tagged_poses(seq, order, poses)
     return (seq, order, poses), sequences.chain_per_sequence(seq, order, poses)
 
@@ -328,20 +338,40 @@ class PairRunner:
     context's rand() stream from params.ransac_seed (each pair is an independent registration, the
     reference's first frame), so a result depends on its pair alone."""
 
-    def __init__(self, pairs, p, dev, local, fuse=True, groups=2, tensors=False, alloc=None):
+    def __init__(self, pairs, p, dev, local, fuse=True, groups=2, tensors=False, alloc=None, host=False):
         self.fuse = fuse
         self.pairs = pairs
         self.ransac = p.solve_method == _abi.IMLS_SOLVE_RANSAC
+        # host: the deployment hand-over (SURVEY §8(d) t_pair) — every context keeps its map as a
+        # device FIFO of the map's scans (max_queue_size = their number, accumulateTargetCloud
+        # laser_odometry.cpp:116-136), and each registration takes the NEWEST scan and the source
+        # from host memory as the reference's 48-B PointXYZINormal records (map_push + set_source:
+        # pack + PCIe inside the timed region).  The pushed scan cycles through the pair's map
+        # scans, so the FIFO always holds the same points, concatenated from a rotating first scan
+        # (self.rot[k] = that scan's index for the context's last load).
+        self.host = host
+        self.local = local
+        self.p = type(p).from_buffer_copy(p)             # (host mode sets its max_queue_size)
+        p = self.p
+        if host:
+            self.parts = [synth.map_parts(q) for q in pairs]
+            self.p.max_queue_size = len(self.parts[0])
+            self.tick = [0] * len(pairs)
+            self.rot = [0] * len(pairs)
         # device copies (anything with data_ptr()): torch tensors, or `alloc(float32 array)`
         to_dev = alloc or (lambda a: __import__("torch").from_numpy(np.ascontiguousarray(a)).to(dev).contiguous())
-        self.s_dev = [to_dev(synth.soa(q.source)) for q in pairs]
-        self.t_dev = [to_dev(synth.soa(q.target)) for q in pairs]
+        self.s_dev = [to_dev(synth.soa(q.source)) for q in pairs] if not host else None
+        self.t_dev = [to_dev(synth.soa(q.target)) for q in pairs] if not host else None
         # config E: the targets' tensor-voting input tensors, SoA (6, M) in HBM
         self.ten_dev = None
         if tensors:
             self.ten_dev = [to_dev(np.ascontiguousarray(q.meta["tensors"].T)) for q in pairs]
         self.ctxs = [imls_icp.ImlsContext(p, device=local) for _ in pairs]
         self.seed_state = self.ctxs[0].rng_state()        # a fresh context's stream (params.ransac_seed)
+        if host:
+            for k, c in enumerate(self.ctxs):             # the FIFO's steady state: every map scan once
+                for part in self.parts[k]:
+                    c.map_push(part, count=False)
         # deferred reads of the count-less device loads: a large batch filters all its members in
         # three launches (the inputs stay resident and unchanged for the whole run)
         per_group = len(pairs) / max(1, groups)
@@ -353,6 +383,14 @@ class PairRunner:
         q = self.pairs[k]
         if self.ransac:
             c.set_rng_state(self.seed_state)
+        if self.host:
+            parts = self.parts[k]
+            i = self.tick[k] % len(parts)
+            self.tick[k] += 1
+            c.map_push(parts[i], count=count)             # the new scan: host records → FIFO
+            self.rot[k] = (i + 1) % len(parts)            # the FIFO now starts at scan i + 1
+            c.set_source(q.source, count=count)
+            return
         c.set_target_device(self.t_dev[k].data_ptr(), q.target.size, count=count)
         if self.ten_dev:
             c.set_target_tensors_device(self.ten_dev[k].data_ptr(), q.target.size)
@@ -380,6 +418,19 @@ class PairRunner:
             out.append((k, pose, it, st, self.ctxs[k].last_trace))
         return out
 
+    def single_fresh(self, k: int, rot: int = 0):
+        """Pair k registered alone on a fresh context whose map is the pair's scans concatenated from
+        scan `rot` on (host mode: what the FIFO held for a load with that rotation): the single-frame
+        kernels, tagged like Pipeline."""
+        parts = self.parts[k] if self.host else [self.pairs[k].target]
+        with imls_icp.ImlsContext(self.p, device=self.local) as c:
+            if self.ransac:
+                c.set_rng_state(self.seed_state)
+            c.set_target(np.concatenate(parts[rot:] + parts[:rot]))
+            c.set_source(self.pairs[k].source)
+            r = c.register_frame()
+        return (k, r["pose"], r["iters"], r["status"], r["trace"])
+
     def drain(self):
         return self.pipe.drain() if self.pipe else []
 
@@ -391,8 +442,12 @@ class PairRunner:
 
 class StreamRunner:
     """Config C/D-like: `n_seq` independent sequences (one context each); each step processes one
-    frame per sequence exactly as LaserOdometry.process does (map_push of the previous filtered
-    scan, set_source of the flat cloud, register).  A sequence ping-pongs over its F produced frames
+    frame per sequence in LaserOdometry.process's order (map_push of the previous filtered scan,
+    set_source of the flat cloud, register).  One difference, for RANSAC only: every frame restarts
+    its context's rand() stream from params.ransac_seed (_prep), so a frame's result depends on that
+    frame alone and can be verified by re-registering it on a fresh context; LaserOdometry and the
+    reference instead run one stream across the sequence's frames.  The draws per frame are the same
+    in number and kind, so the stream-RANSAC frames/s measures the same work.  A sequence ping-pongs over its F produced frames
     (0 … F−1 … 0 …) so every step registers two adjacent frames.  Results are tagged with the
     context index; self.last[q] = (map frame, source frame) of the frame most recently loaded."""
 
@@ -537,6 +592,60 @@ def latency_probe(run_one, ctx, n_pairs: int, iters: int):
                 launches={n: int(v[1]) for n, v in k.items()})
 
 
+def stream_frame_probe(runner, n_frames: int = 40, warm: int = 3) -> dict:
+    """One LaserOdometry.process frame alone — the deployment shape: the ROS node registers one frame
+    at a time, inside the reference's timer "2. Matching and solving in flat points"
+    (laser_odometry.cpp:482, 660; tic_toc.h:28-38).  Host inputs as the node holds them (48-B
+    PointXYZINormal records): the previous filtered scan joins the device map FIFO (map_push), the
+    flat cloud is set, the fused registration runs and its pose returns to the host — one context
+    kept across frames, sequence 0 ping-ponged over its produced frames.  Wall time per frame
+    (median / p90), the host hand-over part (pack + enqueue + filter waits), and the per-kind kernel
+    split from a second pass with HIP events around every launch."""
+    fr = runner.seqs[0]
+    F = len(fr)
+
+    def idx(j):
+        if F == 1:
+            return 0, 0
+        r, ph = divmod(j, F - 1)
+        k = ph if r % 2 == 0 else F - 1 - ph
+        k2 = k + 1 if r % 2 == 0 else k - 1
+        return k, k2                       # map frame, source frame (adjacent)
+    with imls_icp.ImlsContext(runner.p, device=runner.local) as c:
+        def frame(j):
+            m, k = idx(j)
+            t0 = time.perf_counter()
+            c.map_push(fr[m][0])
+            c.set_source(fr[k][1])
+            t1 = time.perf_counter()
+            r = c.register_frame()
+            return t1 - t0, time.perf_counter() - t0, r
+        for j in range(warm):
+            frame(j)
+        lat, hand = [], []
+        for j in range(n_frames):
+            h, t, _ = frame(warm + j)
+            lat.append(t)
+            hand.append(h)
+        c.enable_timing(True)
+        c.reset_timing()
+        nt = max(n_frames // 2, 1)
+        for j in range(nt):
+            frame(warm + n_frames + j)
+        c.enable_timing(False)
+        kinds = ("projection", "index", "solve", "k_knn_wave", "k_finish")
+        split = {}
+        for i, name in enumerate(kinds):
+            ms, n = c.kernel_timing(i)
+            split[name] = {"ms_per_frame": ms / nt, "launches_per_frame": n / nt}
+    lat, hand = np.array(lat) * 1e3, np.array(hand) * 1e3
+    return dict(frames=n_frames, median_ms=float(np.median(lat)), p90_ms=float(np.percentile(lat, 90)),
+                host_handover_median_ms=float(np.median(hand)), kernel_split=split,
+                queries=int(np.mean([len(f[1]) for f in fr])), map_points=int(np.mean([len(f[0]) for f in fr])),
+                rule="LaserOdometry.process shape: map_push(previous filtered scan, host) + set_source(flat cloud, "
+                     "host) + register_frame (20 ICP iterations), one frame at a time, wall clock")
+
+
 def same_result(a, b) -> bool:
     """Bit equality of two tagged results (pose, iterations, status, every trace record)."""
     if not (np.array_equal(np.asarray(a[1]), np.asarray(b[1])) and a[2] == b[2] and a[3] == b[3]):
@@ -620,7 +729,9 @@ def main():
                     help="fused: launch sequences the step's pairs are split into, kept in flight together "
                          "(0 = workload default: B 4, A 1, stream 1)")
     ap.add_argument("--host-inputs", action="store_true",
-                    help="stream: frames handed over in host memory (PCIe inside the timed region)")
+                    help="inputs handed over in host memory, PCIe inside the timed region (stream: the new map "
+                         "scan + flat cloud per frame; A/B: each pair's map is a device FIFO of its scans, the newest "
+                         "scan + the source cross PCIe per registration, SURVEY §8(d) t_pair)")
     ap.add_argument("--latency-pairs", type=int, default=50, help="single-pair latency / roofline probe size")
     ap.add_argument("--busy-steps", type=int, default=5, help="steps of the HIP-event busy-time pass (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
@@ -668,7 +779,10 @@ def main():
         if args.queries > 0:
             pairs = [synth.Pair(synth.fps_subsample(q.source, args.queries, seed=rank), q.target, q.true_pose, q.meta)
                      for q in pairs]
-        runner = PairRunner(pairs, p, dev, local, fuse=fuse, groups=args.groups, tensors=args.workload == "E")
+        if args.host_inputs and args.workload == "E":
+            raise SystemExit("--host-inputs: config E's tensor inputs stay device-resident (not supported)")
+        runner = PairRunner(pairs, p, dev, local, fuse=fuse, groups=args.groups, tensors=args.workload == "E",
+                            host=args.host_inputs)
         queries, map_points = pairs[0].source.size, pairs[0].target.size
     probe_ctx = runner.ctxs[0]
     log(f"[rank {rank}] workload {args.workload} set up in {time.time() - t0:.1f}s: {P} in flight, "
@@ -684,20 +798,22 @@ def main():
     if getattr(runner, "pipe", None):
         runner.pipe.t_wait = runner.pipe.t_launch = runner.pipe.t_prep = runner.pipe.t_tag = 0.0
     # the stream's frame of each result: the (map, source) frames loaded when its batch was prepared
+    # (host-input pairs: the FIFO rotation of each result's load)
     frames_at_launch = {}
-    if stream:
+    tag_loads = stream or (args.host_inputs and not stream)
+    if tag_loads:
         orig_prep = runner._prep
 
         def tagging_prep(idx):
             orig_prep(idx)
             for q in idx:
-                frames_at_launch.setdefault(q, []).append(runner.last[q])
+                frames_at_launch.setdefault(q, []).append(runner.last[q] if stream else runner.rot[q])
         runner._prep = tagging_prep
         if runner.pipe:
             runner.pipe.prep = tagging_prep
     elapsed, per_step, res = timed_steps(runner.step, args.steps, world, dev, torch.cuda.synchronize)
     res += runner.drain()                 # the batches still in flight (already finished: synchronized)
-    if stream:
+    if tag_loads:
         runner._prep = orig_prep
         if runner.pipe:
             runner.pipe.prep = orig_prep
@@ -732,6 +848,28 @@ def main():
                 mism += 0 if ok else 1
         verify = dict(timed_results=len(res), checked=checked, mismatches=mism,
                       rule="sequences 0-7, first two timed frames each, vs a fresh context registering that frame alone")
+    elif args.host_inputs:
+        # each result vs its pair registered alone on a fresh context whose map is the FIFO's content
+        # at that load (same scans, same rotation), single-frame kernels, bit for bit
+        seen, cache, mism = {}, {}, 0
+        for r in res:
+            k = r[0]
+            j = seen.get(k, 0)
+            seen[k] = j + 1
+            key = (k, frames_at_launch[k][j])
+            if args.no_verify:
+                continue
+            if key not in cache:
+                cache[key] = runner.single_fresh(*key)
+            mism += 0 if same_result(r, cache[key]) else 1
+        ref = {k: runner.single_fresh(k, 0) for k in range(len(runner.pairs))}
+        verify = dict(timed_results=len(res), checked=0 if args.no_verify else len(res), mismatches=mism,
+                      distinct_maps=len(cache),
+                      rule="every timed result vs its pair registered alone on a fresh context holding the same FIFO "
+                           "content (single-frame kernels), bit for bit")
+        errs = [np.linalg.norm(ref[k][1][:3, 3] - q.true_pose[:3, 3]) for k, q in enumerate(runner.pairs)]
+        worst = int(np.argmax(errs))
+        log(f"[rank {rank}] max pose error vs synthetic truth {max(errs) * 100:.2f} cm (pair {worst})")
     else:
         ref = {r[0]: r for r in runner.single()}
         mism = 0 if args.no_verify else sum(0 if same_result(r, ref[r[0]]) else 1 for r in res)
@@ -752,9 +890,13 @@ def main():
     allp, trajs = exchange_poses(tags, world, rank)
 
     # (3) single-pair latency + serialised per-launch kernel durations, algorithmic bytes, busy time
-    probe = None
+    probe = single_frame = None
     if not stream:
         probe = latency_probe(lambda: runner.single([0]), probe_ctx, args.latency_pairs, args.iters)
+    elif args.latency_pairs > 0:
+        single_frame = stream_frame_probe(runner, args.latency_pairs)
+        log(f"[rank {rank}] single frame: median {single_frame['median_ms']:.3f} ms, p90 {single_frame['p90_ms']:.3f} ms, "
+            f"host hand-over {single_frame['host_handover_median_ms']:.3f} ms")
     fb = stats_pass(runner)
     bytes_per_step = float(sum(fb.values())) if not stream else float(np.mean(list(fb.values()))) * P
     busy = busy_pass(runner, args.busy_steps, torch.cuda.synchronize) if args.busy_steps > 0 else None
@@ -762,7 +904,7 @@ def main():
 
     if rank != 0:
         runner.close()
-        if world > 1:
+        if _grouped():
             dist.destroy_process_group()
         return
 
@@ -791,7 +933,7 @@ def main():
             q0 = runner.pairs[worst]
             src, tgt, truth = synth.soa(q0.source), synth.soa(q0.target), q0.true_pose
             ten = np.ascontiguousarray(q0.meta["tensors"].T) if args.workload == "E" else None
-            k0, pose0, it0, st0, tr0 = runner.single([worst])[0]
+            k0, pose0, it0, st0, tr0 = runner.single_fresh(worst, 0) if args.host_inputs else runner.single([worst])[0]
             got = dict(pose=pose0, iters=it0, status=st0, trace=tr0)
             label = f"config {args.workload}, pair {worst} (the step's largest error vs the synthetic truth)"
         cpu, want = cpu_baseline(src, tgt, p, label, tensors=ten, faithful=True)
@@ -843,6 +985,9 @@ def main():
     if args.workload == "B":
         metric = "IMLS-ICP scan-pairs/s (HDL-64 ~120k-pt scan vs 10-scan map, 20 ICP iterations)"
         workload = f"config B: HDL-64 scan vs 10-scan local map; a step = {P} independent scan pairs" + (f" as {args.groups} launch sequences in flight" if fuse else " in flight, one stream each")
+        if args.host_inputs:
+            workload += ("; host hand-over: each pair's map is a device FIFO of its 10 scans, the newest scan and the "
+                         "source cross PCIe as 48-B PointXYZINormal records in every registration")
         unit = "scan-pairs/s"
     elif args.workload == "E":
         metric = ("IMLS-ICP scan-pairs/s (config E: tensor-voting normals + IMLS on sparse VLP-16 planetary scans, "
@@ -876,6 +1021,7 @@ def main():
         "pairs_in_flight": P,
         "ms_per_iteration": elapsed / n_pairs * 1e3 / args.iters,
         "single_pair": probe,
+        "single_frame": single_frame,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -888,9 +1034,12 @@ def main():
             "icp_iterations": args.iters,
             "solver": solver_txt,
             "search_number": p.search_number,
+            "inputs": "host memory (PCIe inside the timed region)" if args.host_inputs else "resident in HBM",
             "fused_launch": fuse,
             "launch_groups": args.groups if fuse else P,
-            "parallelism": f"independent pairs per GPU over {world} GPU(s), RCCL pose all-gather" if world > 1 else "1 GPU",
+            "parallelism": (f"independent pairs per GPU over {world} GPU(s), {dist.get_backend()} "
+                            f"({'RCCL' if dist.get_backend() == 'nccl' else 'CPU'}) pose all-gather"
+                            if _grouped() else "1 GPU, no process group"),
         },
         "verify": verify,
         "parity": parity,
@@ -903,7 +1052,7 @@ def main():
     }
     print(json.dumps(out), flush=True)
     runner.close()
-    if world > 1:
+    if _grouped():
         dist.destroy_process_group()
 
 

@@ -294,10 +294,15 @@ int imls_register_frame_result(imls_ctx* ctx, double pose_out[16], int* iters_ru
  * (saveMatchedPointsToFile of in_cloud_vec / ref_cloud_vec into matched_points/<ts>_<i>.txt,
  * laser_odometry.cpp:621-623; saver.cpp:113-133).  While on, each iteration's correspondences are
  * kept on the device (48 B per source point per iteration); after the frame's result,
- * imls_captured_correspondences(iter) returns iteration `iter` (< iters_run) compacted in source
- * order exactly as imls_project does (capacity: the kept source points). */
+ * imls_captured_correspondences(iter) returns iteration `iter` (< iters_run of that frame) compacted in
+ * source order exactly as imls_project does.  `cap` is the capacity of the caller's arrays in rows
+ * (x/y/n: 3·cap floats, index: cap); *n_valid always receives the row count, and with every output
+ * pointer NULL the call is a size query.  More rows than `cap` → IMLS_ERR_ARG, nothing written.
+ * The capture stays readable across set_target / map_push (LaserOdometry writes the files after the
+ * map has taken the new scan); a later set_source or a batched registration drops it
+ * (IMLS_ERR_STATE until the next captured imls_register_frame). */
 int imls_capture_correspondences(imls_ctx* ctx, int on);
-int imls_captured_correspondences(imls_ctx* ctx, int iter, float* x_out, float* y_out, float* n_out,
+int imls_captured_correspondences(imls_ctx* ctx, int iter, size_t cap, float* x_out, float* y_out, float* n_out,
                                   uint32_t* src_index_out, size_t* n_valid);
 
 /* ---- many frames in one launch sequence (configs C/D: many sequences per GPU) ------------ */

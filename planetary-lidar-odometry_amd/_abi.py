@@ -212,7 +212,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_map_size": (C.c_int, [VP, P(SZ), P(SZ)]),
         "imls_set_defer": (C.c_int, [VP, C.c_int]),
         "imls_capture_correspondences": (C.c_int, [VP, C.c_int]),
-        "imls_captured_correspondences": (C.c_int, [VP, C.c_int, VP, VP, VP, VP, P(SZ)]),
+        "imls_captured_correspondences": (C.c_int, [VP, C.c_int, SZ, VP, VP, VP, VP, P(SZ)]),
         "imls_timing_origin": (C.c_int, [VP]),
         "imls_timing_intervals": (C.c_int, [VP, C.c_int, VP, SZ, P(SZ)]),
     }

@@ -12,7 +12,10 @@
 #include <cstring>
 #include <deque>
 #include <string>
+#include <condition_variable>
+#include <functional>
 #include <thread>
+#include <mutex>
 #include <vector>
 
 #include "internal.h"
@@ -99,6 +102,7 @@ struct imls_ctx {
     bool capture = false;
     DevBuf cap_mem;
     int cap_iters = 0, cap_N = 0;
+    int cap_run = -1;                     // iterations the captured frame ran (-1: result not collected yet)
     // async frame results
     imls_iter_trace* h_trace = nullptr;   // pinned
     double* h_misc = nullptr;             // pinned: pose[16], iters, status
@@ -236,6 +240,8 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_KL")) k.kl20 = std::atoi(w);
     k.lazy_listed = 1;
     if (const char* w = std::getenv("IMLS_LAZY_LISTED")) k.lazy_listed = std::atoi(w);
+    k.lds_list = 0;
+    if (const char* w = std::getenv("IMLS_LDS_LIST")) k.lds_list = std::atoi(w);
     // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
     // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)
     k.tv = (p.use_tensor_voting && !p.get_normals && p.matching_method == IMLS_MATCH_IMLS) ? 1 : 0;
@@ -470,13 +476,23 @@ hipEvent_t* project_marks(imls_ctx* c, hipEvent_t marks[3]) {
     return marks;
 }
 
-// Process-wide origin of the timing intervals (imls_timing_origin): one clock for every context
-// of the device, so the busy time of concurrent launch sequences is the union of their intervals.
-hipEvent_t g_origin = nullptr;
-int g_origin_device = -1;
+// Process-wide origin of the timing intervals (imls_timing_origin): one clock per device for every
+// context of that device, so the busy time of concurrent launch sequences is the union of their
+// intervals.  One origin per device, created once and never destroyed while the process runs (a
+// context on another device cannot pull an origin out from under this one); the mutex orders the
+// origin's (re)recording against the comparisons in harvest_timing.
+constexpr int kMaxDevices = 64;
+std::mutex g_origin_mu;
+hipEvent_t g_origin[kMaxDevices] = {};
+bool g_origin_set[kMaxDevices] = {};
+// intervals kept per context and launch kind until imls_reset_timing / imls_timing_origin (a cap:
+// a caller that never resets keeps a bounded record, the oldest first)
+constexpr size_t kMaxIntervals = (size_t)1 << 20;
 
 void harvest_timing(imls_ctx* c) {
-    const bool iv = g_origin && g_origin_device == c->device;
+    std::lock_guard<std::mutex> lk(g_origin_mu);
+    const bool dev_ok = c->device >= 0 && c->device < kMaxDevices;
+    const bool iv = dev_ok && g_origin_set[c->device];
     for (int k = 0; k < kTimingKinds; ++k) {
         for (auto& pr : c->ev_pairs[k]) {
             float ms = 0;
@@ -484,8 +500,9 @@ void harvest_timing(imls_ctx* c) {
                 c->t_ms[k] += ms;
                 c->t_n[k] += 1;
                 float a = 0, b = 0;
-                if (iv && hipEventElapsedTime(&a, g_origin, c->ev[pr.first]) == hipSuccess &&
-                    hipEventElapsedTime(&b, g_origin, c->ev[pr.second]) == hipSuccess)
+                if (iv && c->iv[k].size() < kMaxIntervals &&
+                    hipEventElapsedTime(&a, g_origin[c->device], c->ev[pr.first]) == hipSuccess &&
+                    hipEventElapsedTime(&b, g_origin[c->device], c->ev[pr.second]) == hipSuccess)
                     c->iv[k].push_back({a, b});
             }
         }
@@ -494,8 +511,93 @@ void harvest_timing(imls_ctx* c) {
     c->ev_used = 0;
 }
 
+// Persistent host workers for the upload packing: a scan of ~10^5 points is a strided gather of
+// several MB, split over a few threads — created once per process, not per call (spawning 7
+// std::threads per upload cost ~0.2 ms, more than the gather itself: round 3 measured 333 µs per
+// 118k-point scan).  One job at a time (the mutex serialises contexts on other host threads).
+class PackPool {
+public:
+    static PackPool& get() {
+        static PackPool pool;
+        return pool;
+    }
+    size_t width() const { return workers_.size() + 1; }
+    // fn(i0, i1) over [0, n) in `parts` contiguous chunks (parts ≤ width()), the caller taking the first
+    void run(size_t n, size_t parts, const std::function<void(size_t, size_t)>& fn) {
+        parts = std::max<size_t>(1, std::min(parts, width()));
+        if (parts == 1 || n == 0) {
+            fn(0, n);
+            return;
+        }
+        std::lock_guard<std::mutex> job_lock(job_mu_);
+        const size_t chunk = (n + parts - 1) / parts;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            n_ = n;
+            chunk_ = chunk;
+            parts_ = parts;
+            pending_ = parts - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0, std::min(n, chunk));
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    PackPool() {
+        // the process's CPU share, at most 7 helpers (8 with the caller): the gather is memory-bound
+        size_t hw = std::max<unsigned>(std::thread::hardware_concurrency(), 1u);
+        if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::min<size_t>(hw, (size_t)std::max(1, std::atoi(e)));
+        const size_t helpers = std::min<size_t>(7, hw > 1 ? hw - 1 : 0);
+        for (size_t k = 0; k < helpers; ++k) workers_.emplace_back([this, k] { loop(k + 1); });
+    }
+    ~PackPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    void loop(size_t id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(size_t, size_t)>* fn;
+            size_t i0, i1;
+            bool mine;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                mine = id < parts_;
+                fn = fn_;
+                i0 = std::min(n_, id * chunk_);
+                i1 = std::min(n_, (id + 1) * chunk_);
+            }
+            if (!mine) continue;
+            (*fn)(i0, i1);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_cv_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex job_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(size_t, size_t)>* fn_ = nullptr;
+    size_t n_ = 0, chunk_ = 0, parts_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 // Pack a strided host cloud into SoA6 floats in pinned staging and upload asynchronously (no host
-// wait: the staging buffer is reused only after its previous copy has run).
+// wait: the staging buffer is reused only after its previous copy has run).  The reference's
+// PointXYZINormal records (48 B: x y z pad | nx ny nz pad | intensity curvature pad pad, nrm =
+// xyz + 4, stride 12 floats) take a record-at-a-time path (two 16-B loads per point).
 int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, size_t n, size_t stride, int which) {
     if (!xyz || !nrm || n == 0 || stride < 3) return fail(c, IMLS_ERR_ARG, "bad cloud pointer/size/stride");
     if (!c->ev_stage[which] && hipEventCreateWithFlags(&c->ev_stage[which], hipEventDisableTiming) != hipSuccess)
@@ -510,8 +612,19 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
         c->stage_cap[which] = cap;
     }
     float* h = c->h_stage[which];
-    auto pack = [=](size_t i0, size_t i1) {
+    const bool rec48 = nrm == xyz + 4 && stride == 12 && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0;
+    const std::function<void(size_t, size_t)> pack = [=](size_t i0, size_t i1) {
         float *hx = h, *hy = h + n, *hz = h + 2 * n, *hnx = h + 3 * n, *hny = h + 4 * n, *hnz = h + 5 * n;
+        if (rec48) {
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            const f4* r = reinterpret_cast<const f4*>(xyz);
+            for (size_t i = i0; i < i1; ++i) {
+                const f4 p = r[3 * i], q = r[3 * i + 1];
+                hx[i] = p.x; hy[i] = p.y; hz[i] = p.z;
+                hnx[i] = q.x; hny[i] = q.y; hnz[i] = q.z;
+            }
+            return;
+        }
         for (size_t i = i0; i < i1; ++i) {
             const float* p = xyz + i * stride;
             const float* q = nrm + i * stride;
@@ -519,18 +632,7 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
             hnx[i] = q[0]; hny[i] = q[1]; hnz[i] = q[2];
         }
     };
-    // a scan of ~10^5 points is a strided gather of several MB: split it over host threads
-    const size_t T = std::min<size_t>(std::max<size_t>(std::thread::hardware_concurrency(), 1),
-                                      std::min<size_t>(8, n / 16384 + 1));
-    if (T <= 1) {
-        pack(0, n);
-    } else {
-        std::vector<std::thread> th;
-        const size_t chunk = (n + T - 1) / T;
-        for (size_t t = 1; t < T; ++t) th.emplace_back(pack, std::min(n, t * chunk), std::min(n, (t + 1) * chunk));
-        pack(0, std::min(n, chunk));
-        for (auto& x : th) x.join();
-    }
+    PackPool::get().run(n, n / 16384 + 1, pack);
     if (!grow(dst, 6 * n * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (upload)");
     if (hipMemcpyAsync(dst.p, h, 6 * n * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         hipEventRecord(c->ev_stage[which], c->stream) != hipSuccess)
@@ -779,6 +881,7 @@ int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
 }
 
 int do_set_source(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept, uint32_t* kept_index) {
+    c->cap_iters = 0;                     // a new source drops the captured frame
     if (n == 0 || n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "source size out of range");
     if (kept_index && !grow(c->skept, n * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (kept)");
     if (!c->ev_src && hipEventCreateWithFlags(&c->ev_src, hipEventDisableTiming) != hipSuccess)
@@ -1341,6 +1444,7 @@ int imls_register_frame_async(imls_ctx* c) {
     const TreeView tv = tree_view(c);
     if (int rc = prepare_ransac(c, c->N)) return rc;
     c->cap_iters = 0;
+    c->cap_run = -1;
     if (c->capture && iters > 0) {
         if (!grow(c->cap_mem, (size_t)iters * c->N * 48)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (capture)");
         c->cap_iters = iters;
@@ -1357,9 +1461,13 @@ int imls_register_frame_async(imls_ctx* c) {
         timed_end(c, 0, slot);
         if (c->cap_iters) {   // this iteration's correspondences (stale, and never read, once the frame stopped)
             char* dst = (char*)c->cap_mem.p + (size_t)it * c->N * 48;
-            hipMemcpyAsync(dst, c->cs.p, (size_t)c->N * 16, hipMemcpyDeviceToDevice, c->stream);
-            hipMemcpyAsync(dst + (size_t)c->N * 16, c->cd.p, (size_t)c->N * 16, hipMemcpyDeviceToDevice, c->stream);
-            hipMemcpyAsync(dst + (size_t)c->N * 32, c->cn.p, (size_t)c->N * 16, hipMemcpyDeviceToDevice, c->stream);
+            const size_t nb = (size_t)c->N * 16;
+            if (hipMemcpyAsync(dst, c->cs.p, nb, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
+                hipMemcpyAsync(dst + nb, c->cd.p, nb, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
+                hipMemcpyAsync(dst + 2 * nb, c->cn.p, nb, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) {
+                c->cap_iters = 0;
+                return fail(c, IMLS_ERR_DEVICE, "capture copy");
+            }
         }
         timed_begin(c, 2, slot);
         launch_solve(c->stream, solve_launch(c, tr + it, 1));
@@ -1389,6 +1497,7 @@ int imls_register_frame_result(imls_ctx* c, double pose_out[16], int* iters_run,
     if (pose_out) std::memcpy(pose_out, c->h_misc, 16 * 8);
     if (iters_run) *iters_run = misc[0];
     if (status) *status = st;
+    if (c->cap_iters) c->cap_run = misc[0];
     if (trace && c->pending_iters > 0) std::memcpy(trace, c->h_trace, (size_t)c->pending_iters * sizeof(imls_iter_trace));
     return IMLS_OK;
 }
@@ -1478,6 +1587,7 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
     for (size_t k = 0; k < n; ++k) {
         imls_ctx* c = ctxs[k];
         if (!c) return fail(L, IMLS_ERR_ARG, "null context in the batch");
+        c->cap_iters = 0;                 // batched frames capture nothing: drop an older capture
         if (c->device != L->device) return fail(L, IMLS_ERR_ARG, "batch contexts must share one device");
         imls_params pc = c->P, pl = L->P;
         pc.ransac_seed = pl.ransac_seed = 0;    // each context runs its own rand() stream
@@ -1865,17 +1975,27 @@ int imls_capture_correspondences(imls_ctx* c, int on) {
     return IMLS_OK;
 }
 
-int imls_captured_correspondences(imls_ctx* c, int iter, float* x_out, float* y_out, float* n_out,
+int imls_captured_correspondences(imls_ctx* c, int iter, size_t cap, float* x_out, float* y_out, float* n_out,
                                   uint32_t* src_index_out, size_t* n_valid) {
     if (!c || !n_valid) return IMLS_ERR_ARG;
     if (c->pending) return fail(c, IMLS_ERR_STATE, "collect the frame first (imls_register_frame_result)");
-    if (iter < 0 || iter >= c->cap_iters) return fail(c, IMLS_ERR_STATE, "no captured iteration " + std::to_string(iter));
+    // the captured frame's iterations only: a later set_source or batch drops the capture (its rows
+    // index the old source), and iterations at or past the frame's iters_run hold stale rows
+    if (c->cap_iters == 0 || c->cap_run < 0) return fail(c, IMLS_ERR_STATE, "no captured frame");
+    if (iter < 0 || iter >= std::min(c->cap_iters, c->cap_run))
+        return fail(c, IMLS_ERR_STATE, "no captured iteration " + std::to_string(iter));
     if (int rc = check_device(c)) return rc;
     const size_t N = (size_t)c->cap_N;
     std::vector<float> h(N * 12);
     if (hipMemcpy(h.data(), (const char*)c->cap_mem.p + (size_t)iter * N * 48, N * 48, hipMemcpyDeviceToHost) != hipSuccess)
         return fail(c, IMLS_ERR_DEVICE, "capture download");
     const float *hs = h.data(), *hd = hs + 4 * N, *hn = hs + 8 * N;
+    size_t nv = 0;
+    for (size_t i = 0; i < N; ++i) nv += hs[4 * i + 3] != 0.f ? 1 : 0;
+    *n_valid = nv;
+    const bool want = x_out || y_out || n_out || src_index_out;
+    if (!want) return IMLS_OK;            // size query
+    if (nv > cap) return fail(c, IMLS_ERR_ARG, "capacity " + std::to_string(cap) + " < " + std::to_string(nv) + " rows");
     size_t k = 0;
     for (size_t i = 0; i < N; ++i) {
         if (hs[4 * i + 3] == 0.f) continue;   // rejected (erased from in_cloud by the reference)
@@ -1887,7 +2007,6 @@ int imls_captured_correspondences(imls_ctx* c, int iter, float* x_out, float* y_
         if (src_index_out) src_index_out[k] = (uint32_t)i;
         ++k;
     }
-    *n_valid = k;
     return IMLS_OK;
 }
 
@@ -1900,14 +2019,13 @@ int imls_set_defer(imls_ctx* c, int on) {
 int imls_timing_origin(imls_ctx* c) {
     if (!c) return IMLS_ERR_ARG;
     if (int rc = check_device(c)) return rc;
-    if (g_origin && g_origin_device != c->device) {
-        (void)hipEventDestroy(g_origin);
-        g_origin = nullptr;
-    }
-    if (!g_origin && hipEventCreate(&g_origin) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipEventCreate (origin)");
-    g_origin_device = c->device;
-    if (hipEventRecord(g_origin, c->stream) != hipSuccess || hipEventSynchronize(g_origin) != hipSuccess)
+    if (c->device < 0 || c->device >= kMaxDevices) return fail(c, IMLS_ERR_ARG, "device index");
+    std::lock_guard<std::mutex> lk(g_origin_mu);
+    hipEvent_t& o = g_origin[c->device];
+    if (!o && hipEventCreate(&o) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipEventCreate (origin)");
+    if (hipEventRecord(o, c->stream) != hipSuccess || hipEventSynchronize(o) != hipSuccess)
         return fail(c, IMLS_ERR_DEVICE, "origin event");
+    g_origin_set[c->device] = true;
     for (auto& v : c->iv) v.clear();
     return IMLS_OK;
 }

@@ -321,6 +321,53 @@ __device__ __forceinline__ float need_key(const float (&lk)[KL], float r2, int K
     return cnt_r >= K ? fmaxf(dK, d1) : kInfF;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Slot-id keys (the LDS-list traversal): a lane's top-KL list is its KL keys in registers, kept
+// ascending, each key = the fp32 squared distance with its low IDB mantissa bits replaced by the id
+// of the LDS slot that holds the point's position.  An insertion evicts the list's last key, whose
+// slot takes the new position (one ds_write at a lane-specific address) and whose id the new key
+// inherits; the keys move by med3 alone (one VALU per slot) — the positions never move, where the
+// register list moves every position with two selects per slot (88 → ~26 VALU per insertion).
+//
+// Truncation keeps the search exact.  A point is inserted iff trunc(d) < trunc(max key), i.e.
+// d < thr = float(bits(max) & ~IDM); thr only falls during the walk, so every point never inserted
+// has d ≥ thr_final, and an evicted point's truncated key was ≥ the new maximum's — every point
+// outside the final list has d32 ≥ thr_final, which is the W this traversal reports (≤ 2^(IDB−23)
+// below the full-precision KL-th key: k_finish's fp64 certificate against W is unchanged).
+// Upper bounds taken from a key (need_key_ids, the Verlet reuse) round up: d ≤ float(bits | IDM).
+// Empty slots hold finite sentinels kIdSentinel | id (above every real key, never NaN for med3).
+// ---------------------------------------------------------------------------------------------
+template <int KL>
+struct IdKeys {
+    static constexpr unsigned IDM = KL <= 32 ? 31u : 63u;
+    static constexpr unsigned kSentinel = 0x7F7FFFFFu & ~IDM;
+    __device__ static __forceinline__ float lo(float k) { return __uint_as_float(__float_as_uint(k) & ~IDM); }
+    __device__ static __forceinline__ float hi(float k) { return __uint_as_float(__float_as_uint(k) | IDM); }
+    __device__ static __forceinline__ unsigned id(float k) { return __float_as_uint(k) & IDM; }
+    __device__ static __forceinline__ float make(float d, unsigned s) { return __uint_as_float((__float_as_uint(d) & ~IDM) | s); }
+    __device__ static __forceinline__ float empty(unsigned s) { return __uint_as_float(kSentinel | s); }
+    __device__ static __forceinline__ bool real(float k) { return (__float_as_uint(k) & ~IDM) < kSentinel; }
+};
+
+// need_key over slot-id keys: max(K-th key within r, NN-1 key), every bound rounded up (a key's
+// point lies in [lo, hi]); ∞ when fewer than K keys are surely within r or no NN-1 exists.
+template <int KL>
+__device__ __forceinline__ float need_key_ids(const float (&lk)[KL], float r2, int K) {
+    using I = IdKeys<KL>;
+    const float r2f = r2 * (1.0f + 1e-6f);
+    int cnt_r = 0;
+    float dK = kInfF, d1 = kInfF;
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+        const float up = I::hi(lk[j]);
+        const bool in = I::real(lk[j]) && up <= r2f;
+        cnt_r += in ? 1 : 0;
+        if (in && d1 == kInfF && I::lo(lk[j]) > 1e-15f) d1 = up;
+        if (j == K - 1) dK = up;
+    }
+    return cnt_r >= K ? fmaxf(dK, d1) : kInfF;
+}
+
 // Register cap of the packet traversal: 216 VGPRs (2 waves/SIMD) uncapped; capping at 3 waves/SIMD
 // (168 VGPRs) spills ~56 VGPRs of cold-path state to scratch and measured +4-5 % pairs/s with 4 pairs
 // in flight (more resident waves hide the dependent node/leaf loads).  Longer lists (KL > 24) keep
@@ -329,7 +376,7 @@ __device__ __forceinline__ float need_key(const float (&lk)[KL], float r2, int K
 #define IMLS_KNN_WPE 3
 #endif
 #define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 24 ? IMLS_KNN_WPE : 1)))
-template <int KL, bool LOCKSTEP>
+template <int KL, bool LOCKSTEP, bool LDSL>
 __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
                                                          const double* __restrict__ pose,
@@ -343,7 +390,11 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float4 sbox[kWaveBlock / 64][kWaveStack][2];
     __shared__ float4 sleaf[kWaveBlock / 64][64];   // the current leaf's points (lockstep insertion)
+    // LDSL: the list's positions, slot s of thread tid at spos[s][tid] (slot-id keys, IdKeys)
+    __shared__ int spos[LDSL ? KL : 1][kWaveBlock];
     const int tid = threadIdx.x, lane = tid & 63;
+    int* const mypos = &spos[0][tid];
+    using IK = IdKeys<KL>;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     // a wave owns kp.packet Morton-consecutive queries (64; 32 or 16 in the first iterations, where
     // most lanes seed: a smaller packet's union of neighbourhoods is smaller, and the launch lasts
@@ -358,9 +409,34 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         transform_query(pose, spt[i], make_float4(0.f, 0.f, 0.f, 0.f), 0, xf, ns);
     }
     float lk[KL];
-    int lp[KL];
+    int lp[KL];     // register list only (!LDSL)
 #pragma unroll
-    for (int j = 0; j < KL; ++j) { lk[j] = kInfF; lp[j] = -1; }
+    for (int j = 0; j < KL; ++j) {
+        lk[j] = LDSL ? IK::empty(j) : kInfF;
+        if (!LDSL) lp[j] = -1;
+    }
+    // (LDSL: the slots are cleared here when no seed table is staged; in the first ICP iteration the
+    // table aliases spos and they are cleared after the seed search, below)
+    if (LDSL && use_prev) {
+#pragma unroll
+        for (int j = 0; j < KL; ++j) mypos[j * kWaveBlock] = -1;
+    }
+    // the list behind one interface: thr_ = the strict insertion threshold (a point with key d joins
+    // iff d < thr_()), ins_ = sorted insertion (precondition d < thr_()), pos_ = position of slot s
+    // (any order), full_ = KL real entries, need_ = need_key (upper-rounded for slot-id keys)
+    auto thr_ = [&]() -> float { return LDSL ? IK::lo(lk[KL - 1]) : lk[KL - 1]; };
+    auto full_ = [&]() -> bool { return LDSL ? IK::real(lk[KL - 1]) : lk[KL - 1] < kInfF; };
+    auto pos_ = [&](int s) -> int { return LDSL ? mypos[s * kWaveBlock] : lp[s]; };
+    auto need_ = [&]() -> float { return LDSL ? need_key_ids<KL>(lk, (float)kp.r2, kp.K) : need_key<KL>(lk, (float)kp.r2, kp.K); };
+    auto ins_ = [&](float d, int pos) {
+        if constexpr (LDSL) {
+            const unsigned s = IK::id(lk[KL - 1]);
+            insert_key<KL>(lk, IK::make(d, s));
+            mypos[s * kWaveBlock] = pos;
+        } else {
+            insert_top<KL>(lk, lp, d, pos);
+        }
+    };
     const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
     float bnd = active ? r2s : -1.0f;
     // the lane's bound cap: r2s, or (seed_keys) the seed's KL-th key — a bound the final KL-th key
@@ -396,16 +472,23 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         // and the nearly sorted keys are ordered by an early-exit odd-even transposition sort
         // (the list is full and the bound tight before the traversal starts; a later leaf insert
         // must then skip points already listed)
+        int pj[KL];
 #pragma unroll
-        for (int j = 0; j < KL; ++j) lp[j] = lists[(size_t)j * N + slot];
+        for (int j = 0; j < KL; ++j) pj[j] = lists[(size_t)j * N + slot];
 #pragma unroll
         for (int j = 0; j < KL; ++j) {
-            const float4 q = t.mpt[max(lp[j], 0)];
+            const float4 q = t.mpt[max(pj[j], 0)];
             const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
             const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-            const bool keep = lp[j] >= 0 && d32 <= r2s;
-            lk[j] = keep ? d32 : kInfF;
-            lp[j] = keep ? lp[j] : -1;
+            const bool keep = pj[j] >= 0 && d32 <= r2s;
+            if (LDSL) {
+                // slot j keeps entry j's position; its key carries id j (the keys alone get sorted)
+                lk[j] = keep ? IK::make(d32, j) : IK::empty(j);
+                mypos[j * kWaveBlock] = keep ? pj[j] : -1;
+            } else {
+                lk[j] = keep ? d32 : kInfF;
+                lp[j] = keep ? pj[j] : -1;
+            }
         }
         bool swapped = true;
         while (swapped) {
@@ -416,23 +499,25 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 for (int j = par; j + 1 < KL; j += 2) {
                     const bool sw = lk[j + 1] < lk[j];
                     const float tk = lk[j];
-                    const int tp = lp[j];
                     lk[j] = sw ? lk[j + 1] : lk[j];
-                    lp[j] = sw ? lp[j + 1] : lp[j];
                     lk[j + 1] = sw ? tk : lk[j + 1];
-                    lp[j + 1] = sw ? tp : lp[j + 1];
+                    if (!LDSL) {
+                        const int tp = lp[j];
+                        lp[j] = sw ? lp[j + 1] : lp[j];
+                        lp[j + 1] = sw ? tp : lp[j + 1];
+                    }
                     swapped |= sw;
                 }
             }
         }
-        bnd = fmin_nn(bcap, lk[KL - 1]);
+        bnd = fmin_nn(bcap, thr_());
         // prefill certificate: the stored list re-measured at xf holds its answer when the key that
         // answer relies on (max(K-th key within r, NN-1 key), need_key) is below W' — every point
         // outside the list is at least √W' away (verlet_skip) — so the traversal is skipped exactly
         // as for a Verlet reuse; the stale bound √nr + D there is the worst case of this re-measured
         // key.  (fp32 slack as in verlet_skip; k_finish re-certifies the list in fp64 against W'.)
         if (kp.verlet2 && wlow > 0.f) {
-            const float nk = need_key<KL>(lk, (float)kp.r2, kp.K);
+            const float nk = need_();
             if (nk < kInfF && nk * (1.0f + 1e-5f) < wlow) { skip = true; wskip = wlow; }
         }
     }
@@ -456,7 +541,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         auto listed_mask = [&]() {
 #pragma unroll
             for (int k = 0; k < KL; ++k) {
-                const unsigned rel = (unsigned)(lp[k] - base);
+                const unsigned rel = (unsigned)(pos_(k) - base);
                 inl |= rel < 64u ? (1ull << rel) : 0ull;
             }
         };
@@ -475,12 +560,17 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         if (listed) {
             if (lock_path && kp.lazy_listed) {
 #pragma unroll
-                for (int k = 0; k < KL; ++k) nin += (unsigned)(lp[k] - base) < 64u ? 1 : 0;
+                for (int k = 0; k < KL; ++k) nin += (unsigned)(pos_(k) - base) < (unsigned)cnt ? 1 : 0;
             } else {
                 listed_mask();
                 have_inl = true;
             }
         }
+        // the lockstep paths' candidate bound: it must admit every listed point of the leaf (the
+        // count comparison above counts them as candidates) — bnd itself does for the register list
+        // (listed keys ≤ the KL-th key); slot-id keys truncate, and a listed point can lie up to
+        // hi(max key) (the lockstep loop re-tests d32 < thr_() before inserting)
+        const float cb = LDSL ? fmin_nn(bcap, IK::hi(lk[KL - 1])) : bnd;
         if (lock_path) {
             // few lanes want this leaf (spread-out queries in a dense region): per wanting lane,
             // all leaf points are measured at once (one per lane) and the ones under that lane's
@@ -501,7 +591,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                     const float pz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.z), j));
                     const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
                     const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                    cm |= (wants && d32 <= bnd) ? (1ull << j) : 0ull;
+                    cm |= (wants && d32 <= cb) ? (1ull << j) : 0ull;
                 }
                 if (!have_inl) {
                     const bool more = __popcll(cm) > nin;
@@ -517,7 +607,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                     const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[0]), q));
                     const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[1]), q));
                     const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[2]), q));
-                    const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bnd), q));
+                    const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cb), q));
                     const float ex = mine.x - qx, ey = mine.y - qy, ez = mine.z - qz;
                     const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
                     unsigned long long pm = __ballot(lane < cnt && d32 <= qb);
@@ -551,12 +641,12 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                         const float4 p = sleaf[wv][j];
                         const float ex = p.x - xf[0], ey = p.y - xf[1], ez = p.z - xf[2];
                         const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                        if (d32 <= bnd && d32 < lk[KL - 1]) {
+                        if (d32 <= bnd && d32 < thr_()) {
 #ifdef IMLS_DEBUG_WAVE_TRACE
                             ++dbg_ins;
 #endif
-                            insert_top<KL>(lk, lp, d32, base + j);
-                            bnd = fmin_nn(bcap, lk[KL - 1]);
+                            ins_(d32, base + j);
+                            bnd = fmin_nn(bcap, thr_());
                         }
                     }
 #ifdef IMLS_DEBUG_WAVE_TRACE
@@ -587,12 +677,12 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                     const int j = __builtin_amdgcn_readfirstlane(__builtin_ctzll(pm));
                     pm &= pm - 1;
                     const float dj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d32), j));
-                    if (lane == q && dj <= bnd && dj < lk[KL - 1]) {
+                    if (lane == q && dj <= bnd && dj < thr_()) {
 #ifdef IMLS_DEBUG_WAVE_TRACE
                         ++dbg_sparse_ins;
 #endif
-                        insert_top<KL>(lk, lp, dj, base + j);
-                        bnd = fmin_nn(bcap, lk[KL - 1]);
+                        ins_(dj, base + j);
+                        bnd = fmin_nn(bcap, thr_());
                     }
                 }
             }
@@ -604,15 +694,15 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 const float pz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.z), j));
                 const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
                 const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                const bool ins = wants && d32 <= bnd && d32 < lk[KL - 1] && !((inl >> j) & 1ull);
+                const bool ins = wants && d32 <= bnd && d32 < thr_() && !((inl >> j) & 1ull);
 #ifdef IMLS_DEBUG_WAVE_TRACE
                 const unsigned long long bi = __ballot(ins);
                 dbg_ev += bi ? 1 : 0;
                 dbg_ins += __popcll(bi);
 #endif
                 if (ins) {
-                    insert_top<KL>(lk, lp, d32, base + j);
-                    bnd = fmin_nn(bcap, lk[KL - 1]);
+                    ins_(d32, base + j);
+                    bnd = fmin_nn(bcap, thr_());
                 }
             }
         }
@@ -630,7 +720,10 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     // ~15 dependent global loads per lane (measured: the seed pass was ~half of iterations 0-2)
     // (first ICP iteration only, where every lane seeds: later iterations reseed a few lanes, which
     // would not repay the block barrier)
-    __shared__ unsigned long long skey[kSeedTab];
+    // (LDSL: the table lives in spos, whose slots are not in use yet — cleared after the search)
+    __shared__ unsigned long long skey_own[LDSL ? 1 : kSeedTab];
+    static_assert(!LDSL || KL * kWaveBlock * 4 >= kSeedTab * 8, "seed table fits the slot array");
+    unsigned long long* const skey = LDSL ? reinterpret_cast<unsigned long long*>(&spos[0][0]) : skey_own;
     const int S = use_prev ? t.L : (t.L + kSeedTab - 1) / kSeedTab;
     const int ntab = S > 0 ? (t.L + S - 1) / S : 0;
     if (!use_prev) {
@@ -641,6 +734,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     // lane's bound cap and the list restarts empty — the traversal, which visits the seed leaves
     // anyway, inserts the final members (nothing is listed twice, so no listed-mask is needed)
     const bool seed_keys = kp.seed_keys != 0;
+    int seed_leaf = 0;
     if (greedy) {
         const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
         int j = 0, jh = ntab - 1;
@@ -655,6 +749,15 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             if (t.lkeys[mid] <= qk) l = mid;
             else h = mid - 1;
         }
+        seed_leaf = l;
+    }
+    if (LDSL && !use_prev) {
+        __syncthreads();             // every wave is done with the seed table (it aliases spos)
+#pragma unroll
+        for (int j = 0; j < KL; ++j) mypos[j * kWaveBlock] = -1;
+    }
+    if (greedy) {
+        const int l = seed_leaf;
         const int p0s = max(0, l - kp.seed_half) * B;
         const int pend = min(M, (min(t.L - 1, l + kp.seed_half) + 1) * B);
         float4 qs[kSeedChunk];
@@ -669,25 +772,30 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 const float ex = qs[k].x - xf[0], ey = qs[k].y - xf[1], ez = qs[k].z - xf[2];
                 const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
 #ifdef IMLS_DEBUG_WAVE_TRACE
-                dbg_seed_steps += __ballot(p0 + k < pend && d32 <= bnd && d32 < lk[KL - 1]) ? 1 : 0;
+                dbg_seed_steps += __ballot(p0 + k < pend && d32 <= bnd && d32 < thr_()) ? 1 : 0;
                 ++dbg_seed_pts;
 #endif
-                if (p0 + k < pend && d32 <= bnd && d32 < lk[KL - 1]) {
-                    if (seed_keys) {
+                if (p0 + k < pend && d32 <= bnd && d32 < thr_()) {
+                    if (seed_keys && !LDSL) {
                         insert_key<KL>(lk, d32);
                     } else {
-                        insert_top<KL>(lk, lp, d32, p0 + k);
+                        ins_(d32, p0 + k);
                     }
-                    bnd = fmin_nn(bcap, lk[KL - 1]);
+                    bnd = fmin_nn(bcap, thr_());
                 }
             }
 #pragma unroll
             for (int k = 0; k < kSeedChunk; ++k) qs[k] = nx[k];
         }
         if (seed_keys) {
-            bcap = bnd;
+            bcap = LDSL ? IK::hi(lk[KL - 1]) : bnd;   // a bound the KL seed points lie within
+            if (LDSL) bcap = fmin_nn(bcap, bnd);
 #pragma unroll
-            for (int j = 0; j < KL; ++j) lk[j] = kInfF;
+            for (int j = 0; j < KL; ++j) lk[j] = LDSL ? IK::empty(j) : kInfF;
+            if (LDSL) {
+#pragma unroll
+                for (int j = 0; j < KL; ++j) mypos[j * kWaveBlock] = -1;
+            }
         }
     }
     unsigned n_inner = 0, n_leaf = 0;
@@ -778,12 +886,15 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     if (active && skip) wlist[slot] = wskip;   // a reused list stays in place
     if (active && !skip) {
 #pragma unroll
-        for (int j = 0; j < KL; ++j) lists[(size_t)j * N + slot] = lp[j];
-        wlist[slot] = lk[KL - 1];
+        for (int j = 0; j < KL; ++j) lists[(size_t)j * N + slot] = LDSL ? pos_(IK::id(lk[j])) : lp[j];   // ascending keys
+        const bool full = full_();
+        const float wk = full ? thr_() : kInfF;
+        wlist[slot] = wk;
         // reference position + guarantee of a fresh list: every map point outside it has fp32
-        // key ≥ the KL-th key (full list) or > the search bound (all points within r listed)
-        xref[slot] = make_float4(xf[0], xf[1], xf[2], lk[KL - 1] < kInfF ? lk[KL - 1] : r2s);
-        nref[slot] = need_key<KL>(lk, (float)kp.r2, kp.K);
+        // key ≥ the KL-th key (full list; slot-id keys: its truncation thr_) or > the search bound
+        // (all points within r listed)
+        xref[slot] = make_float4(xf[0], xf[1], xf[2], full ? wk : r2s);
+        nref[slot] = need_();
     }
 #ifdef IMLS_DEBUG_WAVE_TRACE   // debug build only (make DEBUG_WAVE_TRACE=1): insert counters
     if (nbr_stats && lane == 0) {
@@ -802,9 +913,9 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         atomicAdd(&nbr_stats[15], (unsigned long long)__popcll(__ballot(greedy)));
     }
     {
-        const unsigned long long gl = __ballot(greedy), wi = __ballot(active && lk[KL - 1] == kInfF),
-                                 w1 = __ballot(active && lk[KL - 1] > 1.0f);
-        float wmax = active && lk[KL - 1] < kInfF ? lk[KL - 1] : 0.f;
+        const unsigned long long gl = __ballot(greedy), wi = __ballot(active && !full_()),
+                                 w1 = __ballot(active && full_() && thr_() > 1.0f);
+        float wmax = active && full_() ? thr_() : 0.f;
         for (int o = 1; o < 64; o <<= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, o));
         unsigned sins = dbg_sparse_ins;
         for (int o = 1; o < 64; o <<= 1) sins += __shfl_xor(sins, o);
@@ -1353,14 +1464,14 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
 // Kernels: one frame (arguments by value) and batched (frame = tab[blockIdx.y]; blocks past the
 // frame's own grid leave at once).  Both run the same bodies.
 // ---------------------------------------------------------------------------------------------
-template <int KL, bool LOCKSTEP>
+template <int KL, bool LOCKSTEP, bool LDSL>
 __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(
         TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
         const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
         int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
         int use_prev, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_count) {
-    knn_wave_body<KL, LOCKSTEP>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats,
-                                fb_count, (int)blockIdx.x);
+    knn_wave_body<KL, LOCKSTEP, LDSL>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev,
+                                      nbr_stats, fb_count, (int)blockIdx.x);
 }
 
 template <int KL>
@@ -1428,7 +1539,7 @@ __device__ __forceinline__ void batch_block(int xcd, int& frame, int& bx) {
     bx = (int)(s % nx);
 }
 
-template <int KL, bool LOCKSTEP>
+template <int KL, bool LOCKSTEP, bool LDSL>
 __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const PairDev* __restrict__ tab, KParams kp,
                                                                           int use_prev, int npairs) {
     int f, bx;
@@ -1437,7 +1548,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const P
     const PairDev A = tab[f];
     if (use_qwave(kp, A.N) || bx >= knn_blocks_of(A.N, kp.packet)) return;
     float4* xref = xref_dev(A.lists, A.N);
-    knn_wave_body<KL, LOCKSTEP>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
+    knn_wave_body<KL, LOCKSTEP, LDSL>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
                                 wlist_of<KL>(A.lists, A.N), xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats,
                                 A.fb_count, bx);
 }
@@ -1486,8 +1597,9 @@ void launch_wave_batch(hipStream_t s, const PairDev* tab, int npairs, int maxN, 
     }
     if (any_large) {
         const int kb = knn_blocks_of(maxN, kp.packet);
-        if (kp.lockstep) k_knn_wave_b<KL, true><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
-        else k_knn_wave_b<KL, false><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        if (kp.lds_list) k_knn_wave_b<KL, true, true><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        else if (kp.lockstep) k_knn_wave_b<KL, true, false><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        else k_knn_wave_b<KL, false, false><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
     }
     k_finish_b<KL><<<dim3(wb, gy), kWaveBlock, 0, s>>>(tab, kp, it, npairs);
 }
@@ -1516,11 +1628,14 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
                                                                                           delta, lists, wlist, xref, nref, use_prev, stats,
                                                                                           fb_count);
+    else if (kp.lds_list)
+        k_knn_wave<KL, true, true><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
+                                                          nref, use_prev, stats, fb_count);
     else if (kp.lockstep)
-        k_knn_wave<KL, true><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
+        k_knn_wave<KL, true, false><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
                                                           nref, use_prev, stats, fb_count);
     else
-        k_knn_wave<KL, false><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
+        k_knn_wave<KL, false, false><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
                                                            nref, use_prev, stats, fb_count);
     if (marks) (void)hipEventRecord(marks[1], s);
     k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,

@@ -329,13 +329,15 @@ class ImlsContext:
 
     def captured(self, it: int):
         """Iteration `it` of the last register_frame: (x, y, n, source index), source order."""
-        N = max(self.n_source if self.n_source is not None else self.index_stats()["queries"], 1)
+        nv = C.c_size_t()
+        # size query first (all outputs NULL), then arrays of exactly that many rows
+        self._check(self.lib.imls_captured_correspondences(self.ctx, int(it), 0, None, None, None, None, C.byref(nv)))
+        N = nv.value
         x = np.zeros((N, 3), np.float32); y = np.zeros((N, 3), np.float32); n = np.zeros((N, 3), np.float32)
-        idx = np.zeros(N, np.uint32); nv = C.c_size_t()
-        self._check(self.lib.imls_captured_correspondences(self.ctx, int(it), _ptr(x), _ptr(y), _ptr(n), _ptr(idx),
+        idx = np.zeros(N, np.uint32)
+        self._check(self.lib.imls_captured_correspondences(self.ctx, int(it), N, _ptr(x), _ptr(y), _ptr(n), _ptr(idx),
                                                            C.byref(nv)))
-        k = nv.value
-        return x[:k], y[:k], n[:k], idx[:k]
+        return x, y, n, idx
 
     def timing_origin(self):
         """Process-wide origin of the timing intervals (imls_timing_origin)."""

@@ -8,7 +8,12 @@ independent units once their map is known:
 * one long sequence: contiguous blocks of frames per rank, each block preceded by a halo of the
   `max_queue_size` filtered scans before it, pushed into the rank's map FIFO and not registered
   (halo_block) — every frame then sees the same map as on one rank, so its relative pose is the
-  same bits.
+  same bits, for solvers that draw no random numbers (LS, Weighted LS).  RANSAC draws from ONE
+  rand() stream across the whole sequence (the reference's process-wide, never-seeded rand(),
+  common.cpp:49; LaserOdometry keeps its context's stream across frames): a rank starting
+  mid-sequence would need the stream's state after every earlier frame's draws, which only a
+  sequential run produces, so run_halo_block refuses RANSAC (split many sequences instead: each
+  sequence on one rank keeps its stream).
 
 The only exchange is ONE all-gather of the 4×4 relative poses (16 doubles per frame, 128 B) over
 RCCL/xGMI; every rank then chains each sequence T_k = T_{k−1}·ΔT_k (laser_odometry.cpp:652-655).
@@ -42,7 +47,14 @@ def run_halo_block(odo, frames, halo, block):
     """Drive a LaserOdometry-shaped object (map_push(filtered) / register(flat) → rPose) over one
     rank's share of a sequence: the halo scans join the FIFO unregistered, then each block frame is
     registered against the FIFO and its filtered scan pushed, as processData orders them
-    (laser_odometry.cpp:478-670).  Returns the block's relative poses in frame order."""
+    (laser_odometry.cpp:478-670).  Returns the block's relative poses in frame order.  RANSAC is
+    refused (module docstring: its rand() stream runs across the sequence's frames)."""
+    from . import _abi
+    params = (getattr(odo, "params", None) or getattr(odo, "p", None)
+              or getattr(getattr(odo, "ctx", None), "params", None))
+    if params is not None and int(getattr(params, "solve_method", 0)) == _abi.IMLS_SOLVE_RANSAC:
+        raise ValueError("run_halo_block: RANSAC draws one rand() stream across the sequence; a halo "
+                         "split is exact only for LS / Weighted LS — split whole sequences instead")
     for k in halo:
         odo.map_push(frames[k][0])
     rel = []

@@ -362,7 +362,8 @@ def make_pair(model: str = "hdl64", map_scans: int = 10, scene_seed: int = 0, tr
     true_pose = Tk1_inv @ poses[k]
     return Pair(source, target, true_pose,
                 dict(model=model, map_scans=map_scans, scene_seed=scene_seed, traj_seed=traj_seed,
-                     noise_seed=noise_seed, scene_kind=scene_kind, start=start))
+                     noise_seed=noise_seed, scene_kind=scene_kind, start=start,
+                     part_sizes=[len(q) for q in parts]))
 
 
 def make_pairs(n: int, model: str = "hdl64", map_scans: int = 10, scene_seed: int = 0, traj_seed: int = 2000,
@@ -378,11 +379,20 @@ def make_pairs(n: int, model: str = "hdl64", map_scans: int = 10, scene_seed: in
     for j in range(n):
         k = start + j
         Tk1_inv = np.linalg.inv(poses[k - 1])
-        target = np.concatenate([transform_cloud(scans[i], Tk1_inv @ poses[i]) for i in range(k - map_scans, k)])
+        parts = [transform_cloud(scans[i], Tk1_inv @ poses[i]) for i in range(k - map_scans, k)]
+        target = np.concatenate(parts)
         out.append(Pair(scans[k], target, Tk1_inv @ poses[k],
                         dict(model=model, map_scans=map_scans, scene_seed=scene_seed, traj_seed=traj_seed,
-                             noise_seed=noise_seed, scene_kind=scene_kind, start=k)))
+                             noise_seed=noise_seed, scene_kind=scene_kind, start=k,
+                             part_sizes=[len(q) for q in parts])))
     return out
+
+
+def map_parts(pair: "Pair") -> list:
+    """The map's scans (views into pair.target, oldest first; meta part_sizes), for a device FIFO
+    filled scan by scan (accumulateTargetCloud, laser_odometry.cpp:116-136)."""
+    sizes = pair.meta.get("part_sizes") or [len(pair.target)]
+    return np.split(pair.target, np.cumsum(sizes)[:-1])
 
 
 def soa(cloud: np.ndarray) -> np.ndarray:

@@ -117,3 +117,13 @@ def test_halo_split_gloo_world2(queue):
     for _, _, _, allp, traj in res:
         assert np.array_equal(allp, rel1)          # same relative poses, bit for bit
         assert np.array_equal(traj, traj1)         # same chained trajectory
+
+
+def test_halo_split_refuses_ransac():
+    """A halo split is exact only for solvers without random draws: RANSAC's rand() stream runs
+    across the sequence's frames (common.cpp:49, never seeded), so run_halo_block refuses it."""
+    from planetary_lidar_odometry_amd import _abi, sequences
+    odo = OracleOdometry(1)
+    odo.p.solve_method = _abi.IMLS_SOLVE_RANSAC
+    with pytest.raises(ValueError, match="RANSAC"):
+        sequences.run_halo_block(odo, [], range(0), range(1, 2))
