@@ -77,7 +77,14 @@ __device__ __forceinline__ bool angle_reject(const double ns[3], double n0, doub
     double b = n0 * n0;
     b = b + n1 * n1;
     b = b + n2 * n2;
-    const double ca = dot / (sqrt(a) * sqrt(b));
+    const double s = sqrt(a) * sqrt(b);
+    // the same two decisions without the division: outside ±2e-9 of cthr, dot vs (cthr ± 2e-9)·s
+    // decides exactly what ca = dot/s vs cthr ± 1e-9 decides (the division's rounding is ~1e-16
+    // relative), and dot ≥ −s(1 − 1e-12) certifies ca ≥ −1; anything else (the bands, zero / ∞ /
+    // NaN denominators) takes the reference's own evaluation below
+    if (dot > (cthr + 2e-9) * s) return false;
+    if (dot < (cthr - 2e-9) * s && dot >= -s * (1.0 - 1e-12)) return true;
+    const double ca = dot / s;
     if (ca > cthr + 1e-9) return false;
     if (ca < cthr - 1e-9 && ca >= -1.0) return true;
     const double angle = acos(ca) * 180.0 / M_PI;
@@ -375,7 +382,8 @@ __device__ __forceinline__ float need_key_ids(const float (&lk)[KL], float r2, i
 #ifndef IMLS_KNN_WPE
 #define IMLS_KNN_WPE 3
 #endif
-#define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 24 ? IMLS_KNN_WPE : 1)))
+// LDSL (slot-id keys, positions in LDS): ~96 VGPRs and ~29 KB of LDS per 4-wave block — 5 waves/SIMD
+#define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(LDSL ? (KL <= 24 ? 5 : 2) : (KL <= 24 ? IMLS_KNN_WPE : 1))))
 template <int KL, bool LOCKSTEP, bool LDSL>
 __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
@@ -388,8 +396,10 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                                                          unsigned* __restrict__ fb_count, int bx) {
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
-    __shared__ float4 sbox[kWaveBlock / 64][kWaveStack][2];
-    __shared__ float4 sleaf[kWaveBlock / 64][64];   // the current leaf's points (lockstep insertion)
+    __shared__ float4 sboxa[kWaveBlock / 64][kWaveStack];   // stacked node boxes: lo.xyz, hi.x
+    __shared__ float2 sboxb[kWaveBlock / 64][kWaveStack];   //                     hi.yz
+    // the current leaf's points for the lockstep insertion (LDSL: fetched by ds_bpermute instead)
+    __shared__ float4 sleaf[kWaveBlock / 64][LDSL ? 1 : 64];
     // LDSL: the list's positions, slot s of thread tid at spos[s][tid] (slot-id keys, IdKeys)
     __shared__ int spos[LDSL ? KL : 1][kWaveBlock];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -630,15 +640,25 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 }
             }
             if (__ballot(cm != 0ull)) {
-                sleaf[wv][lane] = mine;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (!LDSL) {
+                    sleaf[wv][lane] = mine;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
                 while (__ballot(cm != 0ull)) {
+                    // every lane takes part in the permutes (lanes without a candidate read lane 0)
+                    const int jj = cm ? (int)__builtin_ctzll(cm) : 0;
+                    float4 pl;
+                    if (LDSL) {
+                        pl.x = __shfl(mine.x, jj);
+                        pl.y = __shfl(mine.y, jj);
+                        pl.z = __shfl(mine.z, jj);
+                    }
                     if (cm) {
-                        const int j = (int)__builtin_ctzll(cm);
+                        const int j = jj;
                         cm &= cm - 1;
-                        const float4 p = sleaf[wv][j];
+                        const float4 p = LDSL ? pl : sleaf[wv][j];
                         const float ex = p.x - xf[0], ey = p.y - xf[1], ez = p.z - xf[2];
                         const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
                         if (d32 <= bnd && d32 < thr_()) {
@@ -653,7 +673,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                     ++dbg_ev;
 #endif
                 }
-                __builtin_amdgcn_wave_barrier();   // sleaf is rewritten by the next leaf
+                if (!LDSL) __builtin_amdgcn_wave_barrier();   // sleaf is rewritten by the next leaf
             }
         } else if (__popcll(want) <= sparse_thr) {
             // few lanes want this leaf (spread-out queries in a dense region): per wanting lane,
@@ -855,8 +875,8 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                         if (lane == 0) {
                             const float4 a = R[3 * (k >> 1)], b = R[3 * (k >> 1) + 1], c = R[3 * (k >> 1) + 2];
                             snode[wv][sp] = (node << sw) + k;
-                            sbox[wv][sp][0] = (k & 1) ? make_float4(b.z, b.w, c.x, c.y) : make_float4(a.x, a.y, a.z, a.w);
-                            sbox[wv][sp][1] = (k & 1) ? make_float4(c.z, c.w, 0.f, 0.f) : make_float4(b.x, b.y, 0.f, 0.f);
+                            sboxa[wv][sp] = (k & 1) ? make_float4(b.z, b.w, c.x, c.y) : make_float4(a.x, a.y, a.z, a.w);
+                            sboxb[wv][sp] = (k & 1) ? make_float2(c.z, c.w) : make_float2(b.x, b.y);
                         }
                         ++sp;
                     }
@@ -876,7 +896,8 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         node = 0;
         while (sp > 0) {
             --sp;
-            const float4 b0 = sbox[wv][sp][0], b1 = sbox[wv][sp][1];
+            const float4 b0 = sboxa[wv][sp];
+            const float2 b1 = sboxb[wv][sp];
             const float d = box_d2(xf, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y);
             em = __ballot(d <= bnd * kBoxSlack);
             if (em) { node = snode[wv][sp]; break; }
