@@ -127,7 +127,10 @@ __device__ __forceinline__ void insert_key(float (&lk)[KL], float d) {
 // L = (ld[j], lpos[j]) for j ∈ [first, first+cnt) sorted by (d², index) and its NN-1 (d1, p1);
 // positions are Morton positions (mpt/mnr: the neighbours of a query share cache lines).
 // Returns the reject category or −1 (valid, yf/nf filled).  kq counts the returned neighbours.
-template <int CAP>
+// LAZY_D: ld is not read — the one distance the IMLS bandwidth needs (L[target], Q3) is recomputed
+// from its point (the same fp64 expression, so the same bits), letting the caller's fp64 list die
+// after the certification (k_finish's register budget).
+template <int CAP, bool LAZY_D = false>
 __device__ int finish_query(const float xf[3], const double ns[3], const double (&ld)[CAP], const int (&lpos)[CAP],
                             int first, int cnt, double d1, int p1, const TreeView& t, const KParams& kp, float yf[3],
                             float nf[3], int& kq, int qi) {
@@ -149,23 +152,43 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
     const double xd[3] = {xf[0], xf[1], xf[2]};
     unsigned long long acc = 0ull;
     int nacc = 0;
+    // the normals in chunks of 8 (the loads of a chunk issue together; 24 VGPRs in flight, not 3·CAP)
+    constexpr int kChunk = 8;
 #pragma unroll
-    for (int j = 0; j < CAP; ++j) {
-        const bool inl = j >= first && j < first + cnt;
-        const float4 qn = t.mnr[inl ? lpos[j] : p1];   // unconditional: the loads issue together
-        if (inl) {
-            ++kq;
-            // get_normals=false without count mode (TV's IMLS neighbours): every normal is ∞ (Q1)
-            bool ok = kp.get_normals && isfinite(qn.x) && isfinite(qn.y) && isfinite(qn.z);
-            if (ok && kp.angle_on) ok = !angle_reject(ns, qn.x, qn.y, qn.z, kp.angle_thr_deg, kp.cos_thr);
-            if (ok) { acc |= 1ull << j; ++nacc; }
+    for (int j0 = 0; j0 < CAP; j0 += kChunk) {
+        float4 qn[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u) {
+            const int j = j0 + u;
+            const bool inl = j < CAP && j >= first && j < first + cnt;
+            qn[u] = t.mnr[inl ? lpos[j < CAP ? j : 0] : p1];
+        }
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u) {
+            const int j = j0 + u;
+            const bool inl = j < CAP && j >= first && j < first + cnt;
+            if (inl) {
+                ++kq;
+                // get_normals=false without count mode (TV's IMLS neighbours): every normal is ∞ (Q1)
+                bool ok = kp.get_normals && isfinite(qn[u].x) && isfinite(qn[u].y) && isfinite(qn[u].z);
+                if (ok && kp.angle_on) ok = !angle_reject(ns, qn[u].x, qn[u].y, qn[u].z, kp.angle_thr_deg, kp.cos_thr);
+                if (ok) { acc |= 1ull << j; ++nacc; }
+            }
         }
     }
     if (nacc < 3) return IMLS_REJ_MLS_FAIL;                   // imls_icp.cpp:463-466
     const int target = first + nacc - 1;                      // Q3: index into L, not into S
     double dsel = 0.0;
+    if (LAZY_D) {
+        int ptg = p1;
 #pragma unroll
-    for (int j = 0; j < CAP; ++j) dsel = (j == target) ? ld[j] : dsel;
+        for (int j = 0; j < CAP; ++j) ptg = (j == target) ? lpos[j] : ptg;
+        const float4 q = t.mpt[ptg];
+        dsel = exact_d2(xd, q.x, q.y, q.z);
+    } else {
+#pragma unroll
+        for (int j = 0; j < CAP; ++j) dsel = (j == target) ? ld[j] : dsel;
+    }
     const double hmax = sqrt(dsel) / 3;
     double wsum = 0.0, psum = 0.0;
 #pragma unroll
@@ -1194,11 +1217,11 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
 // =============================================================================================
 // Exact stage + gates + IMLS (hot kernel 2): one lane per query
 // =============================================================================================
-#ifdef IMLS_FINISH_WPE   // experiment: cap the exact stage's registers for more resident waves
-#define IMLS_FINISH_ATTR __attribute__((amdgpu_waves_per_eu(IMLS_FINISH_WPE)))
-#else
-#define IMLS_FINISH_ATTR
+// 4 waves/SIMD (≤ 128 VGPRs): the exact stage waits on its gathers, resident waves hide them
+#ifndef IMLS_FINISH_WPE
+#define IMLS_FINISH_WPE 4
 #endif
+#define IMLS_FINISH_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 24 ? IMLS_FINISH_WPE : 1)))
 template <int KL>
 __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict__ spt,
                                                        const float4* __restrict__ snr,
@@ -1231,7 +1254,7 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
         const double xd[3] = {xf[0], xf[1], xf[2]};
         const float W = wlist[slot];
         double ed[KL];
-        int eo[KL], ep[KL];
+        int ep[KL];
         // all positions, then all points, before any is consumed (two memory round trips)
 #pragma unroll
         for (int j = 0; j < KL; ++j) ep[j] = lists[(size_t)j * N + slot];
@@ -1239,9 +1262,11 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
         for (int j = 0; j < KL; ++j) {
             const float4 q = t.mpt[max(ep[j], 0)];
             ed[j] = ep[j] >= 0 ? exact_d2(xd, q.x, q.y, q.z) : kInfD;
-            eo[j] = ep[j] >= 0 ? (int)__float_as_uint(q.w) : 0x7fffffff;
         }
-        // odd-even transposition sort by (d², index); the fp32 order is already nearly exact
+        // odd-even transposition sort by (d², index); the fp32 order is already nearly exact.  The
+        // index (the filtered index in mpt[].w, libnabo's tie order) is read only for an exact tie
+        // of two distances (duplicate points): not carried in registers
+        auto oidx = [&](int pos) -> int { return pos >= 0 ? (int)__float_as_uint(t.mpt[pos].w) : 0x7fffffff; };
         bool swapped = true;
         while (swapped) {
             swapped = false;
@@ -1249,14 +1274,13 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
             for (int par = 0; par < 2; ++par) {
 #pragma unroll
                 for (int j = par; j + 1 < KL; j += 2) {
-                    const bool sw = lessp(ed[j + 1], eo[j + 1], ed[j], eo[j]);
+                    bool sw = ed[j + 1] < ed[j];
+                    if (ed[j + 1] == ed[j] && ed[j] < kInfD) sw = oidx(ep[j + 1]) < oidx(ep[j]);
                     const double td = ed[j];
-                    const int to = eo[j], tp = ep[j];
+                    const int tp = ep[j];
                     ed[j] = sw ? ed[j + 1] : ed[j];
-                    eo[j] = sw ? eo[j + 1] : eo[j];
                     ep[j] = sw ? ep[j + 1] : ep[j];
                     ed[j + 1] = sw ? td : ed[j + 1];
-                    eo[j + 1] = sw ? to : eo[j + 1];
                     ep[j + 1] = sw ? tp : ep[j + 1];
                     swapped |= sw;
                 }
@@ -1270,7 +1294,7 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
         for (int j = 0; j < KL; ++j) {
             const bool in = ed[j] <= r2;
             cnt_r += in ? 1 : 0;
-            if (in && i1 < 0 && ed[j] > DBL_EPSILON) { d1 = ed[j]; i1 = eo[j]; p1 = ep[j]; }
+            if (in && i1 < 0 && ed[j] > DBL_EPSILON) { d1 = ed[j]; i1 = j; p1 = ep[j]; }
             if (j == K - 1) dK = ed[j];
         }
         const bool full = W < kInfF;
@@ -1293,7 +1317,7 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
             cs[i] = make_float4(0.f, 0.f, 0.f, (float)(fmin(lb, r2) * (1.0 + 1e-6)));
         } else {
             cat = kp.matcher ? finish_plane(xf, ns, p1, t, kp, yf, nf)
-                             : finish_query<KL>(xf, ns, ed, ep, 0, min(K, cnt_r), d1, p1, t, kp, yf, nf, kq, i);
+                             : finish_query<KL, true>(xf, ns, ed, ep, 0, min(K, cnt_r), d1, p1, t, kp, yf, nf, kq, i);
             store_result(i, cat, xf, yf, nf, cs, cd, cn);
         }
     }

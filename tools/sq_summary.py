@@ -11,7 +11,7 @@ for d in sys.argv[1:]:
     per = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            name = re.sub(r"<.*", "", r.get("Kernel_Name", "")).split("(")[0].split("::")[-1]
+            name = re.sub(r"<.*", "", r.get("Kernel_Name", "")).split("::")[-1].split("(")[0].strip()
             per[(name, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     for (name, _), c in per.items():
         for n, v in c.items():
