@@ -68,6 +68,25 @@ __device__ __forceinline__ bool lessp(double da, int ia, double db, int ib) {
 // fp64 acos; inside that band, and for NaN or ca < −1 (acos → NaN → passes), as the reference.
 __device__ __forceinline__ bool angle_reject(const double ns[3], double n0, double n1, double n2, double thr,
                                              double cthr) {
+    // fp32 screen: |ca₃₂ − ca₆₄| ≤ ~1e-6 (inputs rounded to float: 6e-8 each, the dot and the two
+    // squared norms ≤ 3 ulp of their term sums, v_rsq ≤ 2 ulp — Cauchy–Schwarz bounds the dot's
+    // terms by |ns||n|), so outside ±1e-5 of cos(θ) (and of −1) the fp32 cosine decides what the
+    // fp64 evaluation below decides; squared-norm products outside [1e-20, 1e20] (denormal / huge /
+    // NaN normals) and the band go to fp64
+    {
+        const float s0 = (float)ns[0], s1 = (float)ns[1], s2 = (float)ns[2];
+        const float m0 = (float)n0, m1 = (float)n1, m2 = (float)n2;
+        const float a = __builtin_fmaf(s0, s0, __builtin_fmaf(s1, s1, s2 * s2));
+        const float b = __builtin_fmaf(m0, m0, __builtin_fmaf(m1, m1, m2 * m2));
+        const float d = __builtin_fmaf(s0, m0, __builtin_fmaf(s1, m1, s2 * m2));
+        const float ab = a * b;
+        if (ab > 1e-20f && ab < 1e20f) {
+            const float ca = d * __builtin_amdgcn_rsqf(ab);
+            const float c = (float)cthr;
+            if (ca > c + 1e-5f) return false;
+            if (ca < c - 1e-5f && ca > -1.0f + 1e-5f) return true;
+        }
+    }
     double dot = ns[0] * n0;
     dot = dot + ns[1] * n1;
     dot = dot + ns[2] * n2;

@@ -1,5 +1,5 @@
 set -u
-O=gpurun_out/r04f; mkdir -p $O
+O=gpurun_out/${RUNDIR:-r04f}; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_single -o run -- python3 bench.py --no-cpu --inflight 1 --no-fuse --steps 5 --warmup 1 --latency-pairs 5 --busy-steps 0 > $O/kt_single.out 2> $O/kt_single.err
 rc=$?; echo "kt_single rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/kt_single.err; exit $rc; }
