@@ -242,6 +242,8 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_LAZY_LISTED")) k.lazy_listed = std::atoi(w);
     k.lds_list = 1;   // measured: config B 331 → 378 pairs/s, one-pair k_knn_wave 227 → 189 µs (r04b)
     if (const char* w = std::getenv("IMLS_LDS_LIST")) k.lds_list = std::atoi(w);
+    k.qfinish = 0;
+    if (const char* w = std::getenv("IMLS_QFINISH")) k.qfinish = std::atoi(w);
     // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
     // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)
     k.tv = (p.use_tensor_voting && !p.get_normals && p.matching_method == IMLS_MATCH_IMLS) ? 1 : 0;

@@ -67,6 +67,7 @@ struct KParams {
     int kl20;                 // list length (K + slack) used for search_number 17..20: 22 (default), 24 or 26
     int lazy_listed;          // packet traversal: listed-point masks only for leaves with more candidates than listed points
     int lds_list;             // packet traversal: slot-id keys in registers, list positions in LDS (project.hip IdKeys)
+    int qfinish;              // one-frame launches with the wave-per-query traversal: exact stage one wave per query
     int xcd;                  // batched projection: frames grouped per XCD round-robin slot (−1 auto: ≥ 16 frames)
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
     int tv;                   // tensor-voting normals (use_tensor_voting && !get_normals, IMLS matcher)

@@ -1357,6 +1357,213 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
 }
 
 // =============================================================================================
+// Exact stage, one WAVE per query (a small frame registered alone — the config C/D deployment
+// shape, ≤ kQwaveAutoN queries — where k_finish's one-lane-per-query latency chain (~30 µs per
+// launch for 2000 queries in 8 blocks) sets the frame latency): lane j holds list entry j, so the
+// gathers, the exact distances, the gates and the IMLS weights run across the lanes.  Every value is
+// computed by the same expression as k_finish's lane code, the list order is the same (d², index)
+// total order (each lane's rank by counting), the IMLS sums accumulate in that order (lane 0 reads
+// each term in turn) — the correspondences are the lane kernel's bit for bit.  cd[i].w carries the
+// query's category (−1 valid, reject category, −3 deferred) to k_finish_slab, which reduces the
+// pass-1 normal equations per 256-slot block exactly as k_finish does (same slot → thread map,
+// same block_normeq) and counts the rejects.
+// =============================================================================================
+__device__ __forceinline__ double rl_f64(double x, int l) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+template <int KL>
+__device__ __forceinline__ void finish_q_body(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
+                                              const unsigned* __restrict__ qperm, int N, const double* __restrict__ pose,
+                                              const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
+                                              const float* __restrict__ wlist, float4* __restrict__ cs,
+                                              float4* __restrict__ cd, float4* __restrict__ cn,
+                                              unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
+                                              unsigned* __restrict__ fb_count, int bx) {
+    static_assert(KL <= 64, "one list entry per lane");
+    if (done && *done) return;
+    const int lane = threadIdx.x & 63;
+    const int slot = __builtin_amdgcn_readfirstlane(bx * (kWaveBlock / 64) + (int)(threadIdx.x >> 6));
+    if (slot >= N) return;
+    const int i = (int)qperm[slot];
+    float xf[3];
+    double ns[3];
+    transform_query(pose, spt[i], snr[i], kp.transform_normal, xf, ns);
+    const double xd[3] = {xf[0], xf[1], xf[2]};
+    const float W = wlist[slot];
+    const bool ent = lane < KL;
+    const int pos = ent ? lists[(size_t)lane * N + slot] : -1;
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    double ed = kInfD;
+    int eo = 0x7fffffff;
+    if (pos >= 0) {
+        q = t.mpt[pos];
+        ed = exact_d2(xd, q.x, q.y, q.z);
+        eo = (int)__float_as_uint(q.w);
+    }
+    // rank in the (d², index) order (k_finish's sort); empty entries after the real ones, by lane
+    int rank = 0;
+#pragma unroll
+    for (int k = 0; k < KL; ++k) {
+        const double dk = rl_f64(ed, k);
+        const int ok = __builtin_amdgcn_readlane(eo, k);
+        rank += (dk < ed || (dk == ed && (ok < eo || (ok == eo && k < lane)))) ? 1 : 0;
+    }
+    auto lane_of_rank = [&](int r) -> int {
+        const unsigned long long m = __ballot(ent && rank == r);
+        return m ? (int)__builtin_ctzll(m) : -1;
+    };
+    const double r2 = kp.r2;
+    const int K = kp.K;
+    const bool in = ent && ed <= r2;
+    const int cnt_r = __popcll(__ballot(in));
+    // NN-1: the first entry in order within r with d² > DBL_EPSILON (no self match)
+    int r1 = (in && ed > DBL_EPSILON) ? rank : 0x7fffffff;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) r1 = min(r1, __shfl_xor(r1, o, 64));
+    const int l1 = r1 < 0x7fffffff ? lane_of_rank(r1) : -1;
+    const double d1 = l1 >= 0 ? rl_f64(ed, l1) : kInfD;
+    const int p1 = l1 >= 0 ? __builtin_amdgcn_readlane(pos, l1) : -1;
+    const int lK = lane_of_rank(K - 1);
+    const double dK = lK >= 0 ? rl_f64(ed, lK) : 0.0;
+    const bool full = W < kInfF;
+    double need = cnt_r >= K ? dK : r2;
+    bool cert = true;
+    if (full) {
+        if (l1 < 0) cert = false;
+        else need = fmax(need, d1);
+        cert = cert && (need < (double)W / kCertSlack);
+    }
+    if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_FORCE_FALLBACK)
+    int cat = -1, kq = 0;
+    float yf[3] = {0.f, 0.f, 0.f}, nf[3] = {0.f, 0.f, 0.f};
+    if (!cert) {
+        if (lane == 0) {
+            const unsigned at = atomicAdd(fb_count, 1u);
+            fb_list[at] = (unsigned)i;
+            const double lb = l1 < 0 ? r2 : fmax(cnt_r >= K ? dK : r2, d1);
+            cs[i] = make_float4(0.f, 0.f, 0.f, (float)(fmin(lb, r2) * (1.0 + 1e-6)));
+            cd[i] = make_float4(0.f, 0.f, 0.f, -3.f);
+        }
+        return;
+    }
+    if (kp.matcher) {
+        cat = finish_plane(xf, ns, p1, t, kp, yf, nf);
+    } else {
+        // finish_query, entry j of the ordered list = the lane of rank j
+        const int cnt = min(K, cnt_r);
+        double nn[3] = {0.0, 0.0, 0.0};
+        if (p1 < 0 || d1 > kp.h2) {
+            cat = IMLS_REJ_TOO_FAR;                             // imls_icp.cpp:612-625 (Q18)
+        } else if (kp.tv) {
+            const double4 v = t.tvn[i];
+            if (v.w == 0.0) cat = IMLS_REJ_NO_NORMAL;
+            nn[0] = v.x; nn[1] = v.y; nn[2] = v.z;
+        } else if (!kp.get_normals) {
+            cat = IMLS_REJ_INVALID_NORMAL;
+        } else {
+            const float4 n4 = t.mnr[p1];
+            nn[0] = n4.x; nn[1] = n4.y; nn[2] = n4.z;
+        }
+        if (cat == -1 && !(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) cat = IMLS_REJ_INVALID_NORMAL;
+        if (cat == -1 && kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg, kp.cos_thr))
+            cat = IMLS_REJ_NORMAL_CONSTRAINT;
+        if (cat == -1) {
+            const bool inl = ent && rank < cnt;
+            kq = cnt;
+            float4 qn = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (inl) qn = t.mnr[pos];
+            bool ok = inl && kp.get_normals && isfinite(qn.x) && isfinite(qn.y) && isfinite(qn.z);
+            if (ok && kp.angle_on) ok = !angle_reject(ns, qn.x, qn.y, qn.z, kp.angle_thr_deg, kp.cos_thr);
+            const unsigned long long accm = __ballot(ok);
+            const int nacc = __popcll(accm);
+            if (nacc < 3) {
+                cat = IMLS_REJ_MLS_FAIL;                        // imls_icp.cpp:463-466
+            } else {
+                const int lt = lane_of_rank(nacc - 1);          // Q3: L[|S| − 1]
+                const double hmax = sqrt(rl_f64(ed, lt)) / 3;
+                double w = 0.0, pr = 0.0;
+                if (ok) {
+                    const double dx = xd[0] - (double)q.x, dy = xd[1] - (double)q.y, dz = xd[2] - (double)q.z;
+                    double dn = dx * dx;
+                    dn = dn + dy * dy;
+                    dn = dn + dz * dz;
+                    w = exp(-dn / hmax / hmax);
+                    pr = (w * dx) * (double)qn.x;
+                    pr = pr + (w * dy) * (double)qn.y;
+                    pr = pr + (w * dz) * (double)qn.z;
+                }
+                // Σ in list order, as the lane code accumulates
+                double wsum = 0.0, psum = 0.0;
+                for (int r = 0; r < cnt; ++r) {
+                    const int l = lane_of_rank(r);
+                    if ((accm >> l) & 1ull) {
+                        wsum += rl_f64(w, l);
+                        psum += rl_f64(pr, l);
+                    }
+                }
+                const double height = psum / (wsum + 1e-5);     // Q4
+                if (isnan(height) || isinf(height)) {
+                    cat = IMLS_REJ_NAN_INF_HEIGHT;
+                } else {
+                    yf[0] = (float)(xd[0] - height * nn[0]);    // imls_icp.cpp:719-729
+                    yf[1] = (float)(xd[1] - height * nn[1]);
+                    yf[2] = (float)(xd[2] - height * nn[2]);
+                    nf[0] = (float)nn[0]; nf[1] = (float)nn[1]; nf[2] = (float)nn[2];
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        store_result(i, cat, xf, yf, nf, cs, cd, cn);
+        // the category for k_finish_slab in cd.w (y's row is read only behind cs.w's valid flag)
+        cd[i] = cat == -1 ? make_float4(yf[0], yf[1], yf[2], -1.f) : make_float4(0.f, 0.f, 0.f, (float)cat);
+        if (nbr_stats) {
+            if (kq) atomicAdd(&nbr_stats[0], (unsigned long long)kq);
+            if (l1 >= 0) atomicAdd(&nbr_stats[1], 1ull);
+        }
+    }
+}
+
+// pass-1 normal equations + reject counters of k_finish_q's queries, per 256-slot block as k_finish
+__device__ __forceinline__ void finish_slab_body(const unsigned* __restrict__ qperm, int N, const int* __restrict__ done,
+                                                 const float4* __restrict__ cs, const float4* __restrict__ cd,
+                                                 const float4* __restrict__ cn, double* __restrict__ partial1,
+                                                 imls_iter_trace* __restrict__ tr,
+                                                 unsigned long long* __restrict__ nbr_stats, int bx) {
+    if (done && *done) return;
+    __shared__ double red[kWaveBlock / 64][kNormEq];
+    __shared__ double out[kNormEq];
+    __shared__ unsigned rej_s[IMLS_NUM_REJ + 1];
+    const int tid = threadIdx.x;
+    if (tid < IMLS_NUM_REJ + 1) rej_s[tid] = 0;
+    __syncthreads();
+    const int slot = bx * kWaveBlock + tid;
+    int cat = -2;
+    double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
+    if (slot < N) {
+        const int i = (int)qperm[slot];
+        const float4 d4 = cd[i];
+        cat = (int)d4.w;
+        if (cat == -1) {
+            const float4 s4 = cs[i], n4 = cn[i];
+            const float xf[3] = {s4.x, s4.y, s4.z}, yf[3] = {d4.x, d4.y, d4.z}, nf[3] = {n4.x, n4.y, n4.z};
+            plane_row(xf, yf, nf, a, bb);
+            one = 1.0;
+        }
+    }
+    if (cat >= 0) atomicAdd(&rej_s[cat], 1u);
+    if (cat == -3) atomicAdd(&rej_s[IMLS_NUM_REJ], 1u);
+    block_normeq<kWaveBlock>(a, bb, one, red, out);
+    if (tid < kNormEq) partial1[(size_t)bx * kNormEq + tid] = out[tid];
+    if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
+    if (nbr_stats && tid == IMLS_NUM_REJ && rej_s[tid]) atomicAdd(&nbr_stats[5], (unsigned long long)rej_s[tid]);
+}
+
+// =============================================================================================
 // Per-lane exact traversal (fallback for uncertified queries; IMLS_TRAVERSAL=lane mode)
 // =============================================================================================
 template <int KCAP>
@@ -1559,6 +1766,23 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(
                     fb_count, (int)blockIdx.x);
 }
 
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) void k_finish_q(
+        TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qperm,
+        int N, const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
+        const float* __restrict__ wlist, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
+        unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list, unsigned* __restrict__ fb_count) {
+    finish_q_body<KL>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, nbr_stats, fb_list, fb_count,
+                      (int)blockIdx.x);
+}
+__global__ __launch_bounds__(kWaveBlock) void k_finish_slab(const unsigned* __restrict__ qperm, int N,
+                                                            const int* __restrict__ done, const float4* __restrict__ cs,
+                                                            const float4* __restrict__ cd, const float4* __restrict__ cn,
+                                                            double* __restrict__ partial1, imls_iter_trace* __restrict__ tr,
+                                                            unsigned long long* __restrict__ nbr_stats) {
+    finish_slab_body(qperm, N, done, cs, cd, cn, partial1, tr, nbr_stats, (int)blockIdx.x);
+}
+
 template <int KCAP>
 __global__ __launch_bounds__(kProjBlock) void k_project_lane(
         TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qlist,
@@ -1702,8 +1926,15 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
         k_knn_wave<KL, false, false><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
                                                            nref, use_prev, stats, fb_count);
     if (marks) (void)hipEventRecord(marks[1], s);
-    k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr,
-                                               stats, fb_list, fb_count);
+    if (use_qwave(kp, N) && kp.qfinish) {
+        // a small frame alone: the exact stage one wave per query, then the per-block reduction
+        k_finish_q<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(
+            t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, stats, fb_list, fb_count);
+        k_finish_slab<<<blocks, kWaveBlock, 0, s>>>(qperm, N, done, cs, cd, cn, partial1, tr, stats);
+    } else {
+        k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1,
+                                                   tr, stats, fb_list, fb_count);
+    }
     if (marks) (void)hipEventRecord(marks[2], s);
 }
 

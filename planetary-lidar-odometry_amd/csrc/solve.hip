@@ -467,7 +467,9 @@ __device__ __forceinline__ void solve_final_body(const Rows& rows, int N, const 
 // LDS, bitonic sort by (|r| bits, row), ranks [lo, hi] re-reduced, second solve, pose update —
 // instead of five launches whose fixed latency dominates at this size.  Same arithmetic and the
 // same exact (|r|, row) order as the chain.
-constexpr int kSmallBlock = 256;     // 4 waves: cheap barriers for the sort and reductions
+constexpr int kSmallBlock = 512;     // 8 waves: ≤ kSmallPer rows per thread, kept in registers between passes
+constexpr int kSmallPer = kSmallRows / kSmallBlock;
+static_assert(kSmallRows % kSmallBlock == 0, "rows per thread");
 constexpr unsigned long long kNoKey = ~0ull;   // k_solve_small: slot of an invalid row
 constexpr int kSmallBins = 4096;     // LDS histogram: top 12 bits of the float image of |r| (1/16 octave)
 __device__ __forceinline__ int small_bin(unsigned long long keybits) {
@@ -479,6 +481,27 @@ __device__ unsigned long long g_dbg_solve[8];
 #else
 #define DBG_STAMP(k) do { } while (0)
 #endif
+// the row of a float correspondence as Rows::get builds it (solver.cpp:95-103), from its floats
+__device__ __forceinline__ void small_a(const float4& s4, const float4& n4, double a[6]) {
+    const double s[3] = {s4.x, s4.y, s4.z}, n[3] = {n4.x, n4.y, n4.z};
+    a[0] = n[2] * s[1] - n[1] * s[2];
+    a[1] = n[0] * s[2] - n[2] * s[0];
+    a[2] = n[1] * s[0] - n[0] * s[1];
+    a[3] = n[0]; a[4] = n[1]; a[5] = n[2];
+}
+__device__ __forceinline__ double small_b(const float4& s4, const float4& d4, const float4& n4) {
+    const double s[3] = {s4.x, s4.y, s4.z}, d[3] = {d4.x, d4.y, d4.z}, n[3] = {n4.x, n4.y, n4.z};
+    double b = n[0] * (d[0] - s[0]);
+    b = b + n[1] * (d[1] - s[1]);
+    b = b + n[2] * (d[2] - s[2]);
+    return b;
+}
+// (round 4) 512 threads, each owning rows t + k·512: each row's s, n and b stay in registers from the
+// residual pass to the kept-row sums (no second gather), valid rows are counted by wave ballots,
+// the histogram scan is a wave-shuffle block scan and the boundary candidates are ranked by
+// counting (rank_sort) — the phases were latency chains of 256 threads × 8 rows (31 µs per solve on
+// a 1949-row frame, tools/frame_probe.py).  Float rows only (the projection's; RANSAC rows take
+// the grid chain).
 __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const double* __restrict__ partial, int blocks,
                                                  const SolveState& st, imls_iter_trace* tr, const KParams& kp,
                                                  int weighted, int update_pose) {
@@ -487,11 +510,10 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     long long dbg_t = wall_clock64();
 #endif
     __shared__ unsigned long long ck[kSmallRows];
-    __shared__ unsigned cr[kSmallRows];
     __shared__ unsigned long long qk[kSmallRows];
     __shared__ unsigned qr[kSmallRows];
     __shared__ unsigned hist[kSmallBins];
-    __shared__ unsigned csum[kSmallBlock];
+    __shared__ unsigned wsum[kSmallBlock / 64];
     __shared__ int bsel[5];
     __shared__ int ncand;
     __shared__ double red[(kSmallBlock / 64) * kNormEq];
@@ -499,7 +521,7 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     __shared__ double xs[6];
     __shared__ int nkey;
     __shared__ int stop;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63;
     double loc[kNormEq];
 #pragma unroll
     for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
@@ -507,6 +529,19 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
 #pragma unroll
         for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
     if (t == 0) { nkey = 0; stop = 0; }
+    // this thread's rows, loaded now (their latency overlaps the reduction and the first solve):
+    // s (w = valid flag), n, and b = n·(d − s)
+    float4 rs[kSmallPer], rn[kSmallPer];
+    double rb[kSmallPer];
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {
+        const int r = t + k * kSmallBlock;
+        rs[k] = r < N ? rows.cs[r] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool v = r < N && rs[k].w != 0.f;
+        const float4 d4 = v ? rows.cd[r] : make_float4(0.f, 0.f, 0.f, 0.f);
+        rn[k] = v ? rows.cn[r] : make_float4(0.f, 0.f, 0.f, 0.f);
+        rb[k] = small_b(rs[k], d4, rn[k]);
+    }
     block_sum28<kSmallBlock>(loc, red, acc);
     DBG_STAMP(0);
     const double nvalid = acc[27];
@@ -532,20 +567,25 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     DBG_STAMP(1);
     if (stop) return;
     // |r| under the first solution, valid rows only (solver.cpp:110-122).  Keys stay at their row's
-    // slot (invalid rows hold a sentinel) so every later pass walks the rows in a fixed order: the
-    // second reduction's float sums are then the same run to run (an append order would not be)
-    for (int i = t; i < N; i += kSmallBlock) {
-        double a[6], b, wt;
+    // slot (invalid rows hold a sentinel) so every later pass walks the rows in a fixed order
+    int mine = 0;
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {
+        const int r = t + k * kSmallBlock;
+        const bool v = r < N && rs[k].w != 0.f;
         unsigned long long kb = kNoKey;
-        if (rows.get(i, a, b, wt)) {
-            double v = a[0] * xs[0];
-            for (int k = 1; k < 6; ++k) v = v + a[k] * xs[k];
-            kb = (unsigned long long)__double_as_longlong(fabs(v - b));
-            atomicAdd(&nkey, 1);
+        if (v) {
+            double a[6];
+            small_a(rs[k], rn[k], a);
+            double val = a[0] * xs[0];
+            for (int q = 1; q < 6; ++q) val = val + a[q] * xs[q];
+            kb = (unsigned long long)__double_as_longlong(fabs(val - rb[k]));
         }
-        ck[i] = kb;
-        cr[i] = (unsigned)i;
+        if (r < N) ck[r] = kb;
+        mine += __popcll(__ballot(v));
     }
+    if (lane == 0 && mine) atomicAdd(&nkey, mine);
+    for (int b = t; b < kSmallBins; b += kSmallBlock) hist[b] = 0u;
     __syncthreads();
     DBG_STAMP(2);
     const int n = nkey;
@@ -557,25 +597,21 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
         return;                       // n, lo, hi are block-uniform: every thread leaves here
     }
     // exact ranks at the two trim boundaries: a 4096-bin LDS histogram of the float image of |r|
-    // (monotone) locates the boundary bins; only their rows are sorted by (|r| bits, row)
-    for (int b = t; b < kSmallBins; b += kSmallBlock) hist[b] = 0u;
-    __syncthreads();
-    for (int r = t; r < N; r += kSmallBlock)
-        if (ck[r] != kNoKey) atomicAdd(&hist[small_bin(ck[r])], 1u);
+    // (monotone) locates the boundary bins; only their rows are ordered by (|r| bits, row)
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {
+        const int r = t + k * kSmallBlock;
+        if (r < N && ck[r] != kNoKey) atomicAdd(&hist[small_bin(ck[r])], 1u);
+    }
     __syncthreads();
     {
         constexpr int per = kSmallBins / kSmallBlock;
         unsigned loc_sum = 0;
+#pragma unroll
         for (int k = 0; k < per; ++k) loc_sum += hist[t * per + k];
-        csum[t] = loc_sum;
-        __syncthreads();
-        for (int off = 1; off < kSmallBlock; off <<= 1) {
-            const unsigned v = t >= off ? csum[t - off] : 0u;
-            __syncthreads();
-            csum[t] += v;
-            __syncthreads();
-        }
-        long long cum = (long long)csum[t] - loc_sum;
+        unsigned total;
+        long long cum = block_exscan<kSmallBlock>(loc_sum, wsum, &total);
+#pragma unroll
         for (int k = 0; k < per; ++k) {
             const long long c = hist[t * per + k];
             if (lo >= cum && lo < cum + c) { bsel[0] = t * per + k; bsel[2] = (int)cum; }
@@ -587,48 +623,59 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     __syncthreads();
     const int blo = bsel[0], bhi = bsel[1];
     if (t == 0) bsel[4] = (int)hist[blo];           // candidates of the lower boundary bin
-    for (int r = t; r < N; r += kSmallBlock) {
-        if (ck[r] == kNoKey) continue;
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {
+        const int r = t + k * kSmallBlock;
+        if (r >= N || ck[r] == kNoKey) continue;
         const int b = small_bin(ck[r]);
         if (b == blo || b == bhi) {
             const int at = atomicAdd(&ncand, 1);
             qk[at] = ck[r];
-            qr[at] = cr[r];
+            qr[at] = (unsigned)r;
         }
     }
     __syncthreads();
     const int nc = ncand;
-    int np = 1;
-    while (np < nc) np <<= 1;
-    for (int i = nc + t; i < np; i += kSmallBlock) { qk[i] = ~0ull; qr[i] = ~0u; }
-    __syncthreads();
-    bitonic(qk, qr, np);
+    if (nc <= kRankSortMax) {
+        rank_sort(qk, qr, nc);
+    } else {
+        int np = 1;
+        while (np < nc) np <<= 1;
+        for (int i = nc + t; i < np; i += kSmallBlock) { qk[i] = ~0ull; qr[i] = ~0u; }
+        __syncthreads();
+        bitonic(qk, qr, np);
+    }
     DBG_STAMP(3);
 #pragma unroll
     for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
-    auto add_row = [&](unsigned row) {
-        double a[6], b, wt;
-        rows.get((int)row, a, b, wt);
-        int k = 0;
+    auto add_row = [&](const double (&a)[6], double b) {
+        int q = 0;
         for (int p = 0; p < 6; ++p)
-            for (int c = p; c < 6; ++c) loc[k++] += a[p] * a[c];
+            for (int c = p; c < 6; ++c) loc[q++] += a[p] * a[c];
         for (int p = 0; p < 6; ++p) loc[21 + p] += a[p] * b;
         loc[27] += 1.0;
     };
-    for (int r = t; r < N; r += kSmallBlock) {     // interior bins: kept without ranking, row order
-        if (ck[r] == kNoKey) continue;
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {           // interior bins: kept without ranking (registers)
+        const int r = t + k * kSmallBlock;
+        if (r >= N || ck[r] == kNoKey) continue;
         const int b = small_bin(ck[r]);
-        if (b > blo && b < bhi) add_row(cr[r]);
+        if (b > blo && b < bhi) {
+            double a[6];
+            small_a(rs[k], rn[k], a);
+            add_row(a, rb[k]);
+        }
     }
     for (int q = t; q < nc; q += kSmallBlock) {    // boundary bins: exact rank = bin base + order
         const int b = small_bin(qk[q]);
         int first = 0;                              // first candidate of this bin in sorted order
-        if (b == bhi && bhi != blo) {
-            // candidates of blo sort before those of bhi: count them
-            first = bsel[4];
-        }
+        if (b == bhi && bhi != blo) first = bsel[4];  // candidates of blo sort before those of bhi
         const long long rank = (long long)(b == blo ? bsel[2] : bsel[3]) + (q - first);
-        if (rank >= lo && rank <= hi) add_row(qr[q]);
+        if (rank >= lo && rank <= hi) {
+            double a[6], bb, wt;
+            rows.get((int)qr[q], a, bb, wt);
+            add_row(a, bb);
+        }
     }
     block_sum28<kSmallBlock>(loc, red, acc);
     DBG_STAMP(4);
