@@ -219,10 +219,12 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_WAVE_TRACE")) k.wave_trace = std::atoi(w);
     k.wide = 3;
     if (const char* w = std::getenv("IMLS_WIDE")) k.wide = std::max(1, std::min(3, std::atoi(w)));
-    // Verlet-list reuse: on for the packet traversal; off for the wave-per-query traversal, where the
-    // config C-like stream measured 0.109 ms per launch without vs 0.141 ms with it (4 in flight)
+    // Verlet-list reuse: on for the packet traversal; the wave-per-query traversal had it off while the
+    // config C-like stream ran on it (0.109 ms per launch without vs 0.141 ms with it, 4 in flight)
     k.verlet = 1;
-    k.qverlet = 0;
+    // (round 4) on for the wave-per-query traversal too: it now serves lone small frames (latency) and
+    // batches under kQwaveAutoN queries only — a lone 1949-query frame 1.95 -> 1.84 ms
+    k.qverlet = 1;
     if (const char* w = std::getenv("IMLS_VERLET")) k.verlet = k.qverlet = std::atoi(w);
     if (const char* w = std::getenv("IMLS_QVERLET")) k.qverlet = std::atoi(w);
     k.verlet2 = k.verlet;

@@ -164,8 +164,9 @@ __device__ inline int solve6(const double* ne, double x[6]) {
                 stop = true;
             } else {
                 A[j][j] = rkk;
+                const double inv = 1.0 / rkk;   // one division per pivot (round 4: the column scaled by it)
 #pragma unroll
-                for (int r = j + 1; r < 6; ++r) A[r][j] = A[r][j] / rkk;
+                for (int r = j + 1; r < 6; ++r) A[r][j] = A[r][j] * inv;
 #pragma unroll
                 for (int r = j + 1; r < 6; ++r)
 #pragma unroll
