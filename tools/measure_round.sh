@@ -19,6 +19,8 @@ if [ $P1 = 1 ]; then
 [ "${SKIP_TESTS:-0}" = 1 ] || step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step bench_B 600 python3 bench.py
 step bench_stream 300 python3 bench.py --workload stream
+step bench_B_host 400 python3 bench.py --host-inputs --no-cpu
+step bench_B_q2000 400 python3 bench.py --queries 2000
 fi
 if [ $P2 = 1 ]; then
 step bench_stream_host 300 python3 bench.py --workload stream --no-cpu --host-inputs
@@ -32,6 +34,8 @@ step kt_driver 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt
 f=$(find $O/kt_driver -name '*kernel_trace.csv' | head -1)
 python3 tools/trace_frac.py $f $O/kt_driver.out > $O/kt_driver_frac.json && cat $O/kt_driver_frac.json
 step kt_single 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_single -o run -- python3 bench.py --no-cpu --inflight 1 --no-fuse --steps 5 --warmup 1
+f=$(find $O/kt_single -name '*kernel_trace.csv' | head -1)
+python3 tools/iter_profile.py $f > $O/per_iteration_single_pair.txt && cat $O/per_iteration_single_pair.txt
 for c in FETCH_SIZE WRITE_SIZE; do
   step pmc_$c 300 rocprofv3 --kernel-trace --kernel-include-regex 'k_knn_wave|k_finish' --output-format csv \
       --pmc $c -d $O/pmc_$c -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --inflight 1 --no-fuse --latency-pairs 3
