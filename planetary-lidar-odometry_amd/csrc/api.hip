@@ -247,6 +247,10 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_LDS_LIST")) k.lds_list = std::atoi(w);
     k.qfinish = 1;   // measured: a lone 1949-query frame 2.21 -> 1.95 ms (k_finish 30 -> 16.7 us per iteration)
     if (const char* w = std::getenv("IMLS_QFINISH")) k.qfinish = std::atoi(w);
+    k.qfuse = 1;
+    if (const char* w = std::getenv("IMLS_QFUSE")) k.qfuse = std::atoi(w);
+    k.bottom_up = 1;
+    if (const char* w = std::getenv("IMLS_BOTTOM_UP")) k.bottom_up = std::atoi(w);
     // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
     // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)
     k.tv = (p.use_tensor_voting && !p.get_normals && p.matching_method == IMLS_MATCH_IMLS) ? 1 : 0;
@@ -292,6 +296,9 @@ int ensure_solve(imls_ctx* c, int N) {
     n += n / 4 + 64;                      // headroom (see grow): the next frames' N differ a little
     if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, n * 4 + 256))
         return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
+    // deferred-query counter [0] and the fallback's arrival counter [1]: zero from here on (the
+    // launches that use them leave them zero)
+    if (hipMemsetAsync(c->fb.p, 0, 256, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipMemset (fb)");
     if (!grow(c->prevnn, prevnn_bytes((int)n))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
     if (!grow(c->tvn, n * kTvBytesPerQuery)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tvn)");
     const int pb = std::max(project_blocks((int)n), solve_blocks((int)n)) + 1;
@@ -953,6 +960,29 @@ int check_device(imls_ctx* c) {
     return IMLS_OK;
 }
 
+// One frame's prologue / epilogue as one launch each (round 4: the lone-frame latency paid ~11 µs
+// for an H2D pose copy, five fills and four D2H copies around the 20 iterations).
+__global__ void k_frame_init(double* __restrict__ pose, int* __restrict__ done, int* __restrict__ status,
+                             int* __restrict__ iters, unsigned long long* __restrict__ trace, int trace_words,
+                             unsigned long long* __restrict__ stats) {
+    const int t = threadIdx.x;
+    if (t < 16) pose[t] = (t % 5 == 0) ? 1.0 : 0.0;
+    if (t < 4) { done[t] = 0; status[t] = 0; iters[t] = 0; }
+    if (t < 16) stats[t] = 0ull;
+    for (int k = t; k < trace_words; k += blockDim.x) trace[k] = 0ull;
+}
+// pose, iterations, status and the trace records written straight into the pinned host buffers
+// (device-visible host memory; read by the host after the stream synchronisation)
+__global__ void k_frame_results(const double* __restrict__ pose, const int* __restrict__ iters,
+                                const int* __restrict__ status, const unsigned long long* __restrict__ trace,
+                                int trace_words, double* __restrict__ h_misc, unsigned long long* __restrict__ h_trace) {
+    const int t = threadIdx.x;
+    if (t < 16) h_misc[t] = pose[t];
+    if (t == 16) reinterpret_cast<int*>(h_misc + 16)[0] = *iters;
+    if (t == 17) reinterpret_cast<int*>(h_misc + 18)[0] = *status;
+    for (int k = t; k < trace_words; k += blockDim.x) h_trace[k] = trace[k];
+}
+
 }  // namespace
 
 extern "C" {
@@ -1437,13 +1467,10 @@ int imls_register_frame_async(imls_ctx* c) {
     const int iters = c->P.iterations;
     if (int rc = ensure_trace(c, iters)) return rc;
     if (!grow(c->stats, 128)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc");
-    static const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-    hipMemcpyAsync(c->st.pose, I, sizeof(I), hipMemcpyHostToDevice, c->stream);
-    hipMemsetAsync(c->st.done, 0, 16, c->stream);
-    hipMemsetAsync(c->st.status, 0, 16, c->stream);
-    hipMemsetAsync(c->st.iters, 0, 16, c->stream);
-    hipMemsetAsync(c->trace_mem.p, 0, (size_t)std::max(iters, 1) * sizeof(imls_iter_trace), c->stream);
-    hipMemsetAsync(c->stats.p, 0, 128, c->stream);
+    const int trace_words = std::max(iters, 1) * (int)(sizeof(imls_iter_trace) / 8);
+    k_frame_init<<<1, 256, 0, c->stream>>>(c->st.pose, c->st.done, c->st.status, c->st.iters,
+                                           (unsigned long long*)c->trace_mem.p, trace_words,
+                                           (unsigned long long*)c->stats.p);
     imls_iter_trace* tr = (imls_iter_trace*)c->trace_mem.p;
     if (int rc = ensure_map_normals(c)) return rc;
     const TreeView tv = tree_view(c);
@@ -1478,11 +1505,9 @@ int imls_register_frame_async(imls_ctx* c) {
         launch_solve(c->stream, solve_launch(c, tr + it, 1));
         timed_end(c, 2, slot);
     }
-    hipMemcpyAsync(c->h_misc, c->st.pose, 16 * 8, hipMemcpyDeviceToHost, c->stream);
-    hipMemcpyAsync(c->h_misc + 16, c->st.iters, 16, hipMemcpyDeviceToHost, c->stream);
-    hipMemcpyAsync(c->h_misc + 18, c->st.status, 4, hipMemcpyDeviceToHost, c->stream);
-    if (iters > 0)
-        hipMemcpyAsync(c->h_trace, tr, (size_t)iters * sizeof(imls_iter_trace), hipMemcpyDeviceToHost, c->stream);
+    k_frame_results<<<1, 256, 0, c->stream>>>(c->st.pose, c->st.iters, c->st.status, (const unsigned long long*)tr,
+                                              iters * (int)(sizeof(imls_iter_trace) / 8), c->h_misc,
+                                              (unsigned long long*)c->h_trace);
     if (hipGetLastError() != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "launch failed");
     c->pending = true;
     c->pending_iters = iters;

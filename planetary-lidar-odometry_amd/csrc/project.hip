@@ -1013,7 +1013,23 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
 // loads, a leaf is one coalesced load with one point per lane, an insertion is a ballot + shuffle.
 // Output contract identical to k_knn_wave (positions [KL][N], worst key W per query).
 // =============================================================================================
+// FUSED (k_knn_qwave_f, a small frame alone): the wave goes on to the exact stage of its query
+// (finish_q_core) with the list still in its lanes; the deferred-query counter is then reset by the
+// fallback launch (project_lane_body's fb_reset), not here.  Extra arguments unused otherwise.
 template <int KL>
+__device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
+                                              int i, int slot, const double* __restrict__ pose, const KParams& kp,
+                                              int pos, float W, float4* __restrict__ cs, float4* __restrict__ cd,
+                                              float4* __restrict__ cn, imls_iter_trace* __restrict__ tr,
+                                              unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
+                                              unsigned* __restrict__ fb_count);
+struct QFinishArgs {
+    const float4* snr;
+    float4 *cs, *cd, *cn;
+    imls_iter_trace* tr;
+    unsigned* fb_list;
+};
+template <int KL, bool FUSED = false>
 __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restrict__ spt,
                                                           const unsigned* __restrict__ qperm, int N,
                                                           const double* __restrict__ pose,
@@ -1022,7 +1038,8 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
                                                           int* __restrict__ lists, float* __restrict__ wlist,
                                                           float4* __restrict__ xref, float* __restrict__ nref,
                                                           int use_prev, unsigned long long* __restrict__ nbr_stats,
-                                                          unsigned* __restrict__ fb_count, int bx) {
+                                                          unsigned* __restrict__ fb_count, int bx,
+                                                          const QFinishArgs& fa = QFinishArgs{}) {
     static_assert(KL <= 64, "one list entry per lane");
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
@@ -1058,7 +1075,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         bnd = fminf(hmode ? h2s : r2s, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), KL - 1)));
     };
     auto worst = [&]() { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), KL - 1)); };
-    int seed_lo = 0, seed_hi = -1;
+    int seed_lo = 0, seed_hi = -1, seed_leaf = -1;
     bool greedy = !use_prev;
     bool skip = false;
     float wskip = kInfF;
@@ -1104,6 +1121,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         }
         seed_lo = max(0, lo - kp.seed_half);
         seed_hi = min(t.L - 1, lo + kp.seed_half);
+        seed_leaf = lo;
         for (int leaf = seed_lo; leaf <= seed_hi; ++leaf) {
             const int base = leaf * B, cnt = min(B, M - base);
             float d = kInfF;
@@ -1129,7 +1147,37 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         bnd = fminf(bnd, h2s);
     }
     for (int pass = 0; pass < 2; ++pass) {
-    int node = skip ? 0 : 1, sp = 0;
+    int node = 0, sp = 0;
+    if (!skip) {
+        // bottom-up start (round 4): the start leaf — the query's Morton leaf (greedy) or the leaf of
+        // its nearest listed point — and the boxes of the siblings along its root path in ONE
+        // parallel load (lane k: the sibling of the leaf's ancestor k levels up; a node's box sits in
+        // its parent's record).  The leaf and those siblings' subtrees partition the tree, so every
+        // sibling within the bound is stacked (nearest level on top) and the walk begins at the leaf:
+        // the same leaves are reachable as from the root, without the ⌈levels/3⌉ dependent descent
+        const int p0 = __builtin_amdgcn_readfirstlane(lpos);
+        const int sl = greedy ? seed_leaf : (p0 >= 0 ? p0 / B : -1);
+        node = 1;
+        if (sl >= 0 && kp.bottom_up) {
+            const int ln = P + sl;
+            float d = kInfF;
+            int sn = 0;
+            if (lane < t.levels) {
+                sn = (ln >> lane) ^ 1;
+                const float4* rec = t.nodes + 3 * (size_t)(sn >> 1);
+                const float4 a = rec[0], b = rec[1], c = rec[2];
+                d = (sn & 1) ? box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w) : box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+            }
+            const unsigned long long want = __ballot(lane < t.levels && d <= bnd * kBoxSlack);
+            if ((want >> lane) & 1ull) {
+                const int at = __popcll(want >> (lane + 1));
+                snode[wv][at] = sn;
+                sdist[wv][at] = d;
+            }
+            sp = __popcll(want);
+            node = ln;
+        }
+    }
     while (node) {
         if (node < P) {
             // one step descends `sw` binary levels: lane k tests the box of descendant k (the 2^sw
@@ -1227,10 +1275,17 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
         atomicAdd(&nbr_stats[4], 1ull);
     }
-    // k_finish's deferred-query counter, zeroed at the END of the kernel: a global store ahead
-    // of the traversal may-clobbers every later load, and the node records are then fetched by
-    // vector loads instead of through the scalar cache
-    if (bx == 0 && threadIdx.x == 0) *fb_count = 0u;
+    if constexpr (FUSED) {
+        // the list as k_finish_q reads it: in the lanes, or (Verlet skip) still in memory
+        const int pos = lane < KL ? (skip ? lists[(size_t)lane * N + slot] : lpos) : -1;
+        finish_q_core<KL>(t, spt, fa.snr, (int)qperm[slot], slot, pose, kp, pos, skip ? wskip : worst(), fa.cs, fa.cd,
+                          fa.cn, fa.tr, nbr_stats, fa.fb_list, fb_count);
+    } else {
+        // k_finish's deferred-query counter, zeroed at the END of the kernel: a global store ahead
+        // of the traversal may-clobbers every later load, and the node records are then fetched by
+        // vector loads instead of through the scalar cache
+        if (bx == 0 && threadIdx.x == 0) *fb_count = 0u;
+    }
 }
 
 // =============================================================================================
@@ -1363,10 +1418,10 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
 // gathers, the exact distances, the gates and the IMLS weights run across the lanes.  Every value is
 // computed by the same expression as k_finish's lane code, the list order is the same (d², index)
 // total order (each lane's rank by counting), the IMLS sums accumulate in that order (lane 0 reads
-// each term in turn) — the correspondences are the lane kernel's bit for bit.  cd[i].w carries the
-// query's category (−1 valid, reject category, −3 deferred) to k_finish_slab, which reduces the
-// pass-1 normal equations per 256-slot block exactly as k_finish does (same slot → thread map,
-// same block_normeq) and counts the rejects.
+// each term in turn) — the correspondences are the lane kernel's bit for bit.  Rejects are counted
+// by integer atomics (order-free).  The pass-1 slabs (per 256-slot block, exactly k_finish's: same
+// slot → thread map, same block_normeq) are summed by the slab role of the fallback launch that
+// follows anyway (k_fallback_slab), from the rows whose cd.w is −1.
 // =============================================================================================
 __device__ __forceinline__ double rl_f64(double x, int l) {
     const long long b = __double_as_longlong(x);
@@ -1375,27 +1430,23 @@ __device__ __forceinline__ double rl_f64(double x, int l) {
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
+// query i (slot `slot`) from its list: lane k < KL holds entry k's map position `pos` (−1 empty),
+// W is the list's bound (the traversal's worst key).  Run by k_finish_q, and by k_knn_qwave_f
+// straight after the traversal of the same wave (round 4: one launch per iteration fewer)
 template <int KL>
-__device__ __forceinline__ void finish_q_body(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
-                                              const unsigned* __restrict__ qperm, int N, const double* __restrict__ pose,
-                                              const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
-                                              const float* __restrict__ wlist, float4* __restrict__ cs,
-                                              float4* __restrict__ cd, float4* __restrict__ cn,
+__device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
+                                              int i, int slot, const double* __restrict__ pose, const KParams& kp,
+                                              int pos, float W, float4* __restrict__ cs, float4* __restrict__ cd,
+                                              float4* __restrict__ cn, imls_iter_trace* __restrict__ tr,
                                               unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
-                                              unsigned* __restrict__ fb_count, int bx) {
+                                              unsigned* __restrict__ fb_count) {
     static_assert(KL <= 64, "one list entry per lane");
-    if (done && *done) return;
     const int lane = threadIdx.x & 63;
-    const int slot = __builtin_amdgcn_readfirstlane(bx * (kWaveBlock / 64) + (int)(threadIdx.x >> 6));
-    if (slot >= N) return;
-    const int i = (int)qperm[slot];
     float xf[3];
     double ns[3];
     transform_query(pose, spt[i], snr[i], kp.transform_normal, xf, ns);
     const double xd[3] = {xf[0], xf[1], xf[2]};
-    const float W = wlist[slot];
     const bool ent = lane < KL;
-    const int pos = ent ? lists[(size_t)lane * N + slot] : -1;
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     double ed = kInfD;
     int eo = 0x7fffffff;
@@ -1447,6 +1498,7 @@ __device__ __forceinline__ void finish_q_body(TreeView t, const float4* __restri
             const double lb = l1 < 0 ? r2 : fmax(cnt_r >= K ? dK : r2, d1);
             cs[i] = make_float4(0.f, 0.f, 0.f, (float)(fmin(lb, r2) * (1.0 + 1e-6)));
             cd[i] = make_float4(0.f, 0.f, 0.f, -3.f);
+            if (nbr_stats) atomicAdd(&nbr_stats[5], 1ull);
         }
         return;
     }
@@ -1519,8 +1571,10 @@ __device__ __forceinline__ void finish_q_body(TreeView t, const float4* __restri
     }
     if (lane == 0) {
         store_result(i, cat, xf, yf, nf, cs, cd, cn);
-        // the category for k_finish_slab in cd.w (y's row is read only behind cs.w's valid flag)
+        // the slab role of the fallback launch sums the rows with cd.w = −1 (valid here); a
+        // rejected or deferred query carries its category / −3 (the fallback's own rows: w = 0)
         cd[i] = cat == -1 ? make_float4(yf[0], yf[1], yf[2], -1.f) : make_float4(0.f, 0.f, 0.f, (float)cat);
+        if (cat >= 0) atomicAdd((unsigned long long*)&tr->reject[cat], 1ull);   // integer: order-free
         if (nbr_stats) {
             if (kq) atomicAdd(&nbr_stats[0], (unsigned long long)kq);
             if (l1 >= 0) atomicAdd(&nbr_stats[1], 1ull);
@@ -1528,39 +1582,70 @@ __device__ __forceinline__ void finish_q_body(TreeView t, const float4* __restri
     }
 }
 
-// pass-1 normal equations + reject counters of k_finish_q's queries, per 256-slot block as k_finish
-__device__ __forceinline__ void finish_slab_body(const unsigned* __restrict__ qperm, int N, const int* __restrict__ done,
-                                                 const float4* __restrict__ cs, const float4* __restrict__ cd,
-                                                 const float4* __restrict__ cn, double* __restrict__ partial1,
-                                                 imls_iter_trace* __restrict__ tr,
-                                                 unsigned long long* __restrict__ nbr_stats, int bx) {
+template <int KL>
+__device__ __forceinline__ void finish_q_body(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
+                                              const unsigned* __restrict__ qperm, int N, const double* __restrict__ pose,
+                                              const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
+                                              const float* __restrict__ wlist, float4* __restrict__ cs,
+                                              float4* __restrict__ cd, float4* __restrict__ cn,
+                                              imls_iter_trace* __restrict__ tr,
+                                              unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
+                                              unsigned* __restrict__ fb_count, int bx) {
     if (done && *done) return;
+    const int lane = threadIdx.x & 63;
+    const int slot = __builtin_amdgcn_readfirstlane(bx * (kWaveBlock / 64) + (int)(threadIdx.x >> 6));
+    if (slot >= N) return;
+    const int pos = lane < KL ? lists[(size_t)lane * N + slot] : -1;
+    finish_q_core<KL>(t, spt, snr, (int)qperm[slot], slot, pose, kp, pos, wlist[slot], cs, cd, cn, tr, nbr_stats, fb_list,
+                      fb_count);
+}
+
+// pass-1 normal equations of the wave-per-query results, per 256-slot block exactly as k_finish's
+// block_normeq<kWaveBlock> sums them (rows = the queries whose cd.w is −1; rejects were counted by
+// the exact stage), by a block of kProjBlock threads: wave w reduces the 64-slot groups w, w + 2, …
+// with the same wave_total, and the four group totals are added in group order — the same
+// association, so the slabs are k_finish's bit for bit
+__device__ __forceinline__ void finish_slab_body(const unsigned* __restrict__ qperm, int N, const float4* __restrict__ cs,
+                                                 const float4* __restrict__ cd, const float4* __restrict__ cn,
+                                                 double* __restrict__ partial1, int bx) {
     __shared__ double red[kWaveBlock / 64][kNormEq];
-    __shared__ double out[kNormEq];
-    __shared__ unsigned rej_s[IMLS_NUM_REJ + 1];
-    const int tid = threadIdx.x;
-    if (tid < IMLS_NUM_REJ + 1) rej_s[tid] = 0;
-    __syncthreads();
-    const int slot = bx * kWaveBlock + tid;
-    int cat = -2;
-    double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
-    if (slot < N) {
-        const int i = (int)qperm[slot];
-        const float4 d4 = cd[i];
-        cat = (int)d4.w;
-        if (cat == -1) {
-            const float4 s4 = cs[i], n4 = cn[i];
-            const float xf[3] = {s4.x, s4.y, s4.z}, yf[3] = {d4.x, d4.y, d4.z}, nf[3] = {n4.x, n4.y, n4.z};
-            plane_row(xf, yf, nf, a, bb);
-            one = 1.0;
+    const int lane = threadIdx.x & 63;
+    for (int g = (int)(threadIdx.x >> 6); g < kWaveBlock / 64; g += (int)(blockDim.x >> 6)) {
+        const int slot = bx * kWaveBlock + g * 64 + lane;
+        double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
+        if (slot < N) {
+            const int i = (int)qperm[slot];
+            const float4 d4 = cd[i];
+            if (d4.w == -1.f) {
+                const float4 s4 = cs[i], n4 = cn[i];
+                const float xf[3] = {s4.x, s4.y, s4.z}, yf[3] = {d4.x, d4.y, d4.z}, nf[3] = {n4.x, n4.y, n4.z};
+                plane_row(xf, yf, nf, a, bb);
+                one = 1.0;
+            }
         }
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = r; c < 6; ++c) {
+                const double v = wave_total(a[r] * a[c]);
+                if (lane == 63) red[g][k] = v;
+                ++k;
+            }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            const double v = wave_total(a[r] * bb);
+            if (lane == 63) red[g][21 + r] = v;
+        }
+        const double v = wave_total(one);
+        if (lane == 63) red[g][27] = v;
     }
-    if (cat >= 0) atomicAdd(&rej_s[cat], 1u);
-    if (cat == -3) atomicAdd(&rej_s[IMLS_NUM_REJ], 1u);
-    block_normeq<kWaveBlock>(a, bb, one, red, out);
-    if (tid < kNormEq) partial1[(size_t)bx * kNormEq + tid] = out[tid];
-    if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
-    if (nbr_stats && tid == IMLS_NUM_REJ && rej_s[tid]) atomicAdd(&nbr_stats[5], (unsigned long long)rej_s[tid]);
+    __syncthreads();
+    if (threadIdx.x < kNormEq) {
+        double sum = 0.0;
+        for (int w = 0; w < kWaveBlock / 64; ++w) sum += red[w][threadIdx.x];
+        partial1[(size_t)bx * kNormEq + threadIdx.x] = sum;
+    }
 }
 
 // =============================================================================================
@@ -1576,7 +1661,10 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
                                                              float4* __restrict__ cs, float4* __restrict__ cd,
                                                              float4* __restrict__ cn, double* __restrict__ partial1,
                                                              imls_iter_trace* __restrict__ tr,
-                                                             unsigned long long* __restrict__ nbr_stats, int nlog) {
+                                                             unsigned long long* __restrict__ nbr_stats, int nlog,
+                                                             unsigned* __restrict__ fb_reset = nullptr,
+                                                             int arrivals = 0) {
+    // (done: the launch that fed qlist left at once too, so the counter is still zero)
     if (done && *done) return;
     __shared__ uint2 stack[kStackDepth][kProjBlock];
     __shared__ double red[kProjBlock / 64][kNormEq];
@@ -1729,6 +1817,18 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
     if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
+    if (fb_reset) {
+        // the last block to get here (every block has read *qcount and its qlist entries) zeroes the
+        // deferred-query counter [0] for the next fused launch, and the arrival counter [1]
+        __syncthreads();
+        if (tid == 0) {
+            __threadfence();
+            if (atomicAdd(&fb_reset[1], 1u) == (unsigned)arrivals - 1u) {
+                atomicExch(&fb_reset[0], 0u);
+                atomicExch(&fb_reset[1], 0u);
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1756,6 +1856,16 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(
 }
 
 template <int KL>
+__global__ __launch_bounds__(kWaveBlock) void k_knn_qwave_f(
+        TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
+        const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
+        int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
+        int use_prev, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_count, QFinishArgs fa) {
+    knn_qwave_body<KL, true>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats,
+                             fb_count, (int)blockIdx.x, fa);
+}
+
+template <int KL>
 __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(
         TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qperm,
         int N, const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
@@ -1771,16 +1881,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_finish_q(
         TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qperm,
         int N, const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
         const float* __restrict__ wlist, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
-        unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list, unsigned* __restrict__ fb_count) {
-    finish_q_body<KL>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, nbr_stats, fb_list, fb_count,
+        imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
+        unsigned* __restrict__ fb_count) {
+    finish_q_body<KL>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, tr, nbr_stats, fb_list, fb_count,
                       (int)blockIdx.x);
-}
-__global__ __launch_bounds__(kWaveBlock) void k_finish_slab(const unsigned* __restrict__ qperm, int N,
-                                                            const int* __restrict__ done, const float4* __restrict__ cs,
-                                                            const float4* __restrict__ cd, const float4* __restrict__ cn,
-                                                            double* __restrict__ partial1, imls_iter_trace* __restrict__ tr,
-                                                            unsigned long long* __restrict__ nbr_stats) {
-    finish_slab_body(qperm, N, done, cs, cd, cn, partial1, tr, nbr_stats, (int)blockIdx.x);
 }
 
 template <int KCAP>
@@ -1788,9 +1892,30 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(
         TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qlist,
         const unsigned* __restrict__ qcount, int N, const double* __restrict__ pose, const int* __restrict__ done,
         KParams kp, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
-        double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats) {
+        double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats,
+        unsigned* __restrict__ fb_reset) {
     project_lane_body<KCAP>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats,
-                            kFallbackBlocks);
+                            kFallbackBlocks, fb_reset, (int)gridDim.x);
+}
+
+// After the wave-per-query exact stage (k_finish_q / k_knn_qwave_f): blocks [0, kFallbackBlocks)
+// run the exact fallback of the deferred queries (their slabs, and the deferred counter's reset),
+// the blocks after them sum the wave slabs — one launch instead of two (round 4)
+template <int KCAP>
+__global__ __launch_bounds__(kProjBlock) void k_fallback_slab(
+        TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qlist,
+        unsigned* __restrict__ qcount, const unsigned* __restrict__ qperm, int N, const double* __restrict__ pose,
+        const int* __restrict__ done, KParams kp, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
+        double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats) {
+    static_assert(kWaveBlock % kProjBlock == 0 && kProjBlock % 64 == 0, "slab groups per wave");
+    if ((int)blockIdx.x >= kFallbackBlocks) {
+        if (done && *done) return;
+        finish_slab_body(qperm, N, cs, cd, cn, partial1, (int)blockIdx.x - kFallbackBlocks);
+        return;
+    }
+    const int wb = (N + kWaveBlock - 1) / kWaveBlock;
+    project_lane_body<KCAP>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1 + (size_t)wb * kNormEq, tr,
+                            nbr_stats, kFallbackBlocks, qcount, kFallbackBlocks);
 }
 
 __device__ __forceinline__ int wave_blocks_of(int N) { return (N + kWaveBlock - 1) / kWaveBlock; }
@@ -1803,6 +1928,9 @@ __host__ __device__ __forceinline__ int knn_blocks_of(int N, int qp) {
 __host__ __device__ __forceinline__ bool use_qwave(const KParams& kp, int N) {
     return kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN);
 }
+// one-frame launches: the exact stage one wave per query (k_knn_qwave_f / k_finish_q), the slabs
+// and the fallback then in one k_fallback_slab launch
+__host__ __forceinline__ bool q_exact_stage(const KParams& kp, int N) { return use_qwave(kp, N) && kp.qfinish; }
 // the list block of a frame (see launch_wave): positions [KL][N], worst keys [N], xref, nref
 template <int KL>
 __device__ __forceinline__ float* wlist_of(int* lists, int N) { return reinterpret_cast<float*>(lists + (size_t)KL * N); }
@@ -1896,8 +2024,9 @@ template <int KCAP>
 void launch_lane(hipStream_t s, int blocks, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qlist,
                  const unsigned* qcount, int N, const double* pose, const int* done, const KParams& kp, float4* cs,
                  float4* cd, float4* cn, double* partial1, imls_iter_trace* tr, unsigned long long* stats) {
+    // a deferred list (qlist): this launch also resets its counter for the next projection
     k_project_lane<KCAP><<<blocks, kProjBlock, 0, s>>>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1,
-                                                       tr, stats);
+                                                       tr, stats, qlist ? const_cast<unsigned*>(qcount) : nullptr);
 }
 
 
@@ -1912,7 +2041,12 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
     if (marks) (void)hipEventRecord(marks[0], s);
     // sparse query sets (≤ kQwaveAutoN queries, e.g. FPS-sampled frames): one wave per query;
     // dense scans: packets of 64 Morton-coherent queries
-    if (use_qwave(kp, N))
+    const bool small_q = q_exact_stage(kp, N);
+    if (small_q && kp.qfuse)
+        k_knn_qwave_f<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(
+            t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, stats, fb_count,
+            QFinishArgs{snr, cs, cd, cn, tr, fb_list});
+    else if (use_qwave(kp, N))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
                                                                                           delta, lists, wlist, xref, nref, use_prev, stats,
                                                                                           fb_count);
@@ -1926,11 +2060,12 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
         k_knn_wave<KL, false, false><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
                                                            nref, use_prev, stats, fb_count);
     if (marks) (void)hipEventRecord(marks[1], s);
-    if (use_qwave(kp, N) && kp.qfinish) {
-        // a small frame alone: the exact stage one wave per query, then the per-block reduction
+    if (small_q && kp.qfuse) {
+        // the exact stage ran in the traversal kernel; slabs: k_fallback_slab
+    } else if (small_q) {
+        // a small frame alone: the exact stage one wave per query; slabs: k_fallback_slab
         k_finish_q<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(
-            t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, stats, fb_list, fb_count);
-        k_finish_slab<<<blocks, kWaveBlock, 0, s>>>(qperm, N, done, cs, cd, cn, partial1, tr, stats);
+            t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, tr, stats, fb_list, fb_count);
     } else {
         k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1,
                                                    tr, stats, fb_list, fb_count);
@@ -2007,7 +2142,16 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
     else if (K <= 20 && kp.kl20 == 26) launch_wave<26>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else if (K <= 20) launch_wave<22>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
-    // exact fallback for uncertified queries (usually none; the launch exits at once then)
+    // exact fallback for uncertified queries (usually none; the launch exits at once then) — after
+    // the wave-per-query exact stage with the wave slabs' sums in the same launch
+    if (q_exact_stage(kp, N)) {
+        const int g = kFallbackBlocks + wblocks;
+        if (K <= 8) k_fallback_slab<8><<<g, kProjBlock, 0, s>>>(t, spt, snr, fb_list, fb_count, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats);
+        else if (K <= 16) k_fallback_slab<16><<<g, kProjBlock, 0, s>>>(t, spt, snr, fb_list, fb_count, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats);
+        else if (K <= 20) k_fallback_slab<20><<<g, kProjBlock, 0, s>>>(t, spt, snr, fb_list, fb_count, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats);
+        else k_fallback_slab<32><<<g, kProjBlock, 0, s>>>(t, spt, snr, fb_list, fb_count, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats);
+        return;
+    }
     if (K <= 8) launch_lane<8>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
     else if (K <= 16) launch_lane<16>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
     else if (K <= 20) launch_lane<20>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);

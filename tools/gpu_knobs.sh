@@ -14,7 +14,7 @@ if [ -n "${TESTS:-}" ]; then
   rc=$?; echo "tests rc=$rc"; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 fi
 show() { python3 -c "
-import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);r=d['roofline'];sp=d.get('single_pair') or {};s=sp.get('kernel_avg_ms',{})
+import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);r=d['roofline'];sp=d.get('single_pair') or d.get('single_frame') or {};s=sp.get('kernel_avg_ms',{})
 print('$2', round(d['value'],1), 'busy_proj', round(r.get('busy_projection_ms_per_step',0),2), 'knn', round(s.get('k_knn_wave',0)*1e3,1), 'finish', round(s.get('k_finish',0)*1e3,1), 'single', round(sp.get('median_ms',0),2), 'verify', d['verify']['mismatches'])"; }
 for r in $(seq 1 ${ROUNDS:-2}); do
   kn=0

@@ -1,4 +1,4 @@
-"""Per-ICP-iteration medians of the lone-frame kernels (k_knn_qwave, k_finish_q, k_finish_slab,
+"""Per-ICP-iteration medians of the lone-frame kernels (k_knn_qwave[_f], k_finish_q, k_finish_slab,
 k_project_lane, k_solve_small) from a rocprofv3 kernel trace of tools/frame_probe.py (20 iterations
 per frame, launches in stream order)."""
 import collections
@@ -9,7 +9,7 @@ import numpy as np
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-keys = ("k_knn_qwave", "k_finish_q", "k_finish_slab", "k_project_lane", "k_solve_small")
+keys = ("k_knn_qwave", "k_knn_qwave_f", "k_finish_q", "k_finish_slab", "k_fallback_slab", "k_project_lane", "k_solve_small")
 d = collections.defaultdict(list)
 gaps = []
 prev_end = None
