@@ -50,6 +50,8 @@ static_assert(kWaveBlock == kPass1Block && kFallbackBlocks == kPass1Fallback, "p
 constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query up to this many queries
 constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
 constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
+constexpr int kFStack = 256;        // frontier traversal's stack per wave (see knn_qwave_body)
+constexpr int kFBatchMax = 128;     // above this many entries: one entry per step (DFS growth ≤ 8 × 7)
 #ifndef IMLS_SEED_CHUNK
 #define IMLS_SEED_CHUNK 8
 #endif
@@ -1044,10 +1046,15 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float sdist[kWaveBlock / 64][kWaveStack];
+    __shared__ int fnode[kWaveBlock / 64][kFStack];      // frontier traversal (kp.frontier)
+    __shared__ float fdist[kWaveBlock / 64][kFStack];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int slot = __builtin_amdgcn_readfirstlane(bx * (kWaveBlock / 64) + wv);
     if (slot >= N) return;
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    const long long dbg_q0 = wall_clock64();
+#endif
     float xf[3];
     {
         double ns[3];
@@ -1178,6 +1185,118 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
             node = ln;
         }
     }
+    if (kp.frontier && node) {
+        // Frontier traversal (round 4): each step takes up to 8 stacked entries within the bound and
+        // gives each an 8-lane group — an inner node's group tests the boxes of its descendants
+        // `sw` levels down (one record per lane pair), a leaf's group measures its points (B / 8 per
+        // lane) — so a query whose ball spans many leaves walks them 8 at a time instead of one
+        // dependent step per node (the steady-state iterations' tail: 2 % of the queries, 5-10
+        // leaves and 11-16 inner steps each, set the launch time).  Candidates are inserted before
+        // the wanted children are stacked (lower lanes on top), so the bound they face is current.
+        // The same nodes are pruned by the same test (box d² > bound·slack, the bound only shrinks):
+        // exactness is the DFS's.  Near capacity (> kFBatchMax entries) one entry per step keeps the
+        // growth to the DFS's depth × 7.
+        if (lane < sp) { fnode[wv][lane] = snode[wv][lane]; fdist[wv][lane] = sdist[wv][lane]; }
+        if (lane == 0) { fnode[wv][sp] = node; fdist[wv][sp] = 0.0f; }
+        int fsp = sp + 1;
+        const int ppl = (B + 7) >> 3;
+#ifdef IMLS_DEBUG_WAVE_TRACE
+        int dbg_steps = 0;
+#endif
+        while (fsp > 0) {
+#ifdef IMLS_DEBUG_WAVE_TRACE
+            if (++dbg_steps > 20000 || fsp > kFStack) {
+                if (lane == 0)
+                    printf("frontier stuck: slot %d pass %d steps %d fsp %d sp0 %d node0 %d bnd %g P %d levels %d B %d M %d\n",
+                           slot, pass, dbg_steps, fsp, sp, node, (double)bnd, P, t.levels, B, M);
+                break;
+            }
+#endif
+            const int lim = fsp > kFBatchMax ? 1 : 8;
+            const int idx = fsp - 1 - lane;
+            int en = 0;
+            float ed = kInfF;
+            if (idx >= 0) { en = fnode[wv][idx]; ed = fdist[wv][idx]; }
+            const unsigned long long vm = __ballot(idx >= 0 && ed <= bnd * kBoxSlack);
+            unsigned long long rem = vm, taken = 0;
+            int gsrc[8];
+            int ng = 0;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                gsrc[g] = 0;
+                if (g < lim && rem) {
+                    const int b = __builtin_ctzll(rem);
+                    gsrc[g] = b;
+                    taken |= 1ull << b;
+                    rem &= rem - 1;
+                    ++ng;
+                }
+            }
+            fsp -= (ng == lim) ? (64 - __builtin_clzll(taken)) : min(fsp, 64);
+            if (!ng) continue;
+            const int g = lane >> 3, gl = lane & 7;
+            int src = gsrc[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) src = g == k ? gsrc[k] : src;
+            const int gnode = __shfl(en, src, 64);
+            const bool gact = g < ng;
+            const bool ginner = gact && gnode < P, gleaf = gact && gnode >= P;
+            n_inner += __popcll(__ballot(ginner && gl == 0));
+            n_leaf += __popcll(__ballot(gleaf && gl == 0));
+            float cdist = kInfF;
+            int child = 0;
+            if (ginner) {
+                const int lev = 31 - __builtin_clz(gnode);
+                const int sw = min(min(kp.wide, 3), t.levels - lev);     // ≤ 8 descendants: one per lane
+                if (gl < (1 << sw)) {
+                    const float4* rec = t.nodes + 3 * (((size_t)gnode << (sw - 1)) + (gl >> 1));
+                    const float4 a = rec[0], b = rec[1], c = rec[2];
+                    cdist = (gl & 1) ? box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w) : box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+                    child = (gnode << sw) + gl;
+                }
+            }
+            int lbase = 0, lcnt = 0;
+            if (gleaf) {
+                const int leaf = gnode - P;
+                if (leaf < seed_lo || leaf > seed_hi) {
+                    lbase = leaf * B;
+                    lcnt = min(B, M - lbase);
+                }
+            }
+            float pd[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                pd[k] = kInfF;
+                const int j = gl + 8 * k;
+                if (k < ppl && j < lcnt) {
+                    const float4 q = t.mpt[lbase + j];
+                    const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
+                    pd[k] = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k >= ppl) break;
+                unsigned long long m = __ballot(pd[k] <= bnd && pd[k] < worst());
+                while (m) {
+                    const int j = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const float cd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pd[k]), j));
+                    const int cp = __builtin_amdgcn_readlane(lbase + gl + 8 * k, j);
+                    if (cd <= bnd && cd < worst() && !__ballot(lane < KL && lpos == cp)) insert(cd, cp);
+                }
+            }
+            const unsigned long long want = __ballot(child != 0 && cdist <= bnd * kBoxSlack);
+            if ((want >> lane) & 1ull) {
+                // rank among the wanted lanes above this one (a 64-bit shift by 64 is not 0 here)
+                const int at = fsp + (lane == 63 ? 0 : __popcll(want >> (lane + 1)));
+                fnode[wv][at] = child;
+                fdist[wv][at] = cdist;
+            }
+            fsp += __popcll(want);
+        }
+        node = 0;
+    }
     while (node) {
         if (node < P) {
             // one step descends `sw` binary levels: lane k tests the box of descendant k (the 2^sw
@@ -1276,10 +1395,23 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         atomicAdd(&nbr_stats[4], 1ull);
     }
     if constexpr (FUSED) {
+#ifdef IMLS_DEBUG_WAVE_TRACE
+        const long long dbg_q1 = wall_clock64();
+#endif
         // the list as k_finish_q reads it: in the lanes, or (Verlet skip) still in memory
         const int pos = lane < KL ? (skip ? lists[(size_t)lane * N + slot] : lpos) : -1;
         finish_q_core<KL>(t, spt, fa.snr, (int)qperm[slot], slot, pose, kp, pos, skip ? wskip : worst(), fa.cs, fa.cd,
                           fa.cn, fa.tr, nbr_stats, fa.fb_list, fb_count);
+#ifdef IMLS_DEBUG_WAVE_TRACE
+        // per-wave record of the last fused launch: start / traversal end / finish end (100 MHz
+        // clock, low 32 bits), Verlet skip, leaves, inner steps, hardware id
+        if (lane == 0 && slot < kDbgWaves) {
+            unsigned* r = g_dbg_wave[slot];
+            r[0] = (unsigned)dbg_q0; r[1] = (unsigned)dbg_q1; r[2] = (unsigned)wall_clock64();
+            r[3] = skip ? 1u : 0u; r[4] = n_leaf; r[5] = n_inner; r[6] = greedy ? 1u : 0u;
+            r[7] = (unsigned)__builtin_amdgcn_s_getreg((23 << 0) | (0 << 6) | (31 << 11));   // HW_ID / HW_ID1
+        }
+#endif
     } else {
         // k_finish's deferred-query counter, zeroed at the END of the kernel: a global store ahead
         // of the traversal may-clobbers every later load, and the node records are then fetched by

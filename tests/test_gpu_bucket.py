@@ -21,13 +21,16 @@ pytestmark = pytest.mark.gpu
 GOLDEN = pathlib.Path(__file__).resolve().parent / "golden"
 
 
+@pytest.mark.parametrize("qwave", ["0", "1"], ids=["packets", "wave_per_query"])
 @pytest.mark.parametrize("bucket", ["16", "32"])
 @pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair"])
-def test_small_leaves_match_oracle(name, bucket, monkeypatch):
+def test_small_leaves_match_oracle(name, bucket, qwave, monkeypatch):
+    """packets: the lockstep leaf scan; wave per query: the frontier traversal, whose leaf groups
+    measure B / 8 points per lane (2 at B = 16)."""
     g = dict(np.load(GOLDEN / f"{name}.npz"))
     src, tgt = np.ascontiguousarray(g["src"]), np.ascontiguousarray(g["tgt"])
     monkeypatch.setenv("IMLS_BUCKET", bucket)       # read when the context is created
-    monkeypatch.setenv("IMLS_QWAVE", "0")           # packets: the lockstep leaf scan under test
+    monkeypatch.setenv("IMLS_QWAVE", qwave)
     p = config.bench_params(8)
     with imls_icp.ImlsContext(p) as ctx:
         ctx.set_target(np.ascontiguousarray(tgt.T))
