@@ -253,6 +253,8 @@ KParams make_kparams(const imls_params& p) {
     if (const char* w = std::getenv("IMLS_BOTTOM_UP")) k.bottom_up = std::atoi(w);
     k.frontier = 1;
     if (const char* w = std::getenv("IMLS_FRONTIER")) k.frontier = std::atoi(w);
+    k.qexact = 1;
+    if (const char* w = std::getenv("IMLS_QEXACT")) k.qexact = std::atoi(w);
     // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
     // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)
     k.tv = (p.use_tensor_voting && !p.get_normals && p.matching_method == IMLS_MATCH_IMLS) ? 1 : 0;

@@ -71,6 +71,7 @@ struct KParams {
     int qfuse;                // with qfinish: the exact stage inside the traversal kernel (k_knn_qwave_f)
     int bottom_up;            // wave-per-query traversal: start at a leaf with the path's sibling boxes stacked
     int frontier;             // wave-per-query traversal: up to 8 stacked entries per step, 8 lanes each
+    int qexact;               // fused lone-frame path: an uncertified query's exact list in the wave (no fallback launch)
     int xcd;                  // batched projection: frames grouped per XCD round-robin slot (−1 auto: ≥ 16 frames)
     int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
     int tv;                   // tensor-voting normals (use_tensor_voting && !get_normals, IMLS matcher)

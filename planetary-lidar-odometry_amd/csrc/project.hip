@@ -1024,7 +1024,8 @@ __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restri
                                               int pos, float W, float4* __restrict__ cs, float4* __restrict__ cd,
                                               float4* __restrict__ cn, imls_iter_trace* __restrict__ tr,
                                               unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
-                                              unsigned* __restrict__ fb_count);
+                                              unsigned* __restrict__ fb_count, int* stk_n = nullptr,
+                                              float* stk_d = nullptr);
 struct QFinishArgs {
     const float4* snr;
     float4 *cs, *cd, *cn;
@@ -1401,7 +1402,8 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         // the list as k_finish_q reads it: in the lanes, or (Verlet skip) still in memory
         const int pos = lane < KL ? (skip ? lists[(size_t)lane * N + slot] : lpos) : -1;
         finish_q_core<KL>(t, spt, fa.snr, (int)qperm[slot], slot, pose, kp, pos, skip ? wskip : worst(), fa.cs, fa.cd,
-                          fa.cn, fa.tr, nbr_stats, fa.fb_list, fb_count);
+                          fa.cn, fa.tr, nbr_stats, fa.fb_list, fb_count, kp.qexact ? snode[wv] : nullptr,
+                          kp.qexact ? sdist[wv] : nullptr);
 #ifdef IMLS_DEBUG_WAVE_TRACE
         // per-wave record of the last fused launch: start / traversal end / finish end (100 MHz
         // clock, low 32 bits), Verlet skip, leaves, inner steps, hardware id
@@ -1565,13 +1567,121 @@ __device__ __forceinline__ double rl_f64(double x, int l) {
 // query i (slot `slot`) from its list: lane k < KL holds entry k's map position `pos` (−1 empty),
 // W is the list's bound (the traversal's worst key).  Run by k_finish_q, and by k_knn_qwave_f
 // straight after the traversal of the same wave (round 4: one launch per iteration fewer)
+__device__ __forceinline__ double shfl_up_f64(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __shfl_up((int)(unsigned)(b & 0xffffffffll), 1, 64);
+    const int hi = __shfl_up((int)(unsigned)((unsigned long long)b >> 32), 1, 64);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// The exact list of one query by one wave, for a query whose float list failed its certificate
+// (round 4: the fused lone-frame path resolves it in place instead of deferring it to the fallback
+// launch): project_lane_body's search — the K nearest map points by (exact d², original index) with
+// d² ≤ r², NN-1 = the first with d² > DBL_EPSILON, boxes and points pruned by the float bound
+// min(cap, max(K-th, NN-1))·slack — with the list in lanes 0..K−1 instead of registers.  Returns
+// lane k's entry position (−1 empty); an NN-1 outside the K entries (more than K points within
+// DBL_EPSILON of the query) rides in lane K.  stk_n / stk_d: the wave's LDS stack (kWaveStack).
+template <int KL>
+__device__ int exact_wave_list(const TreeView& t, const KParams& kp, const double xd[3], const float xf[3], double cap,
+                               int* stk_n, float* stk_d) {
+    static_assert(KL <= 64, "one list entry per lane");
+    const int lane = threadIdx.x & 63;
+    const int K = kp.K;
+    const double r2 = kp.r2;
+    double ek = kInfD;
+    int eo = 0x7fffffff, ep = -1;
+    double d1 = kInfD;
+    int o1 = 0x7fffffff, p1 = -1;
+    float bf = (float)cap * kBoxSlack + 1e-30f;
+    const int P = t.P, B = t.B, M = t.M;
+    int node = 1, sp = 0;
+    while (true) {
+        if (node < P) {
+            const int lev = 31 - __builtin_clz(node);
+            const int sw = min(min(kp.wide, 3), t.levels - lev);
+            const int nk = 1 << sw;
+            float d = kInfF;
+            if (lane < nk) {
+                const float4* rec = t.nodes + 3 * (((size_t)node << (sw - 1)) + (lane >> 1));
+                const float4 a = rec[0], b = rec[1], c = rec[2];
+                d = (lane & 1) ? box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w) : box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
+            }
+            const unsigned long long want = __ballot(lane < nk && d <= bf);
+            if (want) {
+                const int km = __builtin_ctzll(want);
+                unsigned long long rest = want & (want - 1);
+                while (rest) {
+                    const int kk = 63 - __builtin_clzll(rest);
+                    rest &= ~(1ull << kk);
+                    const float dk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), kk));
+                    if (lane == 0) { stk_n[sp] = (node << sw) + kk; stk_d[sp] = dk; }
+                    ++sp;
+                }
+                node = (node << sw) + km;
+                continue;
+            }
+        } else {
+            const int base = (node - P) * B, cnt = min(B, M - base);
+            double d2 = kInfD;
+            int oi = 0x7fffffff;
+            bool c = false;
+            if (lane < cnt) {
+                const float4 q = t.mpt[base + lane];
+                const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
+                const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                if (d32 <= bf) {
+                    d2 = exact_d2(xd, q.x, q.y, q.z);
+                    oi = (int)__float_as_uint(q.w);
+                    c = d2 <= r2;
+                }
+            }
+            unsigned long long m = __ballot(c);
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                const double cdd = rl_f64(d2, j);
+                const int co = __builtin_amdgcn_readlane(oi, j);
+                bool changed = false;
+                if (cdd > DBL_EPSILON && (cdd < d1 || (cdd == d1 && co < o1))) {
+                    d1 = cdd; o1 = co; p1 = base + j;
+                    changed = true;
+                }
+                const double wk = rl_f64(ek, K - 1);
+                const int wo = __builtin_amdgcn_readlane(eo, K - 1);
+                if (cdd < wk || (cdd == wk && co < wo)) {
+                    const int at = __popcll(__ballot(lane < K && (ek < cdd || (ek == cdd && eo < co))));
+                    const double uk = shfl_up_f64(ek);
+                    const int uo = __shfl_up(eo, 1, 64), up = __shfl_up(ep, 1, 64);
+                    if (lane > at && lane < K) { ek = uk; eo = uo; ep = up; }
+                    if (lane == at) { ek = cdd; eo = co; ep = base + j; }
+                    changed = true;
+                }
+                if (changed) bf = (float)fmin(cap, fmax(rl_f64(ek, K - 1), d1)) * kBoxSlack + 1e-30f;
+            }
+        }
+        node = 0;
+        while (sp > 0) {
+            --sp;
+            if (stk_d[sp] <= bf) { node = stk_n[sp]; break; }
+        }
+        if (!node) break;
+    }
+    if (p1 >= 0 && !__ballot(lane < K && ep == p1) && lane == K) ep = p1;
+    return lane <= K ? ep : -1;
+}
+
+// query i (slot `slot`) from its list: lane k < KL holds entry k's map position `pos` (−1 empty),
+// W is the list's bound (the traversal's worst key).  Run by k_finish_q, and by k_knn_qwave_f
+// straight after the traversal of the same wave (round 4: one launch per iteration fewer).  With an
+// LDS stack (stk_n, the fused kernel) an uncertified query gets its exact list in place
+// (exact_wave_list) instead of being deferred to the fallback launch.
 template <int KL>
 __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
                                               int i, int slot, const double* __restrict__ pose, const KParams& kp,
                                               int pos, float W, float4* __restrict__ cs, float4* __restrict__ cd,
                                               float4* __restrict__ cn, imls_iter_trace* __restrict__ tr,
                                               unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
-                                              unsigned* __restrict__ fb_count) {
+                                              unsigned* __restrict__ fb_count, int* stk_n, float* stk_d) {
     static_assert(KL <= 64, "one list entry per lane");
     const int lane = threadIdx.x & 63;
     float xf[3];
@@ -1579,39 +1689,47 @@ __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restri
     transform_query(pose, spt[i], snr[i], kp.transform_normal, xf, ns);
     const double xd[3] = {xf[0], xf[1], xf[2]};
     const bool ent = lane < KL;
-    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-    double ed = kInfD;
-    int eo = 0x7fffffff;
-    if (pos >= 0) {
-        q = t.mpt[pos];
-        ed = exact_d2(xd, q.x, q.y, q.z);
-        eo = (int)__float_as_uint(q.w);
-    }
-    // rank in the (d², index) order (k_finish's sort); empty entries after the real ones, by lane
-    int rank = 0;
-#pragma unroll
-    for (int k = 0; k < KL; ++k) {
-        const double dk = rl_f64(ed, k);
-        const int ok = __builtin_amdgcn_readlane(eo, k);
-        rank += (dk < ed || (dk == ed && (ok < eo || (ok == eo && k < lane)))) ? 1 : 0;
-    }
+    const double r2 = kp.r2;
+    const int K = kp.K;
+    float4 q;
+    double ed, d1, dK;
+    int eo, rank, cnt_r, l1, p1, lK;
+    bool in;
     auto lane_of_rank = [&](int r) -> int {
         const unsigned long long m = __ballot(ent && rank == r);
         return m ? (int)__builtin_ctzll(m) : -1;
     };
-    const double r2 = kp.r2;
-    const int K = kp.K;
-    const bool in = ent && ed <= r2;
-    const int cnt_r = __popcll(__ballot(in));
-    // NN-1: the first entry in order within r with d² > DBL_EPSILON (no self match)
-    int r1 = (in && ed > DBL_EPSILON) ? rank : 0x7fffffff;
+    // the list's exact keys, its (d², index) order (k_finish's sort; empty entries after the real
+    // ones, by lane), the count within r, the NN-1 and the K-th
+    auto analyse = [&]() {
+        q = make_float4(0.f, 0.f, 0.f, 0.f);
+        ed = kInfD;
+        eo = 0x7fffffff;
+        if (pos >= 0) {
+            q = t.mpt[pos];
+            ed = exact_d2(xd, q.x, q.y, q.z);
+            eo = (int)__float_as_uint(q.w);
+        }
+        rank = 0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) r1 = min(r1, __shfl_xor(r1, o, 64));
-    const int l1 = r1 < 0x7fffffff ? lane_of_rank(r1) : -1;
-    const double d1 = l1 >= 0 ? rl_f64(ed, l1) : kInfD;
-    const int p1 = l1 >= 0 ? __builtin_amdgcn_readlane(pos, l1) : -1;
-    const int lK = lane_of_rank(K - 1);
-    const double dK = lK >= 0 ? rl_f64(ed, lK) : 0.0;
+        for (int k = 0; k < KL; ++k) {
+            const double dk = rl_f64(ed, k);
+            const int ok = __builtin_amdgcn_readlane(eo, k);
+            rank += (dk < ed || (dk == ed && (ok < eo || (ok == eo && k < lane)))) ? 1 : 0;
+        }
+        in = ent && ed <= r2;
+        cnt_r = __popcll(__ballot(in));
+        // NN-1: the first entry in order within r with d² > DBL_EPSILON (no self match)
+        int r1 = (in && ed > DBL_EPSILON) ? rank : 0x7fffffff;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) r1 = min(r1, __shfl_xor(r1, o, 64));
+        l1 = r1 < 0x7fffffff ? lane_of_rank(r1) : -1;
+        d1 = l1 >= 0 ? rl_f64(ed, l1) : kInfD;
+        p1 = l1 >= 0 ? __builtin_amdgcn_readlane(pos, l1) : -1;
+        lK = lane_of_rank(K - 1);
+        dK = lK >= 0 ? rl_f64(ed, lK) : 0.0;
+    };
+    analyse();
     const bool full = W < kInfF;
     double need = cnt_r >= K ? dK : r2;
     bool cert = true;
@@ -1624,15 +1742,23 @@ __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restri
     int cat = -1, kq = 0;
     float yf[3] = {0.f, 0.f, 0.f}, nf[3] = {0.f, 0.f, 0.f};
     if (!cert) {
-        if (lane == 0) {
-            const unsigned at = atomicAdd(fb_count, 1u);
-            fb_list[at] = (unsigned)i;
-            const double lb = l1 < 0 ? r2 : fmax(cnt_r >= K ? dK : r2, d1);
-            cs[i] = make_float4(0.f, 0.f, 0.f, (float)(fmin(lb, r2) * (1.0 + 1e-6)));
-            cd[i] = make_float4(0.f, 0.f, 0.f, -3.f);
-            if (nbr_stats) atomicAdd(&nbr_stats[5], 1ull);
+        // the fallback's search ball: the list's bound (k_project_lane reads it from cs.w)
+        const double lb = l1 < 0 ? r2 : fmax(cnt_r >= K ? dK : r2, d1);
+        const float capf = (float)(fmin(lb, r2) * (1.0 + 1e-6));
+        if (stk_n) {
+            pos = exact_wave_list<KL>(t, kp, xd, xf, fmin(r2, (double)capf), stk_n, stk_d);
+            analyse();
+            if (nbr_stats && lane == 0) atomicAdd(&nbr_stats[5], 1ull);
+        } else {
+            if (lane == 0) {
+                const unsigned at = atomicAdd(fb_count, 1u);
+                fb_list[at] = (unsigned)i;
+                cs[i] = make_float4(0.f, 0.f, 0.f, capf);
+                cd[i] = make_float4(0.f, 0.f, 0.f, -3.f);
+                if (nbr_stats) atomicAdd(&nbr_stats[5], 1ull);
+            }
+            return;
         }
-        return;
     }
     if (kp.matcher) {
         cat = finish_plane(xf, ns, p1, t, kp, yf, nf);
@@ -2276,6 +2402,11 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
     else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     // exact fallback for uncertified queries (usually none; the launch exits at once then) — after
     // the wave-per-query exact stage with the wave slabs' sums in the same launch
+    if (q_exact_stage(kp, N) && kp.qfuse && kp.qexact && N <= kSmallRows) {
+        // nothing deferred (uncertified queries got their exact list in the fused kernel) and no
+        // slabs needed (k_solve_small forms pass 1 from the rows): no launch
+        return;
+    }
     if (q_exact_stage(kp, N)) {
         const int g = kFallbackBlocks + wblocks;
         if (K <= 8) k_fallback_slab<8><<<g, kProjBlock, 0, s>>>(t, spt, snr, fb_list, fb_count, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats);

@@ -463,7 +463,7 @@ __device__ __forceinline__ void solve_final_body(const Rows& rows, int N, const 
 }
 
 // Small systems (≤ kSmallRows rows, e.g. the ≤2000-query frames of the config-C stream): the whole
-// LS solve in ONE block — reduce the pass-1 slabs, first solve, |r| keys of the valid rows into
+// LS solve in ONE block — pass-1 normal equations from the rows, first solve, |r| keys of the valid rows into
 // LDS, bitonic sort by (|r| bits, row), ranks [lo, hi] re-reduced, second solve, pose update —
 // instead of five launches whose fixed latency dominates at this size.  Same arithmetic and the
 // same exact (|r|, row) order as the chain.
@@ -502,8 +502,8 @@ __device__ __forceinline__ double small_b(const float4& s4, const float4& d4, co
 // counting (rank_sort) — the phases were latency chains of 256 threads × 8 rows (31 µs per solve on
 // a 1949-row frame, tools/frame_probe.py).  Float rows only (the projection's; RANSAC rows take
 // the grid chain).
-__device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const double* __restrict__ partial, int blocks,
-                                                 const SolveState& st, imls_iter_trace* tr, const KParams& kp,
+__device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const SolveState& st, imls_iter_trace* tr,
+                                                 const KParams& kp,
                                                  int weighted, int update_pose) {
     if (*st.done) return;
 #ifdef IMLS_DEBUG_WAVE_TRACE
@@ -525,12 +525,18 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     double loc[kNormEq];
 #pragma unroll
     for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
-    for (int b = t; b < blocks; b += kSmallBlock)
-#pragma unroll
-        for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
+    auto add_row = [&](const double (&a)[6], double b) {
+        int q = 0;
+        for (int p = 0; p < 6; ++p)
+            for (int c = p; c < 6; ++c) loc[q++] += a[p] * a[c];
+        for (int p = 0; p < 6; ++p) loc[21 + p] += a[p] * b;
+        loc[27] += 1.0;
+    };
     if (t == 0) { nkey = 0; stop = 0; }
-    // this thread's rows, loaded now (their latency overlaps the reduction and the first solve):
-    // s (w = valid flag), n, and b = n·(d − s)
+    // this thread's rows: s (w = valid flag), n, and b = n·(d − s), kept in registers for every pass.
+    // Pass 1 (the normal equations of every valid row, solver.cpp:89-107) is formed here from them
+    // (round 4): the lone-frame path then needs no slab launch, and every small frame — batched or
+    // alone, whatever exact stage produced its rows — sums them in this one order
     float4 rs[kSmallPer], rn[kSmallPer];
     double rb[kSmallPer];
 #pragma unroll
@@ -541,6 +547,14 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
         const float4 d4 = v ? rows.cd[r] : make_float4(0.f, 0.f, 0.f, 0.f);
         rn[k] = v ? rows.cn[r] : make_float4(0.f, 0.f, 0.f, 0.f);
         rb[k] = small_b(rs[k], d4, rn[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {
+        if (t + k * kSmallBlock < N && rs[k].w != 0.f) {
+            double a[6];
+            small_a(rs[k], rn[k], a);
+            add_row(a, rb[k]);
+        }
     }
     block_sum28<kSmallBlock>(loc, red, acc);
     DBG_STAMP(0);
@@ -648,13 +662,6 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     DBG_STAMP(3);
 #pragma unroll
     for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
-    auto add_row = [&](const double (&a)[6], double b) {
-        int q = 0;
-        for (int p = 0; p < 6; ++p)
-            for (int c = p; c < 6; ++c) loc[q++] += a[p] * a[c];
-        for (int p = 0; p < 6; ++p) loc[21 + p] += a[p] * b;
-        loc[27] += 1.0;
-    };
 #pragma unroll
     for (int k = 0; k < kSmallPer; ++k) {           // interior bins: kept without ranking (registers)
         const int r = t + k * kSmallBlock;
@@ -707,10 +714,9 @@ __global__ __launch_bounds__(kFinalBlock) void k_solve_final(Rows rows, int N, S
                                                             int update_pose) {
     solve_final_body(rows, N, st, tr, partial2, nparts, kp, update_pose);
 }
-__global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, const double* __restrict__ partial, int blocks,
-                                                            SolveState st, imls_iter_trace* tr, KParams kp, int weighted,
-                                                            int update_pose) {
-    solve_small_body(rows, N, partial, blocks, st, tr, kp, weighted, update_pose);
+__global__ __launch_bounds__(kSmallBlock) void k_solve_small(Rows rows, int N, SolveState st, imls_iter_trace* tr, KParams kp,
+                                                            int weighted, int update_pose) {
+    solve_small_body(rows, N, st, tr, kp, weighted, update_pose);
 }
 
 // grid shapes of the chain, per frame (shared by the one-frame and the batched launches)
@@ -734,7 +740,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_solve_small_b(const PairDev* __
                                                               int it) {
     const PairDev A = tab[blockIdx.y];
     if (A.N > kSmallRows) return;
-    solve_small_body(frame_rows(A, 0, 0), A.N, A.st.partial1, pass1_blocks_of(A.N), A.st, A.trace + it, kp, weighted, 1);
+    solve_small_body(frame_rows(A, 0, 0), A.N, A.st, A.trace + it, kp, weighted, 1);
 }
 __global__ __launch_bounds__(256) void k_solve_first_b(const PairDev* __restrict__ tab, KParams kp, int weighted, int it,
                                                        int src) {
@@ -785,7 +791,7 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
     }
     const int weighted = kp.solve_method == IMLS_SOLVE_WEIGHTED_LS;
     if (!rows_are_double && N <= kSmallRows) {
-        k_solve_small<<<1, kSmallBlock, 0, s>>>(rows, N, st.partial1, blocks1, st, tr, kp, weighted, update_pose);
+        k_solve_small<<<1, kSmallBlock, 0, s>>>(rows, N, st, tr, kp, weighted, update_pose);
         return;
     }
     k_solve_first<<<1, 256, 0, s>>>(st.partial1, blocks1, st, tr, kp, weighted, update_pose);

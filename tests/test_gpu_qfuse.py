@@ -1,13 +1,12 @@
 """The lone-small-frame exact stage: fused into the wave-per-query traversal (k_knn_qwave_f, the
 default), as its own launch (k_finish_q, IMLS_QFUSE=0) and lane per query (k_finish, IMLS_QFINISH=0)
-must give the same frame bit for bit: the correspondences are the same, and the pass-1 slabs the
-wave-per-query paths leave to k_fallback_slab's slab role are k_finish's own (same 256-slot blocks,
-same reduction order).  With every 3rd query deferred to the exact fallback (IMLS_FORCE_FALLBACK)
-the fused path's deferred-query counter is reset by the fallback launch (last block to arrive);
-frames registered back to back in one context check that no stale count leaks into the next
-iteration or frame.  Deferred queries are listed in atomic order, so their fallback slabs may
-associate differently from run to run: those frames are compared to 1e-12 (counts exact).  One path
-is also compared with the CPU oracle (imls_icp.cpp:496-745 restated in oracle/imls_oracle.cpp)."""
+must give the same frame bit for bit: the correspondences are the same, and k_solve_small forms the
+pass-1 normal equations from the rows in one fixed order whichever kernel produced them.  With every
+3rd query uncertified (IMLS_FORCE_FALLBACK) the fused path builds those queries' exact lists in the
+wave (exact_wave_list) while the other two defer them to the fallback launch (k_project_lane's
+search): the same correspondences, so the same poses; frames registered back to back in one
+context also check the deferred-query counter's reset.  One path is also compared with the CPU
+oracle (imls_icp.cpp:496-745 restated in oracle/imls_oracle.cpp)."""
 import pathlib
 
 import numpy as np
@@ -55,15 +54,14 @@ def test_exact_stage_paths_bit_identical(name, monkeypatch):
                 runs[(path, force)] = _run(ctx, p, env, force, monkeypatch)
     ref = runs[("fused", False)]
     for key, r in runs.items():
-        exact = not key[1]
         assert r["iters"] == ref["iters"] and r["status"] == ref["status"], key
         dp = np.abs(r["pose"] - ref["pose"]).max()
-        assert (dp == 0) if exact else (dp < 1e-12), (key, dp)
+        assert dp == 0, (key, dp)
         for ta, tb in zip(r["trace"], ref["trace"]):
             assert ta.n_valid == tb.n_valid and ta.n_kept == tb.n_kept, key
             assert list(ta.reject) == list(tb.reject), key
             dd = np.abs(np.array(ta.delta) - np.array(tb.delta)).max()
-            assert (dd == 0) if exact else (dd < 1e-12), (key, dd)
+            assert dd == 0, (key, dd)
     for path in PATHS:
         assert runs[(path, True)]["stats"]["uncertified"] > 0.3 * len(src[0]), (path, runs[(path, True)]["stats"])
     want = oc.register_frame(src, tgt, p)
