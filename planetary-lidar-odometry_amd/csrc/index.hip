@@ -59,9 +59,8 @@ __global__ void k_compact(const float* __restrict__ soa, size_t n, const unsigne
     if (kept_index) kept_index[o] = (unsigned)i;
 }
 
-__global__ void k_bbox_partial(const float4* __restrict__ pt, const int* __restrict__ count, float* __restrict__ part) {
+__global__ void k_bbox_partial(const float4* __restrict__ pt, int M, float* __restrict__ part) {
     __shared__ float red[6][kBlock];
-    int M = *count;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
         float4 p = pt[i];
@@ -81,7 +80,7 @@ __global__ void k_bbox_partial(const float4* __restrict__ pt, const int* __restr
     if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = red[threadIdx.x][0];
 }
 
-__global__ void k_bbox_final(const float* __restrict__ part, int nparts, float* __restrict__ bbox) {
+__global__ void k_bbox_final(const float* __restrict__ part, int nparts, float* __restrict__ bbox, float* __restrict__ qp) {
     __shared__ float red[6][kBlock];
     float r[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
     for (int b = threadIdx.x; b < nparts; b += kBlock)
@@ -100,19 +99,16 @@ __global__ void k_bbox_final(const float* __restrict__ part, int nparts, float* 
         __syncthreads();
     }
     if (threadIdx.x < 6) bbox[threadIdx.x] = red[threadIdx.x][0];
+    if (threadIdx.x == 0) {    // the quantisation (k_qparams' arithmetic), one launch fewer
+        const float ext = fmaxf(fmaxf(fmaxf(red[3][0] - red[0][0], red[4][0] - red[1][0]), red[5][0] - red[2][0]), 1e-6f);
+        qp[0] = red[0][0]; qp[1] = red[1][0]; qp[2] = red[2][0];
+        qp[3] = 65535.f / ext;
+    }
 }
 
-__global__ void k_qparams(const float* __restrict__ bbox, float* __restrict__ qp) {
-    if (threadIdx.x) return;
-    const float ext = fmaxf(fmaxf(fmaxf(bbox[3] - bbox[0], bbox[4] - bbox[1]), bbox[5] - bbox[2]), 1e-6f);
-    qp[0] = bbox[0]; qp[1] = bbox[1]; qp[2] = bbox[2];
-    qp[3] = 65535.f / ext;
-}
-
-__global__ void k_morton(const float4* __restrict__ pt, const int* __restrict__ count, const float* __restrict__ qp,
+__global__ void k_morton(const float4* __restrict__ pt, int M, const float* __restrict__ qp,
                          unsigned long long* __restrict__ key, unsigned* __restrict__ val) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    int M = *count;
     if (i >= M) return;
     float4 p = pt[i];
     key[i] = morton48(p.x, p.y, p.z, qp);
@@ -355,13 +351,20 @@ int filter_batch(hipStream_t s, const std::vector<FilterJob>& jobs, DevBuf& scra
 
 namespace {
 
+// The sort orders the Morton codes by their top 32 bits (bit 16 up: cells of 1/1625 of the bbox
+// extent per axis; stable, so deterministic).  The order only shapes the leaves and the query
+// packets — every search is exact whatever the order — and two radix passes fewer cost the lone
+// frame's index build ~20 µs less (round 4).  Leaf keys stay monotone in those bits, which is all
+// the seed bisection needs to land near the query.
+constexpr int kMortonSortLo = 16;
+
 // Permutation (sorted → input index) of n float4 points by 48-bit Morton code over their bbox.
 // With lkeys: also the first key of each B-point leaf and the quantisation (seed search).
 int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf& perm, std::string& err,
                 DevBuf* lkeys = nullptr, int B = 0) {
     size_t cub_bytes = 0;
     hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                       (unsigned*)nullptr, (unsigned*)nullptr, n, 0, 48, s);
+                                       (unsigned*)nullptr, (unsigned*)nullptr, n, kMortonSortLo, 48, s);
     const int bb_parts = 512;
     size_t need = 2 * (((size_t)n * 8 + 255) / 256 * 256) + (((size_t)n * 4 + 255) / 256 * 256) +
                   ((cub_bytes + 255) / 256) * 256 + bb_parts * 24 + 1024;
@@ -378,13 +381,12 @@ int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf
     const int L = B > 0 ? (n + B - 1) / B : 0;
     if (lkeys && !ensure(*lkeys, (size_t)L * 8 + 16, err)) return IMLS_ERR_DEVICE;
     if (lkeys) qp = (float*)((unsigned long long*)lkeys->p + L);   // qparams live after the keys
-    hipMemcpyAsync(cnt, &n, sizeof(int), hipMemcpyHostToDevice, s);
+    (void)cnt;
     int nb = std::min(bb_parts, (int)grid_for(n));
-    k_bbox_partial<<<nb, kBlock, 0, s>>>(pts, cnt, bbpart);
-    k_bbox_final<<<1, kBlock, 0, s>>>(bbpart, nb, bbox);
-    k_qparams<<<1, 64, 0, s>>>(bbox, qp);
-    k_morton<<<grid_for(n), kBlock, 0, s>>>(pts, cnt, qp, k0, v0);
-    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, (unsigned*)perm.p, n, 0, 48, s);
+    k_bbox_partial<<<nb, kBlock, 0, s>>>(pts, n, bbpart);
+    k_bbox_final<<<1, kBlock, 0, s>>>(bbpart, nb, bbox, qp);
+    k_morton<<<grid_for(n), kBlock, 0, s>>>(pts, n, qp, k0, v0);
+    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, (unsigned*)perm.p, n, kMortonSortLo, 48, s);
     if (lkeys) k_leaf_keys<<<grid_for(L), kBlock, 0, s>>>(k1, n, B, (unsigned long long*)lkeys->p);
     if (hipGetLastError() != hipSuccess) { err = "morton sort launch failed"; return IMLS_ERR_DEVICE; }
     return IMLS_OK;
@@ -633,7 +635,7 @@ int build_batch(hipStream_t s, std::vector<BuildJob>& jobs, DevBuf& scratch, Dev
     while ((1ll << (end_bit - 48)) < nj) ++end_bit;
     size_t cub_bytes = 0;
     hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                       (unsigned*)nullptr, (unsigned*)nullptr, (int)std::max<size_t>(total, 1), 0, end_bit, s);
+                                       (unsigned*)nullptr, (unsigned*)nullptr, (int)std::max<size_t>(total, 1), kMortonSortLo, end_bit, s);
     const size_t need = 2 * ((total * 8 + 255) / 256 * 256) + 2 * ((total * 4 + 255) / 256 * 256) +
                         (cub_bytes + 255) / 256 * 256 + (size_t)nj * (kBBoxParts * 6 * 4 + 256) + (leaf_floats + root_floats) * 4 +
                         (size_t)nj * 4 * 256 + 4096;
@@ -701,7 +703,7 @@ int build_batch(hipStream_t s, std::vector<BuildJob>& jobs, DevBuf& scratch, Dev
     k_bbox_b<<<dim3(std::min<unsigned>(kBBoxParts, gx), nj), kBlock, 0, s>>>(jd);
     k_qparams_b<<<nj, 64, 0, s>>>(jd);
     k_morton_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd, k0, v0);
-    if (total > 0) hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, v1, (int)total, 0, end_bit, s);
+    if (total > 0) hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, v1, (int)total, kMortonSortLo, end_bit, s);
     k_place_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd, k1, v1);
     bool any_tree = false;
     for (auto& b : jobs) any_tree |= b.B > 0 && b.n > 0;
