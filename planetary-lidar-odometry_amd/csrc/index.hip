@@ -351,12 +351,10 @@ int filter_batch(hipStream_t s, const std::vector<FilterJob>& jobs, DevBuf& scra
 
 namespace {
 
-// The sort orders the Morton codes by their top 32 bits (bit 16 up: cells of 1/1625 of the bbox
-// extent per axis; stable, so deterministic).  The order only shapes the leaves and the query
-// packets — every search is exact whatever the order — and two radix passes fewer cost the lone
-// frame's index build ~20 µs less (round 4).  Leaf keys stay monotone in those bits, which is all
-// the seed bisection needs to land near the query.
-constexpr int kMortonSortLo = 16;
+// The sort orders the full 48-bit Morton codes.  Sorting their top 32 bits only (two radix passes
+// fewer, the lone frame's index build ~15 µs shorter) coarsens the order inside 1/1625-extent cells:
+// config B's leaves and packets lose coherence, 423.7 → 397.5 pairs/s (round 4, profiles/r04_final3)
+constexpr int kMortonSortLo = 0;
 
 // Permutation (sorted → input index) of n float4 points by 48-bit Morton code over their bbox.
 // With lkeys: also the first key of each B-point leaf and the quantisation (seed search).

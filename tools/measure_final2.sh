@@ -13,7 +13,7 @@ step() {
   local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/$name.err; exit $rc; }
 }
 if [ "${PART:-1}" = 1 ]; then
-step gpu_tests 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+[ "${SKIP_TESTS:-0}" = 1 ] || step gpu_tests 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step bench_B 600 python3 bench.py
 step bench_stream 300 python3 bench.py --workload stream
@@ -24,6 +24,8 @@ step bench_stream_ransac 400 python3 bench.py --workload stream --no-cpu --solve
 step bench_A 400 python3 bench.py --workload A
 step bench_E 500 python3 bench.py --workload E
 step bench_B_q2000 400 python3 bench.py --queries 2000
+step bench_A_ransac 400 python3 bench.py --workload A --solver RANSAC_DRPM
+step bench_B_host 400 python3 bench.py --host-inputs --no-cpu
 step dist1 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
     --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu
 fi
