@@ -505,7 +505,9 @@ __device__ __forceinline__ double small_b(const float4& s4, const float4& d4, co
 __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const SolveState& st, imls_iter_trace* tr,
                                                  const KParams& kp,
                                                  int weighted, int update_pose) {
-    if (*st.done) return;
+    // the stop flag is read with the rows, not ahead of them (one dependent load fewer; the rows
+    // are only read before the test)
+    const int stopped = *st.done;
 #ifdef IMLS_DEBUG_WAVE_TRACE
     long long dbg_t = wall_clock64();
 #endif
@@ -548,6 +550,7 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
         rn[k] = v ? rows.cn[r] : make_float4(0.f, 0.f, 0.f, 0.f);
         rb[k] = small_b(rs[k], d4, rn[k]);
     }
+    if (stopped) return;              // block-uniform, before any LDS write or barrier
 #pragma unroll
     for (int k = 0; k < kSmallPer; ++k) {
         if (t + k * kSmallBlock < N && rs[k].w != 0.f) {
