@@ -459,6 +459,39 @@ int imls_sample_point_cloud(imls_ctx* ctx, const imls_sample_params* p, const fl
                             const float* last_xyz, size_t last_stride_floats, size_t m, int32_t* sampled_out,
                             size_t* n_sampled, float* bin_weights_out);
 
+/* ---- runtime options ------------------------------------------------------------------- */
+/* No reference equivalent: the documented tuning parameters and test hooks of the GPU path, per
+ * context (the library reads no environment variable except IMLS_DEBUG_HOST, a host-side trace).
+ * The defaults are the measured best; every value gives the same correspondences
+ * and poses (the tests run each against the default).  Contexts registered together
+ * (imls_register_frames) must share their options.  Returns IMLS_ERR_ARG for an unknown option or
+ * an invalid value (the option is then unchanged). */
+typedef enum imls_option {
+    IMLS_OPT_TRAVERSAL = 0,            /* imls_traversal (default IMLS_TRAVERSAL_AUTO) */
+    IMLS_OPT_LIST_REUSE = 1,           /* 1 (default): a query's neighbour list is reused without a
+                                          traversal while its certificate holds (Verlet lists); 0 off */
+    IMLS_OPT_TEMPORAL_SEED = 2,        /* 1 (default): iterations > 0 prefill the lists from the
+                                          previous iteration's; 0: every iteration seeds afresh */
+    IMLS_OPT_LEAF_SIZE = 3,            /* points per index leaf, a power of two in [4, 64] (default
+                                          64); applies from the next index build */
+    IMLS_OPT_FIRST_PACKET = 4,         /* queries per wave in the first ICP iteration(s) of a frame
+                                          registered alone: 16, 32 (default) or 64 */
+    IMLS_OPT_FIRST_PACKET_ITERS = 5,   /* ... for this many iterations (default 1) */
+    IMLS_OPT_FIRST_PACKET_BATCHED = 6, /* ... in batched registrations too: 0 (default) or 1 */
+    IMLS_OPT_TV_SKIN = 7,              /* tensor voting: a query's ball list is reused while it moved
+                                          <= skin metres (default 0.03; 0 = walk every iteration) */
+    IMLS_OPT_FORCE_FALLBACK = 8        /* test hook: every n-th query's list is treated as uncertified
+                                          (resolved by the exact search); 0 off (default) */
+} imls_option;
+typedef enum imls_traversal {
+    IMLS_TRAVERSAL_AUTO = 0,           /* one wave per query up to 16384 queries, packets above */
+    IMLS_TRAVERSAL_PACKETS = 1,        /* packets of 64 Morton-coherent queries per wave */
+    IMLS_TRAVERSAL_WAVE_PER_QUERY = 2, /* one wave per query */
+    IMLS_TRAVERSAL_LANE = 3            /* reference mode: every query by the exact per-lane search */
+} imls_traversal;
+int imls_set_option(imls_ctx* ctx, int32_t option, double value);
+int imls_get_option(imls_ctx* ctx, int32_t option, double* value);
+
 /* ---- instrumentation ------------------------------------------------------------------- */
 /* When enabled, HIP events bracket every launch of the projection kernel (on the stream it is
  * launched on); imls_kernel_timing returns the accumulated milliseconds and launch count since

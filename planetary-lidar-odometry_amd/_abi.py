@@ -20,6 +20,15 @@ IMLS_FINAL_LS, IMLS_FINAL_WEIGHTED_LS, IMLS_FINAL_DRPM = 0, 1, 2
 IMLS_FRAME_MAX_ITERS, IMLS_FRAME_CONVERGED, IMLS_FRAME_TOO_FEW, IMLS_FRAME_SOLVE_FAILED = 0, 1, 2, 3
 REJECT_NAMES = ("no_normal", "too_far", "invalid_normal", "normal_constraint", "mls_fail", "nan_inf_height")
 IMLS_NUM_REJ = 6
+# imls_set_option (include/imls_gpu.h "runtime options"): option ids and the traversal values
+(IMLS_OPT_TRAVERSAL, IMLS_OPT_LIST_REUSE, IMLS_OPT_TEMPORAL_SEED, IMLS_OPT_LEAF_SIZE, IMLS_OPT_FIRST_PACKET,
+ IMLS_OPT_FIRST_PACKET_ITERS, IMLS_OPT_FIRST_PACKET_BATCHED, IMLS_OPT_TV_SKIN, IMLS_OPT_FORCE_FALLBACK) = range(9)
+IMLS_TRAVERSAL_AUTO, IMLS_TRAVERSAL_PACKETS, IMLS_TRAVERSAL_WAVE_PER_QUERY, IMLS_TRAVERSAL_LANE = 0, 1, 2, 3
+OPTION_IDS = {"traversal": IMLS_OPT_TRAVERSAL, "list_reuse": IMLS_OPT_LIST_REUSE,
+              "temporal_seed": IMLS_OPT_TEMPORAL_SEED, "leaf_size": IMLS_OPT_LEAF_SIZE,
+              "first_packet": IMLS_OPT_FIRST_PACKET, "first_packet_iters": IMLS_OPT_FIRST_PACKET_ITERS,
+              "first_packet_batched": IMLS_OPT_FIRST_PACKET_BATCHED, "tv_skin": IMLS_OPT_TV_SKIN,
+              "force_fallback": IMLS_OPT_FORCE_FALLBACK}
 
 STATUS_NAMES = {0: "IMLS_OK", -1: "IMLS_ERR_ARG", -2: "IMLS_ERR_DEVICE", -3: "IMLS_ERR_STATE",
                 -4: "IMLS_ERR_UNSUPPORTED", -5: "IMLS_ERR_CAPACITY"}
@@ -211,6 +220,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "imls_map_clear": (C.c_int, [VP]),
         "imls_map_size": (C.c_int, [VP, P(SZ), P(SZ)]),
         "imls_set_defer": (C.c_int, [VP, C.c_int]),
+        "imls_set_option": (C.c_int, [VP, C.c_int32, C.c_double]),
+        "imls_get_option": (C.c_int, [VP, C.c_int32, P(C.c_double)]),
         "imls_capture_correspondences": (C.c_int, [VP, C.c_int]),
         "imls_captured_correspondences": (C.c_int, [VP, C.c_int, SZ, VP, VP, VP, VP, P(SZ)]),
         "imls_timing_origin": (C.c_int, [VP]),
@@ -237,7 +248,7 @@ ABI_SYMBOLS = (
     "imls_register_frames", "imls_register_frames_async", "imls_register_frames_result",
     "imls_default_front_params", "imls_scan_front_end", "imls_enable_stats", "imls_set_defer",
     "imls_timing_origin", "imls_timing_intervals", "imls_capture_correspondences",
-    "imls_captured_correspondences",
+    "imls_captured_correspondences", "imls_set_option", "imls_get_option",
 )
 
 _LIB = None

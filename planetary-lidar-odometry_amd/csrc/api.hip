@@ -18,12 +18,33 @@
 #include <thread>
 #include <mutex>
 #include <vector>
+#include <unistd.h>
 
 #include "internal.h"
 
 using namespace imlsgpu;
 
 constexpr int kTimingKinds = 8;   // projection, index, solve chain, k_knn_wave, k_finish, k_ring_pca, k_major_avg, front end
+
+// Runtime options of a context (imls_set_option; include/imls_gpu.h documents each): the validated
+// tuning parameters and test hooks.  Nothing is read from the environment.
+struct Options {
+    int traversal = IMLS_TRAVERSAL_AUTO;
+    int list_reuse = 1;
+    int temporal_seed = 1;
+    int leaf_size = 64;
+    int first_packet = 32;
+    int first_packet_iters = 1;
+    int first_packet_batched = 0;
+    double tv_skin = 0.03;
+    int force_fallback = 0;
+};
+
+inline bool same_options(const Options& a, const Options& b) {
+    return a.traversal == b.traversal && a.list_reuse == b.list_reuse && a.temporal_seed == b.temporal_seed &&
+           a.leaf_size == b.leaf_size && a.first_packet == b.first_packet && a.first_packet_iters == b.first_packet_iters &&
+           a.first_packet_batched == b.first_packet_batched && a.tv_skin == b.tv_skin && a.force_fallback == b.force_fallback;
+}
 
 struct imls_ctx {
     int device = 0;
@@ -45,7 +66,8 @@ struct imls_ctx {
     std::vector<DevBuf> slot_pool;        // freed slots, reused (no allocation per frame)
     DevBuf macc;
     size_t map_points = 0;                // Σ n over the FIFO (before the NaN filter)
-    DevBuf fb;                            // fallback query list + count
+    DevBuf fb;                            // deferred-query counts per k_finish block + their lists
+    size_t fb_off = 64;                   // words: start of the lists in fb
     DevBuf lkeys;                         // leaf first Morton keys + quantisation (seed search)
     DevBuf rnr;                           // recomputed map normals (count mode), Morton order
     bool rnr_valid = false;
@@ -60,8 +82,9 @@ struct imls_ctx {
     DevBuf front_mem;                     // imls_scan_front_end scratch
     size_t n_target_in = 0;               // input size of the last set_target (tensor arrays match it)
     bool has_tensors = false;
-    int lane_mode = 0;
-    int temporal_seed = 1;
+    Options opt;                          // imls_set_option
+    int lane_mode = 0;                    // opt.traversal == IMLS_TRAVERSAL_LANE
+    int temporal_seed = 1;                // opt.temporal_seed
     int N = 0;
     bool has_source = false;
     // deferred index builds: set_target / map_push / set_source without a requested count only
@@ -164,7 +187,7 @@ bool grow(DevBuf& b, size_t bytes) {
     return true;
 }
 
-KParams make_kparams(const imls_params& p) {
+KParams make_kparams(const imls_params& p, const Options& o) {
     KParams k{};
     k.h2 = p.h * p.h;
     k.r2 = p.r * p.r;
@@ -197,73 +220,30 @@ KParams make_kparams(const imls_params& p) {
         k.angle_on = p.picp_normal_angle_constraint ? 1 : 0;
         k.angle_thr_deg = p.picp_angle_diff_threshold;
     }
-    k.seed_half = 1;
-    k.reseed = 0.25f;
-    k.sparse_lanes = 32;
-    if (const char* w = std::getenv("IMLS_SPARSE")) k.sparse_lanes = std::atoi(w);
-    k.packet = 64;
+    // traversal (imls_set_option, include/imls_gpu.h): −1 auto = one wave per query up to
+    // kQwaveAutoN queries (the exact stage fused in for ≤ kSmallRows), packets above
+    k.qwave = o.traversal == IMLS_TRAVERSAL_PACKETS ? 0 : o.traversal == IMLS_TRAVERSAL_WAVE_PER_QUERY ? 1 : -1;
     // one frame alone on the GPU (imls_register_frame): its first ICP iteration, where every lane
     // seeds, traverses in 32-query packets (the launch lasts as long as its slowest wave; measured
     // on config B, one pair: k_knn_wave 240 -> 229 us per launch, 8.35 -> 8.14 ms per pair).
     // Batched launches keep 64 (with 4 pairs in flight 32 measured 295 vs 305 pairs/s: the GPU is
     // then throughput-bound and the idle half-waves cost more than the shorter tail saves).
-    k.pk_small = 32;
-    k.pk_iters = 1;
-    k.pk_batch = 0;
-    if (const char* w = std::getenv("IMLS_PACKET")) k.pk_small = std::atoi(w) == 16 ? 16 : std::atoi(w) == 32 ? 32 : 64;
-    if (const char* w = std::getenv("IMLS_PACKET_ITERS")) k.pk_iters = std::atoi(w);
-    if (const char* w = std::getenv("IMLS_PACKET_BATCH")) k.pk_batch = std::atoi(w);
-    k.qwave = -1;   // auto
-    if (const char* w = std::getenv("IMLS_QWAVE")) k.qwave = std::atoi(w);
-    if (const char* w = std::getenv("IMLS_SEED_HALF")) k.seed_half = std::atoi(w);
-    if (const char* w = std::getenv("IMLS_RESEED")) k.reseed = (float)std::atof(w);
-    if (const char* w = std::getenv("IMLS_WAVE_TRACE")) k.wave_trace = std::atoi(w);
-    k.wide = 3;
-    if (const char* w = std::getenv("IMLS_WIDE")) k.wide = std::max(1, std::min(3, std::atoi(w)));
-    // Verlet-list reuse: on for the packet traversal; the wave-per-query traversal had it off while the
-    // config C-like stream ran on it (0.109 ms per launch without vs 0.141 ms with it, 4 in flight)
-    k.verlet = 1;
-    // (round 4) on for the wave-per-query traversal too: it now serves lone small frames (latency) and
-    // batches under kQwaveAutoN queries only — a lone 1949-query frame 1.95 -> 1.84 ms
-    k.qverlet = 1;
-    if (const char* w = std::getenv("IMLS_VERLET")) k.verlet = k.qverlet = std::atoi(w);
-    if (const char* w = std::getenv("IMLS_QVERLET")) k.qverlet = std::atoi(w);
-    k.verlet2 = k.verlet;
-    if (const char* w = std::getenv("IMLS_VERLET2")) k.verlet2 = std::atoi(w);
-    k.force_fb = 0;
-    if (const char* w = std::getenv("IMLS_FORCE_FALLBACK")) k.force_fb = std::max(0, std::atoi(w));
-    k.lockstep = 1;
-    if (const char* w = std::getenv("IMLS_LOCKSTEP")) k.lockstep = std::atoi(w);
-    k.bcast_lock = 0;
-    k.xcd = -1;
-    if (const char* w = std::getenv("IMLS_XCD")) k.xcd = std::atoi(w);
-    if (const char* w = std::getenv("IMLS_BCAST_LOCK")) k.bcast_lock = std::atoi(w);
-    k.seed_keys = 0;
-    if (const char* w = std::getenv("IMLS_SEED_KEYS")) k.seed_keys = std::atoi(w);
-    k.kl20 = 22;
-    if (const char* w = std::getenv("IMLS_KL")) k.kl20 = std::atoi(w);
-    k.lazy_listed = 1;
-    if (const char* w = std::getenv("IMLS_LAZY_LISTED")) k.lazy_listed = std::atoi(w);
-    k.lds_list = 1;   // measured: config B 331 → 378 pairs/s, one-pair k_knn_wave 227 → 189 µs (r04b)
-    if (const char* w = std::getenv("IMLS_LDS_LIST")) k.lds_list = std::atoi(w);
-    k.qfinish = 1;   // measured: a lone 1949-query frame 2.21 -> 1.95 ms (k_finish 30 -> 16.7 us per iteration)
-    if (const char* w = std::getenv("IMLS_QFINISH")) k.qfinish = std::atoi(w);
-    k.qfuse = 1;
-    if (const char* w = std::getenv("IMLS_QFUSE")) k.qfuse = std::atoi(w);
-    k.bottom_up = 1;
-    if (const char* w = std::getenv("IMLS_BOTTOM_UP")) k.bottom_up = std::atoi(w);
-    k.frontier = 1;
-    if (const char* w = std::getenv("IMLS_FRONTIER")) k.frontier = std::atoi(w);
-    k.qexact = 1;
-    if (const char* w = std::getenv("IMLS_QEXACT")) k.qexact = std::atoi(w);
+    k.packet = 64;
+    k.pk_small = o.first_packet;
+    k.pk_iters = o.first_packet_iters;
+    k.pk_batch = o.first_packet_batched;
+    // Verlet-list reuse (and the prefill certificate), both traversals (round 4: a lone 1949-query
+    // frame 1.95 -> 1.84 ms with it on the wave-per-query traversal)
+    k.reuse = o.list_reuse;
+    k.force_fb = o.force_fallback;
+    k.xcd = -1;   // auto: XCD-grouped frames for batches of ≥ 16 frames
     // tensor voting replaces the NN-1 normal only on the IMLS matcher's get_normals=false branch
     // (imls_icp.cpp:514, 630-644); the IMLS neighbours keep the recompute branch (404-434)
     k.tv = (p.use_tensor_voting && !p.get_normals && p.matching_method == IMLS_MATCH_IMLS) ? 1 : 0;
     k.tv_k = p.tensor_k;
     k.tv_sigma = p.tensor_sigma;
     k.tv_thr = p.tensor_distance_threshold;
-    k.tv_skin = 0.03f;
-    if (const char* w = std::getenv("IMLS_TV_SKIN")) k.tv_skin = (float)std::atof(w);
+    k.tv_skin = (float)o.tv_skin;
     k.cos_thr = std::cos(k.angle_thr_deg * M_PI / 180.0);
     return k;
 }
@@ -299,11 +279,12 @@ int ensure_solve(imls_ctx* c, int N) {
     if (c->st_N >= N && c->st.trace) return IMLS_OK;
     size_t n = (size_t)std::max(N, 1);
     n += n / 4 + 64;                      // headroom (see grow): the next frames' N differ a little
-    if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, n * 4 + 256))
+    // deferred (uncertified) queries: k_finish block b writes its count to word b and its queries,
+    // in slot order, to the region fb_off + b·256 (project.hip finish_body, k_project_lane)
+    const size_t nfb = (n + 255) / 256;
+    c->fb_off = (nfb + 63) / 64 * 64;
+    if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, (c->fb_off + nfb * 256) * 4))
         return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
-    // deferred-query counter [0] and the fallback's arrival counter [1]: zero from here on (the
-    // launches that use them leave them zero)
-    if (hipMemsetAsync(c->fb.p, 0, 256, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipMemset (fb)");
     if (!grow(c->prevnn, prevnn_bytes((int)n))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
     if (!grow(c->tvn, n * kTvBytesPerQuery)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tvn)");
     const int pb = std::max(project_blocks((int)n), solve_blocks((int)n)) + 1;
@@ -433,7 +414,7 @@ int ensure_trace(imls_ctx* c, int iters) {
 
 unsigned* fb_count(imls_ctx* c) { return (unsigned*)c->fb.p; }
 unsigned long long* stats_ptr(imls_ctx* c) { return c->collect_stats ? (unsigned long long*)c->stats.p : nullptr; }
-unsigned* fb_list(imls_ctx* c) { return (unsigned*)c->fb.p + 64; }
+unsigned* fb_list(imls_ctx* c) { return (unsigned*)c->fb.p + c->fb_off; }
 
 TreeView tree_view(imls_ctx* c) {
     TreeView t;
@@ -542,7 +523,8 @@ public:
     // fn(i0, i1) over [0, n) in `parts` contiguous chunks (parts ≤ width()), the caller taking the first
     void run(size_t n, size_t parts, const std::function<void(size_t, size_t)>& fn) {
         parts = std::max<size_t>(1, std::min(parts, width()));
-        if (parts == 1 || n == 0) {
+        // a forked child inherits the pool object but not its threads: pack serially there
+        if (parts == 1 || n == 0 || getpid() != pid_) {
             fn(0, n);
             return;
         }
@@ -569,6 +551,7 @@ public:
         std::unique_lock<std::mutex> lk(mu_);
         done_cv_.wait(lk, [&] { return pending_ == 0; });
         fn_ = nullptr;
+        last_job_ns_.store(now_ns(), std::memory_order_release);
     }
 
 private:
@@ -578,8 +561,6 @@ private:
         size_t hw = std::max<unsigned>(std::thread::hardware_concurrency(), 1u);
         if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::min<size_t>(hw, (size_t)std::max(1, std::atoi(e)));
         size_t cap = kMaxHelpers;
-        if (const char* e = std::getenv("IMLS_PACK_THREADS")) cap = (size_t)std::max(0, std::atoi(e) - 1);
-        if (const char* e = std::getenv("IMLS_PACK_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
         const size_t helpers = std::min<size_t>(cap, hw > 1 ? hw - 1 : 0);
         for (size_t k = 0; k < helpers; ++k) workers_.emplace_back([this, k] { loop(k + 1); });
     }
@@ -598,9 +579,12 @@ private:
             size_t i0, i1;
             bool mine;
             {
-                // a job soon after the last one (frames back to back) starts without a wake-up
+                // a job soon after the last one (frames back to back) starts without a wake-up: a
+                // helper polls up to spin_us_ only while jobs come in bursts (the last one ended
+                // < kBurstNs ago), so an idle pool sleeps at once instead of holding cores
                 const auto t0 = std::chrono::steady_clock::now();
-                while (gen_seen_.load(std::memory_order_acquire) == seen &&
+                const bool burst = now_ns() - last_job_ns_.load(std::memory_order_acquire) < kBurstNs;
+                while (burst && gen_seen_.load(std::memory_order_acquire) == seen &&
                        std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us_)) {
                 }
                 std::unique_lock<std::mutex> lk(mu_);
@@ -627,6 +611,12 @@ private:
     static constexpr size_t kMaxHelpers = 15;
     std::atomic<uint64_t> gen_seen_{0};       // gen_, readable without the mutex (the helpers' poll)
     std::atomic<size_t> pending_left_{0};      // pending_, likewise (the caller's poll)
+    static int64_t now_ns() {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    static constexpr int64_t kBurstNs = 2000000;   // 2 ms
+    std::atomic<int64_t> last_job_ns_{0};
+    const pid_t pid_ = getpid();
     int spin_us_ = 200;
     uint64_t gen_ = 0;
     bool stop_ = false;
@@ -1075,12 +1065,6 @@ imls_ctx* imls_create(int device, const imls_params* p) {
         delete c;
         return nullptr;
     }
-    if (const char* b = std::getenv("IMLS_BUCKET")) {
-        int v = std::atoi(b);
-        if (v >= 4 && v <= 64 && (v & (v - 1)) == 0) c->B = v;   // a leaf is one wave-wide load
-    }
-    if (const char* m = std::getenv("IMLS_TRAVERSAL")) c->lane_mode = std::string(m) == "lane";
-    if (const char* m = std::getenv("IMLS_TEMPORAL_SEED")) c->temporal_seed = std::atoi(m) != 0;
     imls_params d;
     imls_default_params(&d);
     d.solve_method = IMLS_SOLVE_LS;
@@ -1142,7 +1126,78 @@ int imls_set_params(imls_ctx* c, const imls_params* p) {
         c->rng_dirty = true;
     }
     c->P = *p;
-    c->kp = make_kparams(*p);
+    c->kp = make_kparams(*p, c->opt);
+    return IMLS_OK;
+}
+
+int imls_set_option(imls_ctx* c, int32_t option, double value) {
+    if (!c) return IMLS_ERR_ARG;
+    if (!std::isfinite(value)) return fail(c, IMLS_ERR_ARG, "option value must be finite");
+    const int v = (int)value;
+    const bool integral = (double)v == value;
+    Options& o = c->opt;
+    switch (option) {
+    case IMLS_OPT_TRAVERSAL:
+        if (!integral || v < IMLS_TRAVERSAL_AUTO || v > IMLS_TRAVERSAL_LANE) return fail(c, IMLS_ERR_ARG, "traversal: 0..3");
+        o.traversal = v;
+        break;
+    case IMLS_OPT_LIST_REUSE:
+        if (!integral || (v != 0 && v != 1)) return fail(c, IMLS_ERR_ARG, "list_reuse: 0 or 1");
+        o.list_reuse = v;
+        break;
+    case IMLS_OPT_TEMPORAL_SEED:
+        if (!integral || (v != 0 && v != 1)) return fail(c, IMLS_ERR_ARG, "temporal_seed: 0 or 1");
+        o.temporal_seed = v;
+        break;
+    case IMLS_OPT_LEAF_SIZE:   // a leaf is one wave-wide load
+        if (!integral || v < 4 || v > 64 || (v & (v - 1))) return fail(c, IMLS_ERR_ARG, "leaf_size: a power of two in [4, 64]");
+        o.leaf_size = v;
+        break;
+    case IMLS_OPT_FIRST_PACKET:
+        if (!integral || (v != 16 && v != 32 && v != 64)) return fail(c, IMLS_ERR_ARG, "first_packet: 16, 32 or 64");
+        o.first_packet = v;
+        break;
+    case IMLS_OPT_FIRST_PACKET_ITERS:
+        if (!integral || v < 0) return fail(c, IMLS_ERR_ARG, "first_packet_iters: >= 0");
+        o.first_packet_iters = v;
+        break;
+    case IMLS_OPT_FIRST_PACKET_BATCHED:
+        if (!integral || (v != 0 && v != 1)) return fail(c, IMLS_ERR_ARG, "first_packet_batched: 0 or 1");
+        o.first_packet_batched = v;
+        break;
+    case IMLS_OPT_TV_SKIN:
+        if (value < 0.0 || value > 1.0) return fail(c, IMLS_ERR_ARG, "tv_skin: [0, 1] m");
+        o.tv_skin = value;
+        break;
+    case IMLS_OPT_FORCE_FALLBACK:
+        if (!integral || v < 0) return fail(c, IMLS_ERR_ARG, "force_fallback: >= 0");
+        o.force_fallback = v;
+        break;
+    default:
+        return fail(c, IMLS_ERR_ARG, "unknown option");
+    }
+    c->B = o.leaf_size;                          // the next index build
+    c->lane_mode = o.traversal == IMLS_TRAVERSAL_LANE;
+    c->temporal_seed = o.temporal_seed;
+    c->kp = make_kparams(c->P, o);
+    return IMLS_OK;
+}
+
+int imls_get_option(imls_ctx* c, int32_t option, double* value) {
+    if (!c || !value) return IMLS_ERR_ARG;
+    const Options& o = c->opt;
+    switch (option) {
+    case IMLS_OPT_TRAVERSAL: *value = o.traversal; break;
+    case IMLS_OPT_LIST_REUSE: *value = o.list_reuse; break;
+    case IMLS_OPT_TEMPORAL_SEED: *value = o.temporal_seed; break;
+    case IMLS_OPT_LEAF_SIZE: *value = o.leaf_size; break;
+    case IMLS_OPT_FIRST_PACKET: *value = o.first_packet; break;
+    case IMLS_OPT_FIRST_PACKET_ITERS: *value = o.first_packet_iters; break;
+    case IMLS_OPT_FIRST_PACKET_BATCHED: *value = o.first_packet_batched; break;
+    case IMLS_OPT_TV_SKIN: *value = o.tv_skin; break;
+    case IMLS_OPT_FORCE_FALLBACK: *value = o.force_fallback; break;
+    default: return fail(c, IMLS_ERR_ARG, "unknown option");
+    }
     return IMLS_OK;
 }
 
@@ -1649,8 +1704,8 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
         pc.ransac_seed = pl.ransac_seed = 0;    // each context runs its own rand() stream
         if (std::memcmp(&pc, &pl, sizeof(imls_params)) != 0)
             return fail(L, IMLS_ERR_ARG, "batch contexts must share their params (context " + std::to_string(k) + ")");
-        if (c->lane_mode != L->lane_mode || c->temporal_seed != L->temporal_seed || c->B != L->B)
-            return fail(L, IMLS_ERR_ARG, "batch contexts must share their traversal settings");
+        if (!same_options(c->opt, L->opt))
+            return fail(L, IMLS_ERR_ARG, "batch contexts must share their options (imls_set_option)");
         if (c->pending || c->batch_member || (k > 0 && c->batch_pending))
             return fail(L, IMLS_ERR_STATE, "context " + std::to_string(k) + " has a frame pending");
     }

@@ -49,31 +49,15 @@ struct KParams {
     int matcher;              // imls_match_method: 0 IMLS, 1 plane_ICP (NN-1 tangent-plane projection)
     int proj;                 // projected-distance candidate rule (brute force in the reference)
     double gate_dist, gate_proj;   // proj mode: ‖p−x‖ < gate_dist and ‖(p−x)×n_s‖ < gate_proj
-    int seed_half;            // seed pass scans the nearest leaf ± seed_half Morton neighbours
-    float reseed;             // temporal seed unless displacement² > reseed · previous worst key
-    int sparse_lanes;         // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
-    int qwave;                // traversal: 0 = packets of 64 queries per wave, 1 = one wave per query
+    // traversal tuning: documented runtime options (imls_set_option, include/imls_gpu.h), fixed
+    // constants otherwise (project.hip: kSeedHalf, kReseed, kSparseLanes, kWide)
+    int qwave;                // traversal: −1 auto (one wave per query up to kQwaveAutoN queries), 0 packets, 1 wave per query
     int packet;               // packet traversal: queries per wave in this launch (64, or 32 / 16: see pk_small)
     int pk_small, pk_iters;   // the first pk_iters ICP iterations (mostly seeding lanes) use pk_small-query packets
     int pk_batch;             // … in batched launches too (imls_register_frames; off: measured slower there)
-    int wide;                 // packet traversal: binary levels descended per step (1..3)
-    int verlet;               // reuse a query's list without traversal while its certification holds
-    int verlet2;              // … or while the re-measured prefilled list certifies itself (packet traversal)
-    int force_fb;             // test hook: every force_fb-th query slot deferred to the exact fallback (0 off)
-    int qverlet;              // the same for the wave-per-query traversal (off by default: measured slower)
-    int lockstep;             // packet traversal: per-lane candidate masks, then lockstep insertion
-    int bcast_lock;           // … also for broadcast leaves: 0 never, 1 first ICP iteration, 2 always
-    int seed_keys;            // packet traversal: the seed keeps keys only and yields a bound cap; the list refills from empty
-    int kl20;                 // list length (K + slack) used for search_number 17..20: 22 (default), 24 or 26
-    int lazy_listed;          // packet traversal: listed-point masks only for leaves with more candidates than listed points
-    int lds_list;             // packet traversal: slot-id keys in registers, list positions in LDS (project.hip IdKeys)
-    int qfinish;              // one-frame launches with the wave-per-query traversal: exact stage one wave per query
-    int qfuse;                // with qfinish: the exact stage inside the traversal kernel (k_knn_qwave_f)
-    int bottom_up;            // wave-per-query traversal: start at a leaf with the path's sibling boxes stacked
-    int frontier;             // wave-per-query traversal: up to 8 stacked entries per step, 8 lanes each
-    int qexact;               // fused lone-frame path: an uncertified query's exact list in the wave (no fallback launch)
+    int reuse;                // Verlet reuse of a query's list without traversal while its certificate holds
+    int force_fb;             // test hook: every force_fb-th query slot's list treated as uncertified (0 off)
     int xcd;                  // batched projection: frames grouped per XCD round-robin slot (−1 auto: ≥ 16 frames)
-    int wave_trace;           // debug (IMLS_WAVE_TRACE=1): per-wave cycle/visit printf from k_knn_wave
     int tv;                   // tensor-voting normals (use_tensor_voting && !get_normals, IMLS matcher)
     int tv_k;                 // use_tensor_voting.k (≤ kTvMaxK)
     double tv_sigma, tv_thr;  // use_tensor_voting.sigma, .distance_threshold

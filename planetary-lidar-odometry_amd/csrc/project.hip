@@ -27,7 +27,7 @@
 //   y = float(x − height·n_NN), and the pass-1 normal-equation partials of the LS solve
 //   (solver.cpp:89-107): 21 JᵀJ + 6 Jᵀb + count per block, fp64.
 // k_project_lane — one lane per query, exact fp64 list during the traversal (the fallback, and
-// the IMLS_TRAVERSAL=lane reference mode).
+// the IMLS_TRAVERSAL_LANE reference mode, imls_set_option).
 // Compiled with -ffp-contract=off: every fp64 expression evaluates as written.
 #include <algorithm>
 #include <cfloat>
@@ -52,11 +52,20 @@ constexpr int kWideMax = 8;         // packet traversal: children tested per ste
 constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
 constexpr int kFStack = 256;        // frontier traversal's stack per wave (see knn_qwave_body)
 constexpr int kFBatchMax = 128;     // above this many entries: one entry per step (DFS growth ≤ 8 × 7)
+// frontier stack bound: a step at ≤ kFBatchMax entries pushes ≤ 8 groups × 8 children; above it one
+// entry per step grows the stack by ≤ 7 per descent step, and a walk descends ≤ ⌈(kStackDepth−1)/kWide⌉
+// steps (the index refuses deeper trees, index.hip) — so fsp never exceeds kFStack
+static_assert(kFBatchMax + 64 + 7 * ((24 + 2) / 3) <= kFStack, "frontier stack bound");
 #ifndef IMLS_SEED_CHUNK
 #define IMLS_SEED_CHUNK 8
 #endif
 constexpr int kSeedChunk = IMLS_SEED_CHUNK;   // per-lane reseed: points loaded per batch
 constexpr int kSeedTab = 1024;                // seed search: coarse leaf-key table entries in LDS (8 KB)
+// traversal constants (measured in rounds 1-4; no runtime selectors)
+constexpr int kSeedHalf = 1;        // a seed scans the query's Morton leaf ± 1 neighbour leaf
+constexpr float kReseed = 0.25f;    // temporal seed unless displacement² > kReseed · previous worst key
+constexpr int kSparseLanes = 32;    // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
+constexpr int kWide = 3;            // binary levels descended per traversal step (8 boxes per step)
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
 constexpr double kCertSlack = 1.0 + 4e-7;
 
@@ -419,16 +428,10 @@ __device__ __forceinline__ float need_key_ids(const float (&lk)[KL], float r2, i
     return cnt_r >= K ? fmaxf(dK, d1) : kInfF;
 }
 
-// Register cap of the packet traversal: 216 VGPRs (2 waves/SIMD) uncapped; capping at 3 waves/SIMD
-// (168 VGPRs) spills ~56 VGPRs of cold-path state to scratch and measured +4-5 % pairs/s with 4 pairs
-// in flight (more resident waves hide the dependent node/leaf loads).  Longer lists (KL > 24) keep
-// the uncapped allocation.
-#ifndef IMLS_KNN_WPE
-#define IMLS_KNN_WPE 3
-#endif
-// LDSL (slot-id keys, positions in LDS): ~96 VGPRs and ~29 KB of LDS per 4-wave block — 5 waves/SIMD
-#define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(LDSL ? (KL <= 24 ? 5 : 2) : (KL <= 24 ? IMLS_KNN_WPE : 1))))
-template <int KL, bool LOCKSTEP, bool LDSL>
+// Slot-id keys in registers, positions in LDS: ~96 VGPRs and ~29 KB of LDS per 4-wave block — 5
+// waves/SIMD (round 4: the register list needed 160 VGPRs, 3 waves/SIMD; config B 331 → 406 pairs/s)
+#define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 24 ? 5 : 2)))
+template <int KL>
 __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
                                                          const double* __restrict__ pose,
@@ -437,15 +440,13 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                                                          int* __restrict__ lists, float* __restrict__ wlist,
                                                          float4* __restrict__ xref, float* __restrict__ nref,
                                                          int use_prev, unsigned long long* __restrict__ nbr_stats,
-                                                         unsigned* __restrict__ fb_count, int bx) {
+                                                         int bx) {
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float4 sboxa[kWaveBlock / 64][kWaveStack];   // stacked node boxes: lo.xyz, hi.x
     __shared__ float2 sboxb[kWaveBlock / 64][kWaveStack];   //                     hi.yz
-    // the current leaf's points for the lockstep insertion (LDSL: fetched by ds_bpermute instead)
-    __shared__ float4 sleaf[kWaveBlock / 64][LDSL ? 1 : 64];
-    // LDSL: the list's positions, slot s of thread tid at spos[s][tid] (slot-id keys, IdKeys)
-    __shared__ int spos[LDSL ? KL : 1][kWaveBlock];
+    // the list's positions, slot s of thread tid at spos[s][tid] (slot-id keys, IdKeys)
+    __shared__ int spos[KL][kWaveBlock];
     const int tid = threadIdx.x, lane = tid & 63;
     int* const mypos = &spos[0][tid];
     using IK = IdKeys<KL>;
@@ -463,39 +464,28 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         transform_query(pose, spt[i], make_float4(0.f, 0.f, 0.f, 0.f), 0, xf, ns);
     }
     float lk[KL];
-    int lp[KL];     // register list only (!LDSL)
 #pragma unroll
-    for (int j = 0; j < KL; ++j) {
-        lk[j] = LDSL ? IK::empty(j) : kInfF;
-        if (!LDSL) lp[j] = -1;
-    }
-    // (LDSL: the slots are cleared here when no seed table is staged; in the first ICP iteration the
-    // table aliases spos and they are cleared after the seed search, below)
-    if (LDSL && use_prev) {
+    for (int j = 0; j < KL; ++j) lk[j] = IK::empty(j);
+    // the slots are cleared here when no seed table is staged; in the first ICP iteration the table
+    // aliases spos and they are cleared after the seed search, below
+    if (use_prev) {
 #pragma unroll
         for (int j = 0; j < KL; ++j) mypos[j * kWaveBlock] = -1;
     }
     // the list behind one interface: thr_ = the strict insertion threshold (a point with key d joins
     // iff d < thr_()), ins_ = sorted insertion (precondition d < thr_()), pos_ = position of slot s
     // (any order), full_ = KL real entries, need_ = need_key (upper-rounded for slot-id keys)
-    auto thr_ = [&]() -> float { return LDSL ? IK::lo(lk[KL - 1]) : lk[KL - 1]; };
-    auto full_ = [&]() -> bool { return LDSL ? IK::real(lk[KL - 1]) : lk[KL - 1] < kInfF; };
-    auto pos_ = [&](int s) -> int { return LDSL ? mypos[s * kWaveBlock] : lp[s]; };
-    auto need_ = [&]() -> float { return LDSL ? need_key_ids<KL>(lk, (float)kp.r2, kp.K) : need_key<KL>(lk, (float)kp.r2, kp.K); };
+    auto thr_ = [&]() -> float { return IK::lo(lk[KL - 1]); };
+    auto full_ = [&]() -> bool { return IK::real(lk[KL - 1]); };
+    auto pos_ = [&](int s) -> int { return mypos[s * kWaveBlock]; };
+    auto need_ = [&]() -> float { return need_key_ids<KL>(lk, (float)kp.r2, kp.K); };
     auto ins_ = [&](float d, int pos) {
-        if constexpr (LDSL) {
-            const unsigned s = IK::id(lk[KL - 1]);
-            insert_key<KL>(lk, IK::make(d, s));
-            mypos[s * kWaveBlock] = pos;
-        } else {
-            insert_top<KL>(lk, lp, d, pos);
-        }
+        const unsigned s = IK::id(lk[KL - 1]);
+        insert_key<KL>(lk, IK::make(d, s));
+        mypos[s * kWaveBlock] = pos;
     };
     const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
     float bnd = active ? r2s : -1.0f;
-    // the lane's bound cap: r2s, or (seed_keys) the seed's KL-th key — a bound the final KL-th key
-    // never exceeds (KL seed points lie within it), kept while the list refills from empty
-    float bcap = r2s;
     const int P = t.P, B = t.B, M = t.M;
 #ifdef IMLS_DEBUG_WAVE_TRACE
     const long long dbg_t0 = wall_clock64();
@@ -516,16 +506,17 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             }
         const float tn = (float)sqrt(delta[3] * delta[3] + delta[7] * delta[7] + delta[11] * delta[11]);
         const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
-        greedy = disp * disp > kp.reseed * wlist[slot];
+        greedy = disp * disp > kReseed * wlist[slot];
     }
     float wlow = -1.0f;              // W' of the stored list at xf (prefill certificate below)
-    if (active && !greedy && kp.verlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip, wlow);
+    if (active && !greedy && kp.reuse) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip, wlow);
     if (active && !greedy && !skip) {
         // prefill from the previous iteration's list re-measured at the new pose: all positions,
         // then all points are loaded before any is consumed (two memory round trips, not 2·KL),
         // and the nearly sorted keys are ordered by an early-exit odd-even transposition sort
         // (the list is full and the bound tight before the traversal starts; a later leaf insert
-        // must then skip points already listed)
+        // must then skip points already listed).  Slot j keeps entry j's position; its key carries
+        // id j (the keys alone get sorted)
         int pj[KL];
 #pragma unroll
         for (int j = 0; j < KL; ++j) pj[j] = lists[(size_t)j * N + slot];
@@ -535,14 +526,8 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
             const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
             const bool keep = pj[j] >= 0 && d32 <= r2s;
-            if (LDSL) {
-                // slot j keeps entry j's position; its key carries id j (the keys alone get sorted)
-                lk[j] = keep ? IK::make(d32, j) : IK::empty(j);
-                mypos[j * kWaveBlock] = keep ? pj[j] : -1;
-            } else {
-                lk[j] = keep ? d32 : kInfF;
-                lp[j] = keep ? pj[j] : -1;
-            }
+            lk[j] = keep ? IK::make(d32, j) : IK::empty(j);
+            mypos[j * kWaveBlock] = keep ? pj[j] : -1;
         }
         bool swapped = true;
         while (swapped) {
@@ -555,22 +540,17 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                     const float tk = lk[j];
                     lk[j] = sw ? lk[j + 1] : lk[j];
                     lk[j + 1] = sw ? tk : lk[j + 1];
-                    if (!LDSL) {
-                        const int tp = lp[j];
-                        lp[j] = sw ? lp[j + 1] : lp[j];
-                        lp[j + 1] = sw ? tp : lp[j + 1];
-                    }
                     swapped |= sw;
                 }
             }
         }
-        bnd = fmin_nn(bcap, thr_());
+        bnd = fmin_nn(r2s, thr_());
         // prefill certificate: the stored list re-measured at xf holds its answer when the key that
         // answer relies on (max(K-th key within r, NN-1 key), need_key) is below W' — every point
         // outside the list is at least √W' away (verlet_skip) — so the traversal is skipped exactly
         // as for a Verlet reuse; the stale bound √nr + D there is the worst case of this re-measured
         // key.  (fp32 slack as in verlet_skip; k_finish re-certifies the list in fp64 against W'.)
-        if (kp.verlet2 && wlow > 0.f) {
+        if (kp.reuse && wlow > 0.f) {
             const float nk = need_();
             if (nk < kInfF && nk * (1.0f + 1e-5f) < wlow) { skip = true; wskip = wlow; }
         }
@@ -578,8 +558,6 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     // leaf scan shared by the seed pass and the traversal: the lanes in `want` test every point of
     // leaf `leaf` against their bound; `listed`: the leaf may hold points already in a lane's
     // list (prefilled or seeded), which must not be inserted twice
-    int sparse_thr = kp.sparse_lanes;
-    const bool bcast_lock = kp.bcast_lock == 2 || (kp.bcast_lock == 1 && !use_prev);
 #ifdef IMLS_DEBUG_WAVE_TRACE
     unsigned dbg_ev = 0, dbg_ins = 0;
     unsigned dbg_sparse = 0, dbg_bcast = 0, dbg_sparse_lanes = 0, dbg_sparse_ins = 0;
@@ -599,130 +577,34 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 inl |= rel < 64u ? (1ull << rel) : 0ull;
             }
         };
+        const bool sparse = __popcll(want) <= kSparseLanes;
 #ifdef IMLS_DEBUG_WAVE_TRACE
-        if (__popcll(want) <= sparse_thr) { ++dbg_sparse; dbg_sparse_lanes += __popcll(want); } else { ++dbg_bcast; }
+        if (sparse) { ++dbg_sparse; dbg_sparse_lanes += __popcll(want); } else { ++dbg_bcast; }
 #endif
-        const bool sparse = __popcll(want) <= sparse_thr;
-        // lockstep paths: only the NUMBER of listed points in the leaf per lane up front (3 ops per
-        // list slot instead of 7).  Every listed point of the leaf is a candidate of its lane (its
-        // key, recomputed here bit for bit, is ≤ the lane's bound: bnd = min(cap, KL-th key) and
-        // listed keys are ≤ both), so a lane with exactly that many candidates has no new one; the
-        // mask itself is built only when some lane has more (a leaf with new points).
-        const bool lock_path = LOCKSTEP && (sparse || bcast_lock);
-        int nin = 0;
-        bool have_inl = !listed;
-        if (listed) {
-            if (lock_path && kp.lazy_listed) {
-#pragma unroll
-                for (int k = 0; k < KL; ++k) nin += (unsigned)(pos_(k) - base) < (unsigned)cnt ? 1 : 0;
-            } else {
-                listed_mask();
-                have_inl = true;
-            }
-        }
-        // the lockstep paths' candidate bound: it must admit every listed point of the leaf (the
-        // count comparison above counts them as candidates) — bnd itself does for the register list
-        // (listed keys ≤ the KL-th key); slot-id keys truncate, and a listed point can lie up to
-        // hi(max key) (the lockstep loop re-tests d32 < thr_() before inserting)
-        const float cb = LDSL ? fmin_nn(bcap, IK::hi(lk[KL - 1])) : bnd;
-        if (lock_path) {
+        if (sparse) {
             // few lanes want this leaf (spread-out queries in a dense region): per wanting lane,
             // all leaf points are measured at once (one per lane) and the ones under that lane's
             // bound and not yet listed become its candidate mask; then the lanes insert their own
-            // candidates in lockstep, each its lowest pending point per step (index order) read
-            // back from LDS — max(per-lane candidates) insertion steps instead of one per
-            // candidate of every lane.  bcast_lock: many lanes want the leaf, each lane's mask is
-            // built by the broadcast scan, then the same lockstep insertion (loose early bounds:
-            // the candidates of different lanes fall at different points).  Per lane, the
-            // insertions are exactly the sequential scan's (same order, re-tested at the current
-            // bound; a non-candidate was above the leaf-start bound already).
+            // candidates in lockstep, each its lowest pending point per step (index order) fetched
+            // by ds_bpermute — max(per-lane candidates) insertion steps instead of one per
+            // candidate of every lane.  Per lane, the insertions are exactly the sequential scan's
+            // (same order, re-tested at the current bound; a non-candidate was above the
+            // leaf-start bound already).
+            // Listed points: only their NUMBER in the leaf per lane up front (3 ops per list slot
+            // instead of 7).  Every listed point of the leaf is a candidate of its lane (its key,
+            // recomputed here bit for bit, is ≤ the lane's candidate bound cb), so a lane with
+            // exactly that many candidates has no new one; the mask itself is built only when some
+            // lane has more (a leaf with new points).  cb must admit every listed point: slot-id
+            // keys truncate, so a listed point can lie up to hi(max key) (the insertion loop
+            // re-tests d32 < thr_())
+            int nin = 0;
+            bool have_inl = !listed;
+            if (listed) {
+#pragma unroll
+                for (int k = 0; k < KL; ++k) nin += (unsigned)(pos_(k) - base) < (unsigned)cnt ? 1 : 0;
+            }
+            const float cb = fmin_nn(r2s, IK::hi(lk[KL - 1]));
             unsigned long long cm = 0ull;
-            if (!sparse) {
-                const bool wants = (want >> lane) & 1ull;
-                for (int j = 0; j < cnt; ++j) {
-                    const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
-                    const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.y), j));
-                    const float pz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.z), j));
-                    const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
-                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                    cm |= (wants && d32 <= cb) ? (1ull << j) : 0ull;
-                }
-                if (!have_inl) {
-                    const bool more = __popcll(cm) > nin;
-                    if (__ballot(more)) listed_mask();
-                    cm = more ? cm : 0ull;
-                }
-                cm &= ~inl;
-            } else {
-                unsigned long long m = want;
-                while (m) {
-                    const int q = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
-                    m &= m - 1;
-                    const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[0]), q));
-                    const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[1]), q));
-                    const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[2]), q));
-                    const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cb), q));
-                    const float ex = mine.x - qx, ey = mine.y - qy, ez = mine.z - qz;
-                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                    unsigned long long pm = __ballot(lane < cnt && d32 <= qb);
-                    if (!have_inl) {
-                        const int nq = __builtin_amdgcn_readlane(nin, q);
-                        if (__popcll(pm) > nq) {
-                            listed_mask();
-                            have_inl = true;
-                        } else {
-                            pm = 0ull;
-                        }
-                    }
-                    if (pm) {
-                        const unsigned long long inq =
-                            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(inl >> 32), q) << 32) |
-                            (unsigned)__builtin_amdgcn_readlane((int)(unsigned)inl, q);
-                        pm &= ~inq;
-                    }
-                    if (lane == q) cm = pm;
-                }
-            }
-            if (__ballot(cm != 0ull)) {
-                if (!LDSL) {
-                    sleaf[wv][lane] = mine;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                }
-                while (__ballot(cm != 0ull)) {
-                    // every lane takes part in the permutes (lanes without a candidate read lane 0)
-                    const int jj = cm ? (int)__builtin_ctzll(cm) : 0;
-                    float4 pl;
-                    if (LDSL) {
-                        pl.x = __shfl(mine.x, jj);
-                        pl.y = __shfl(mine.y, jj);
-                        pl.z = __shfl(mine.z, jj);
-                    }
-                    if (cm) {
-                        const int j = jj;
-                        cm &= cm - 1;
-                        const float4 p = LDSL ? pl : sleaf[wv][j];
-                        const float ex = p.x - xf[0], ey = p.y - xf[1], ez = p.z - xf[2];
-                        const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                        if (d32 <= bnd && d32 < thr_()) {
-#ifdef IMLS_DEBUG_WAVE_TRACE
-                            ++dbg_ins;
-#endif
-                            ins_(d32, base + j);
-                            bnd = fmin_nn(bcap, thr_());
-                        }
-                    }
-#ifdef IMLS_DEBUG_WAVE_TRACE
-                    ++dbg_ev;
-#endif
-                }
-                if (!LDSL) __builtin_amdgcn_wave_barrier();   // sleaf is rewritten by the next leaf
-            }
-        } else if (__popcll(want) <= sparse_thr) {
-            // few lanes want this leaf (spread-out queries in a dense region): per wanting lane,
-            // all leaf points are measured at once (one per lane) and only the ones under that
-            // lane's bound and not yet listed are handed to it, in index order
             unsigned long long m = want;
             while (m) {
                 const int q = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
@@ -730,27 +612,51 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[0]), q));
                 const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[1]), q));
                 const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf[2]), q));
-                const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bnd), q));
-                const unsigned long long inq =
-                    ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(inl >> 32), q) << 32) |
-                    (unsigned)__builtin_amdgcn_readlane((int)(unsigned)inl, q);
+                const float qb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cb), q));
                 const float ex = mine.x - qx, ey = mine.y - qy, ez = mine.z - qz;
                 const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                unsigned long long pm = __ballot(lane < cnt && d32 <= qb) & ~inq;
-                while (pm) {
-                    const int j = __builtin_amdgcn_readfirstlane(__builtin_ctzll(pm));
-                    pm &= pm - 1;
-                    const float dj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d32), j));
-                    if (lane == q && dj <= bnd && dj < thr_()) {
-#ifdef IMLS_DEBUG_WAVE_TRACE
-                        ++dbg_sparse_ins;
-#endif
-                        ins_(dj, base + j);
-                        bnd = fmin_nn(bcap, thr_());
+                unsigned long long pm = __ballot(lane < cnt && d32 <= qb);
+                if (!have_inl) {
+                    const int nq = __builtin_amdgcn_readlane(nin, q);
+                    if (__popcll(pm) > nq) {
+                        listed_mask();
+                        have_inl = true;
+                    } else {
+                        pm = 0ull;
                     }
                 }
+                if (pm) {
+                    const unsigned long long inq =
+                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(inl >> 32), q) << 32) |
+                        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)inl, q);
+                    pm &= ~inq;
+                }
+                if (lane == q) cm = pm;
+            }
+            while (__ballot(cm != 0ull)) {
+                // every lane takes part in the permutes (lanes without a candidate read lane 0)
+                const int jj = cm ? (int)__builtin_ctzll(cm) : 0;
+                const float px = __shfl(mine.x, jj), py = __shfl(mine.y, jj), pz = __shfl(mine.z, jj);
+                if (cm) {
+                    cm &= cm - 1;
+                    const float ex = px - xf[0], ey = py - xf[1], ez = pz - xf[2];
+                    const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                    if (d32 <= bnd && d32 < thr_()) {
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                        ++dbg_ins;
+#endif
+                        ins_(d32, base + jj);
+                        bnd = fmin_nn(r2s, thr_());
+                    }
+                }
+#ifdef IMLS_DEBUG_WAVE_TRACE
+                ++dbg_ev;
+#endif
             }
         } else {
+            // broadcast: each point goes to every lane by v_readlane, every wanting lane tests it
+            // against its list
+            if (listed) listed_mask();
             const bool wants = (want >> lane) & 1ull;
             for (int j = 0; j < cnt; ++j) {
                 const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
@@ -766,38 +672,30 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
 #endif
                 if (ins) {
                     ins_(d32, base + j);
-                    bnd = fmin_nn(bcap, thr_());
+                    bnd = fmin_nn(r2s, thr_());
                 }
             }
         }
     };
     // seed (first ICP iteration, or a lane that moved far): the leaf holding the lane's own Morton
-    // key (binary search over the leaves' first keys) ± seed_half, scanned per lane — Morton-near
+    // key (binary search over the leaves' first keys) ± kSeedHalf, scanned per lane — Morton-near
     // points are mostly space-near, while a greedy box-distance descent goes astray in the heavily
     // overlapping upper-level boxes.  The traversal re-scans these leaves harmlessly (listed points
-    // are masked, the rest are not under the bound).  (A wave-wide seed pass over the packet's
-    // leaves measured no faster, and its second inlined copy of scan_leaf raised the kernel's
-    // register demand from ~160 to ~200 VGPRs.)
+    // are masked, the rest are not under the bound).
     const unsigned long long gmask = __ballot(greedy);
     // the seed search's leaf: its first ~10 bisection steps run in a coarse table of every S-th
     // leaf key staged in LDS (one coalesced block load), the last ⌈log2 S⌉ in HBM/L2 — instead of
-    // ~15 dependent global loads per lane (measured: the seed pass was ~half of iterations 0-2)
-    // (first ICP iteration only, where every lane seeds: later iterations reseed a few lanes, which
-    // would not repay the block barrier)
-    // (LDSL: the table lives in spos, whose slots are not in use yet — cleared after the search)
-    __shared__ unsigned long long skey_own[LDSL ? 1 : kSeedTab];
-    static_assert(!LDSL || KL * kWaveBlock * 4 >= kSeedTab * 8, "seed table fits the slot array");
-    unsigned long long* const skey = LDSL ? reinterpret_cast<unsigned long long*>(&spos[0][0]) : skey_own;
+    // ~15 dependent global loads per lane (first ICP iteration only, where every lane seeds: later
+    // iterations reseed a few lanes, which would not repay the block barrier).  The table lives in
+    // spos, whose slots are not in use yet (cleared after the search)
+    static_assert(KL * kWaveBlock * 4 >= kSeedTab * 8, "seed table fits the slot array");
+    unsigned long long* const skey = reinterpret_cast<unsigned long long*>(&spos[0][0]);
     const int S = use_prev ? t.L : (t.L + kSeedTab - 1) / kSeedTab;
     const int ntab = S > 0 ? (t.L + S - 1) / S : 0;
     if (!use_prev) {
         for (int k = threadIdx.x; k < ntab; k += kWaveBlock) skey[k] = t.lkeys[(size_t)k * S];
         __syncthreads();
     }
-    // seed_keys: the seed keeps keys only (med3 insertion, no positions): its KL-th key becomes the
-    // lane's bound cap and the list restarts empty — the traversal, which visits the seed leaves
-    // anyway, inserts the final members (nothing is listed twice, so no listed-mask is needed)
-    const bool seed_keys = kp.seed_keys != 0;
     int seed_leaf = 0;
     if (greedy) {
         const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
@@ -815,15 +713,15 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         }
         seed_leaf = l;
     }
-    if (LDSL && !use_prev) {
+    if (!use_prev) {
         __syncthreads();             // every wave is done with the seed table (it aliases spos)
 #pragma unroll
         for (int j = 0; j < KL; ++j) mypos[j * kWaveBlock] = -1;
     }
     if (greedy) {
         const int l = seed_leaf;
-        const int p0s = max(0, l - kp.seed_half) * B;
-        const int pend = min(M, (min(t.L - 1, l + kp.seed_half) + 1) * B);
+        const int p0s = max(0, l - kSeedHalf) * B;
+        const int pend = min(M, (min(t.L - 1, l + kSeedHalf) + 1) * B);
         float4 qs[kSeedChunk];
 #pragma unroll
         for (int k = 0; k < kSeedChunk; ++k) qs[k] = t.mpt[min(p0s + k, pend - 1)];
@@ -840,26 +738,12 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                 ++dbg_seed_pts;
 #endif
                 if (p0 + k < pend && d32 <= bnd && d32 < thr_()) {
-                    if (seed_keys && !LDSL) {
-                        insert_key<KL>(lk, d32);
-                    } else {
-                        ins_(d32, p0 + k);
-                    }
-                    bnd = fmin_nn(bcap, thr_());
+                    ins_(d32, p0 + k);
+                    bnd = fmin_nn(r2s, thr_());
                 }
             }
 #pragma unroll
             for (int k = 0; k < kSeedChunk; ++k) qs[k] = nx[k];
-        }
-        if (seed_keys) {
-            bcap = LDSL ? IK::hi(lk[KL - 1]) : bnd;   // a bound the KL seed points lie within
-            if (LDSL) bcap = fmin_nn(bcap, bnd);
-#pragma unroll
-            for (int j = 0; j < KL; ++j) lk[j] = LDSL ? IK::empty(j) : kInfF;
-            if (LDSL) {
-#pragma unroll
-                for (int j = 0; j < KL; ++j) mypos[j * kWaveBlock] = -1;
-            }
         }
     }
     unsigned n_inner = 0, n_leaf = 0;
@@ -878,7 +762,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             // ≤ 192 B), so a root-to-leaf walk costs ⌈levels/3⌉ dependent loads instead of levels
             ++n_inner;
             const int lev = 31 - __builtin_clz(node);
-            const int sw = min(kp.wide, t.levels - lev);
+            const int sw = min(kWide, t.levels - lev);
             const int nk = 1 << sw, nrec = nk >> 1;
             // the records are read-only for the whole kernel and the address is wave-uniform: read
             // them through the constant address space so they come by scalar loads into SGPRs (a
@@ -934,7 +818,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             const int leaf = node - P;
             float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
             if (lane < min(B, M - leaf * B)) mine = t.mpt[leaf * B + lane];
-            scan_leaf(leaf, em, use_prev || (gmask && !seed_keys), mine);
+            scan_leaf(leaf, em, use_prev || gmask, mine);
         }
         // pop: the stacked node's box is in LDS — re-check it against the shrunken lane bounds
         node = 0;
@@ -951,13 +835,13 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     if (active && skip) wlist[slot] = wskip;   // a reused list stays in place
     if (active && !skip) {
 #pragma unroll
-        for (int j = 0; j < KL; ++j) lists[(size_t)j * N + slot] = LDSL ? pos_(IK::id(lk[j])) : lp[j];   // ascending keys
+        for (int j = 0; j < KL; ++j) lists[(size_t)j * N + slot] = pos_(IK::id(lk[j]));   // ascending keys
         const bool full = full_();
         const float wk = full ? thr_() : kInfF;
         wlist[slot] = wk;
         // reference position + guarantee of a fresh list: every map point outside it has fp32
-        // key ≥ the KL-th key (full list; slot-id keys: its truncation thr_) or > the search bound
-        // (all points within r listed)
+        // key ≥ the KL-th key's truncation thr_ (full list) or > the search bound (all points
+        // within r listed)
         xref[slot] = make_float4(xf[0], xf[1], xf[2], full ? wk : r2s);
         nref[slot] = need_();
     }
@@ -1002,10 +886,6 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         atomicAdd(&nbr_stats[3], (unsigned long long)n_inner);
         atomicAdd(&nbr_stats[4], 1ull);
     }
-    // k_finish's deferred-query counter, zeroed at the END of the kernel: a global store ahead
-    // of the traversal may-clobbers every later load, and the node records are then fetched by
-    // vector loads instead of through the scalar cache
-    if (bx == 0 && threadIdx.x == 0) *fb_count = 0u;
 }
 
 // =============================================================================================
@@ -1016,21 +896,18 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
 // Output contract identical to k_knn_wave (positions [KL][N], worst key W per query).
 // =============================================================================================
 // FUSED (k_knn_qwave_f, a small frame alone): the wave goes on to the exact stage of its query
-// (finish_q_core) with the list still in its lanes; the deferred-query counter is then reset by the
-// fallback launch (project_lane_body's fb_reset), not here.  Extra arguments unused otherwise.
+// (finish_q_core) with the list still in its lanes, an uncertified list resolved in the same wave
+// (exact_wave_list) — nothing is deferred.  Extra arguments unused otherwise.
 template <int KL>
 __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
                                               int i, int slot, const double* __restrict__ pose, const KParams& kp,
                                               int pos, float W, float4* __restrict__ cs, float4* __restrict__ cd,
                                               float4* __restrict__ cn, imls_iter_trace* __restrict__ tr,
-                                              unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
-                                              unsigned* __restrict__ fb_count, int* stk_n = nullptr,
-                                              float* stk_d = nullptr);
+                                              unsigned long long* __restrict__ nbr_stats, int* stk_n, float* stk_d);
 struct QFinishArgs {
     const float4* snr;
     float4 *cs, *cd, *cn;
     imls_iter_trace* tr;
-    unsigned* fb_list;
 };
 template <int KL, bool FUSED = false>
 __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restrict__ spt,
@@ -1041,13 +918,12 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
                                                           int* __restrict__ lists, float* __restrict__ wlist,
                                                           float4* __restrict__ xref, float* __restrict__ nref,
                                                           int use_prev, unsigned long long* __restrict__ nbr_stats,
-                                                          unsigned* __restrict__ fb_count, int bx,
-                                                          const QFinishArgs& fa = QFinishArgs{}) {
+                                                          int bx, const QFinishArgs& fa = QFinishArgs{}) {
     static_assert(KL <= 64, "one list entry per lane");
     if (done && *done) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float sdist[kWaveBlock / 64][kWaveStack];
-    __shared__ int fnode[kWaveBlock / 64][kFStack];      // frontier traversal (kp.frontier)
+    __shared__ int fnode[kWaveBlock / 64][kFStack];      // frontier traversal
     __shared__ float fdist[kWaveBlock / 64][kFStack];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1098,10 +974,10 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
             }
         const float tn = (float)sqrt(delta[3] * delta[3] + delta[7] * delta[7] + delta[11] * delta[11]);
         const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
-        greedy = disp * disp > kp.reseed * wlist[slot];
+        greedy = disp * disp > kReseed * wlist[slot];
     }
     float wlow = -1.0f;
-    if (!greedy && kp.qverlet) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip, wlow);
+    if (!greedy && kp.reuse) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip, wlow);
     if (skip) {
         // the list stays in place
     } else if (!greedy) {
@@ -1127,8 +1003,8 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
             if (t.lkeys[mid] <= qk) lo = mid;
             else hi = mid - 1;
         }
-        seed_lo = max(0, lo - kp.seed_half);
-        seed_hi = min(t.L - 1, lo + kp.seed_half);
+        seed_lo = max(0, lo - kSeedHalf);
+        seed_hi = min(t.L - 1, lo + kSeedHalf);
         seed_leaf = lo;
         for (int leaf = seed_lo; leaf <= seed_hi; ++leaf) {
             const int base = leaf * B, cnt = min(B, M - base);
@@ -1166,7 +1042,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         const int p0 = __builtin_amdgcn_readfirstlane(lpos);
         const int sl = greedy ? seed_leaf : (p0 >= 0 ? p0 / B : -1);
         node = 1;
-        if (sl >= 0 && kp.bottom_up) {
+        if (sl >= 0) {
             const int ln = P + sl;
             float d = kInfF;
             int sn = 0;
@@ -1186,7 +1062,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
             node = ln;
         }
     }
-    if (kp.frontier && node) {
+    if (node) {
         // Frontier traversal (round 4): each step takes up to 8 stacked entries within the bound and
         // gives each an 8-lane group — an inner node's group tests the boxes of its descendants
         // `sw` levels down (one record per lane pair), a leaf's group measures its points (B / 8 per
@@ -1248,7 +1124,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
             int child = 0;
             if (ginner) {
                 const int lev = 31 - __builtin_clz(gnode);
-                const int sw = min(min(kp.wide, 3), t.levels - lev);     // ≤ 8 descendants: one per lane
+                const int sw = min(kWide, t.levels - lev);     // ≤ 8 descendants: one per lane
                 if (gl < (1 << sw)) {
                     const float4* rec = t.nodes + 3 * (((size_t)gnode << (sw - 1)) + (gl >> 1));
                     const float4 a = rec[0], b = rec[1], c = rec[2];
@@ -1296,73 +1172,6 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
             }
             fsp += __popcll(want);
         }
-        node = 0;
-    }
-    while (node) {
-        if (node < P) {
-            // one step descends `sw` binary levels: lane k tests the box of descendant k (the 2^sw
-            // boxes sit in 2^(sw−1) consecutive records of the intermediate level, one parallel load
-            // per lane pair), the nearest wanted descendant is entered and the others are stacked
-            // (lower index popped first) — ⌈levels/3⌉ dependent loads per root-to-leaf walk
-            ++n_inner;
-            const int lev = 31 - __builtin_clz(node);
-            const int sw = min(kp.wide, t.levels - lev);
-            const int nk = 1 << sw;
-            float d = kInfF;
-            if (lane < nk) {
-                const float4* rec = t.nodes + 3 * (((size_t)node << (sw - 1)) + (lane >> 1));
-                const float4 a = rec[0], b = rec[1], c = rec[2];
-                d = (lane & 1) ? box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w) : box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
-            }
-            const unsigned long long want = __ballot(lane < nk && d <= bnd * kBoxSlack);
-            if (want) {
-                float dm = ((want >> lane) & 1ull) ? d : kInfF;
-                int km = lane;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const float od = __shfl_xor(dm, o, 64);
-                    const int ok = __shfl_xor(km, o, 64);
-                    if (od < dm || (od == dm && ok < km)) { dm = od; km = ok; }
-                }
-                km = __builtin_amdgcn_readfirstlane(km);
-                unsigned long long rest = want & ~(1ull << km);
-                while (rest) {
-                    const int kk = 63 - __builtin_clzll(rest);
-                    rest &= ~(1ull << kk);
-                    const float dk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), kk));
-                    if (lane == 0) { snode[wv][sp] = (node << sw) + kk; sdist[wv][sp] = dk; }
-                    ++sp;
-                }
-                node = (node << sw) + km;
-                continue;
-            }
-        } else {
-            ++n_leaf;
-            const int leaf = node - P;
-            if (leaf < seed_lo || leaf > seed_hi) {
-                const int base = leaf * B, cnt = min(B, M - base);
-                float d = kInfF;
-                if (lane < cnt) {
-                    const float4 q = t.mpt[base + lane];
-                    const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
-                    d = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                }
-                unsigned long long m = __ballot(lane < cnt && d <= bnd && d < worst());
-                while (m) {
-                    const int j = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const float cd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), j));
-                    const int cp = base + j;
-                    if (cd <= bnd && cd < worst() && !__ballot(lane < KL && lpos == cp)) insert(cd, cp);
-                }
-            }
-        }
-        node = 0;
-        while (sp > 0) {
-            --sp;
-            if (sdist[wv][sp] <= bnd * kBoxSlack) { node = snode[wv][sp]; break; }
-        }
-        if (!node) break;
     }
     if (!hmode) break;
     if (!(nearest() <= h2s)) {
@@ -1402,8 +1211,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         // the list as k_finish_q reads it: in the lanes, or (Verlet skip) still in memory
         const int pos = lane < KL ? (skip ? lists[(size_t)lane * N + slot] : lpos) : -1;
         finish_q_core<KL>(t, spt, fa.snr, (int)qperm[slot], slot, pose, kp, pos, skip ? wskip : worst(), fa.cs, fa.cd,
-                          fa.cn, fa.tr, nbr_stats, fa.fb_list, fb_count, kp.qexact ? snode[wv] : nullptr,
-                          kp.qexact ? sdist[wv] : nullptr);
+                          fa.cn, fa.tr, nbr_stats, snode[wv], sdist[wv]);
 #ifdef IMLS_DEBUG_WAVE_TRACE
         // per-wave record of the last fused launch: start / traversal end / finish end (100 MHz
         // clock, low 32 bits), Verlet skip, leaves, inner steps, hardware id
@@ -1414,11 +1222,6 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
             r[7] = (unsigned)__builtin_amdgcn_s_getreg((23 << 0) | (0 << 6) | (31 << 11));   // HW_ID / HW_ID1
         }
 #endif
-    } else {
-        // k_finish's deferred-query counter, zeroed at the END of the kernel: a global store ahead
-        // of the traversal may-clobbers every later load, and the node records are then fetched by
-        // vector loads instead of through the scalar cache
-        if (bx == 0 && threadIdx.x == 0) *fb_count = 0u;
     }
 }
 
@@ -1513,11 +1316,9 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
             else need = fmax(need, d1);
             cert = cert && (need < (double)W / kCertSlack);
         }
-        if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_FORCE_FALLBACK)
+        if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_OPT_FORCE_FALLBACK)
         if (!cert) {
-            const unsigned pos = atomicAdd(fb_count, 1u);
-            fb_list[pos] = (unsigned)i;
-            cat = -3;                                         // deferred to k_project_lane
+            cat = -3;                                         // deferred to k_project_lane (listed below)
             // the list's own bound for the exact re-run: its points are real, so the exact answer
             // needs no point beyond max(K-th listed key within r, listed NN-1) (r² when either is
             // missing) — the fallback's search ball, instead of the whole radius r
@@ -1535,10 +1336,31 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
         if (i1 >= 0) atomicAdd(&rej_s[IMLS_NUM_REJ + 1], 1u);
     }
     if (cat == -3) atomicAdd(&rej_s[IMLS_NUM_REJ + 2], 1u);
-    double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
-    if (cat == -1) { plane_row(xf, yf, nf, a, bb); one = 1.0; }
-    block_normeq<kWaveBlock>(a, bb, one, red, out);
-    if (tid < kNormEq) partial1[(size_t)bx * kNormEq + tid] = out[tid];
+    // the deferred queries of this block, listed in slot order in its own region
+    // fb_list[bx·256, …) with their count in fb_count[bx] — no atomics: k_project_lane walks the
+    // regions in block order, so the fallback's rows (and its slab sums) do not depend on timing
+    {
+        __shared__ unsigned wcnt[kWaveBlock / 64];
+        const unsigned long long dm = __ballot(cat == -3);
+        if ((tid & 63) == 0) wcnt[tid >> 6] = (unsigned)__popcll(dm);
+        __syncthreads();
+        unsigned before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kWaveBlock / 64; ++w) {
+            before += w < (tid >> 6) ? wcnt[w] : 0u;
+            total += wcnt[w];
+        }
+        if (cat == -3) fb_list[(size_t)bx * kWaveBlock + before + __popcll(dm & ((1ull << (tid & 63)) - 1ull))] = (unsigned)i;
+        if (tid == 0) fb_count[bx] = total;
+    }
+    // pass-1 slabs only for the grid solve chain (frames of ≤ kSmallRows rows: k_solve_small forms
+    // pass 1 from the rows); N is block-uniform
+    if (N > kSmallRows) {
+        double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
+        if (cat == -1) { plane_row(xf, yf, nf, a, bb); one = 1.0; }
+        block_normeq<kWaveBlock>(a, bb, one, red, out);
+        if (tid < kNormEq) partial1[(size_t)bx * kNormEq + tid] = out[tid];
+    }
     if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
@@ -1547,15 +1369,15 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
 
 // =============================================================================================
 // Exact stage, one WAVE per query (a small frame registered alone — the config C/D deployment
-// shape, ≤ kQwaveAutoN queries — where k_finish's one-lane-per-query latency chain (~30 µs per
+// shape, ≤ kSmallRows queries — where k_finish's one-lane-per-query latency chain (~30 µs per
 // launch for 2000 queries in 8 blocks) sets the frame latency): lane j holds list entry j, so the
 // gathers, the exact distances, the gates and the IMLS weights run across the lanes.  Every value is
 // computed by the same expression as k_finish's lane code, the list order is the same (d², index)
 // total order (each lane's rank by counting), the IMLS sums accumulate in that order (lane 0 reads
 // each term in turn) — the correspondences are the lane kernel's bit for bit.  Rejects are counted
-// by integer atomics (order-free).  The pass-1 slabs (per 256-slot block, exactly k_finish's: same
-// slot → thread map, same block_normeq) are summed by the slab role of the fallback launch that
-// follows anyway (k_fallback_slab), from the rows whose cd.w is −1.
+// by integer atomics (order-free).  No pass-1 slabs: frames of ≤ kSmallRows rows are solved by
+// k_solve_small, which forms pass 1 from the rows (the same order for every small frame, batched
+// or alone, whichever exact stage produced its rows).
 // =============================================================================================
 __device__ __forceinline__ double rl_f64(double x, int l) {
     const long long b = __double_as_longlong(x);
@@ -1598,7 +1420,7 @@ __device__ int exact_wave_list(const TreeView& t, const KParams& kp, const doubl
     while (true) {
         if (node < P) {
             const int lev = 31 - __builtin_clz(node);
-            const int sw = min(min(kp.wide, 3), t.levels - lev);
+            const int sw = min(kWide, t.levels - lev);
             const int nk = 1 << sw;
             float d = kInfF;
             if (lane < nk) {
@@ -1671,17 +1493,15 @@ __device__ int exact_wave_list(const TreeView& t, const KParams& kp, const doubl
 }
 
 // query i (slot `slot`) from its list: lane k < KL holds entry k's map position `pos` (−1 empty),
-// W is the list's bound (the traversal's worst key).  Run by k_finish_q, and by k_knn_qwave_f
-// straight after the traversal of the same wave (round 4: one launch per iteration fewer).  With an
-// LDS stack (stk_n, the fused kernel) an uncertified query gets its exact list in place
-// (exact_wave_list) instead of being deferred to the fallback launch.
+// W is the list's bound (the traversal's worst key).  Run by k_knn_qwave_f straight after the
+// traversal of the same wave (round 4: one launch per iteration fewer); an uncertified query gets its
+// exact list in place (exact_wave_list, with the wave's LDS stack stk_n / stk_d) — nothing is deferred.
 template <int KL>
 __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
                                               int i, int slot, const double* __restrict__ pose, const KParams& kp,
                                               int pos, float W, float4* __restrict__ cs, float4* __restrict__ cd,
                                               float4* __restrict__ cn, imls_iter_trace* __restrict__ tr,
-                                              unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
-                                              unsigned* __restrict__ fb_count, int* stk_n, float* stk_d) {
+                                              unsigned long long* __restrict__ nbr_stats, int* stk_n, float* stk_d) {
     static_assert(KL <= 64, "one list entry per lane");
     const int lane = threadIdx.x & 63;
     float xf[3];
@@ -1738,27 +1558,17 @@ __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restri
         else need = fmax(need, d1);
         cert = cert && (need < (double)W / kCertSlack);
     }
-    if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_FORCE_FALLBACK)
+    if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_OPT_FORCE_FALLBACK)
     int cat = -1, kq = 0;
     float yf[3] = {0.f, 0.f, 0.f}, nf[3] = {0.f, 0.f, 0.f};
     if (!cert) {
-        // the fallback's search ball: the list's bound (k_project_lane reads it from cs.w)
+        // the exact search ball: the list's bound (its points are real, the exact answer needs
+        // nothing farther — the bound k_project_lane gets from k_finish through cs.w)
         const double lb = l1 < 0 ? r2 : fmax(cnt_r >= K ? dK : r2, d1);
         const float capf = (float)(fmin(lb, r2) * (1.0 + 1e-6));
-        if (stk_n) {
-            pos = exact_wave_list<KL>(t, kp, xd, xf, fmin(r2, (double)capf), stk_n, stk_d);
-            analyse();
-            if (nbr_stats && lane == 0) atomicAdd(&nbr_stats[5], 1ull);
-        } else {
-            if (lane == 0) {
-                const unsigned at = atomicAdd(fb_count, 1u);
-                fb_list[at] = (unsigned)i;
-                cs[i] = make_float4(0.f, 0.f, 0.f, capf);
-                cd[i] = make_float4(0.f, 0.f, 0.f, -3.f);
-                if (nbr_stats) atomicAdd(&nbr_stats[5], 1ull);
-            }
-            return;
-        }
+        pos = exact_wave_list<KL>(t, kp, xd, xf, fmin(r2, (double)capf), stk_n, stk_d);
+        analyse();
+        if (nbr_stats && lane == 0) atomicAdd(&nbr_stats[5], 1ull);
     }
     if (kp.matcher) {
         cat = finish_plane(xf, ns, p1, t, kp, yf, nf);
@@ -1829,9 +1639,6 @@ __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restri
     }
     if (lane == 0) {
         store_result(i, cat, xf, yf, nf, cs, cd, cn);
-        // the slab role of the fallback launch sums the rows with cd.w = −1 (valid here); a
-        // rejected or deferred query carries its category / −3 (the fallback's own rows: w = 0)
-        cd[i] = cat == -1 ? make_float4(yf[0], yf[1], yf[2], -1.f) : make_float4(0.f, 0.f, 0.f, (float)cat);
         if (cat >= 0) atomicAdd((unsigned long long*)&tr->reject[cat], 1ull);   // integer: order-free
         if (nbr_stats) {
             if (kq) atomicAdd(&nbr_stats[0], (unsigned long long)kq);
@@ -1840,74 +1647,8 @@ __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restri
     }
 }
 
-template <int KL>
-__device__ __forceinline__ void finish_q_body(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
-                                              const unsigned* __restrict__ qperm, int N, const double* __restrict__ pose,
-                                              const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
-                                              const float* __restrict__ wlist, float4* __restrict__ cs,
-                                              float4* __restrict__ cd, float4* __restrict__ cn,
-                                              imls_iter_trace* __restrict__ tr,
-                                              unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
-                                              unsigned* __restrict__ fb_count, int bx) {
-    if (done && *done) return;
-    const int lane = threadIdx.x & 63;
-    const int slot = __builtin_amdgcn_readfirstlane(bx * (kWaveBlock / 64) + (int)(threadIdx.x >> 6));
-    if (slot >= N) return;
-    const int pos = lane < KL ? lists[(size_t)lane * N + slot] : -1;
-    finish_q_core<KL>(t, spt, snr, (int)qperm[slot], slot, pose, kp, pos, wlist[slot], cs, cd, cn, tr, nbr_stats, fb_list,
-                      fb_count);
-}
-
-// pass-1 normal equations of the wave-per-query results, per 256-slot block exactly as k_finish's
-// block_normeq<kWaveBlock> sums them (rows = the queries whose cd.w is −1; rejects were counted by
-// the exact stage), by a block of kProjBlock threads: wave w reduces the 64-slot groups w, w + 2, …
-// with the same wave_total, and the four group totals are added in group order — the same
-// association, so the slabs are k_finish's bit for bit
-__device__ __forceinline__ void finish_slab_body(const unsigned* __restrict__ qperm, int N, const float4* __restrict__ cs,
-                                                 const float4* __restrict__ cd, const float4* __restrict__ cn,
-                                                 double* __restrict__ partial1, int bx) {
-    __shared__ double red[kWaveBlock / 64][kNormEq];
-    const int lane = threadIdx.x & 63;
-    for (int g = (int)(threadIdx.x >> 6); g < kWaveBlock / 64; g += (int)(blockDim.x >> 6)) {
-        const int slot = bx * kWaveBlock + g * 64 + lane;
-        double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
-        if (slot < N) {
-            const int i = (int)qperm[slot];
-            const float4 d4 = cd[i];
-            if (d4.w == -1.f) {
-                const float4 s4 = cs[i], n4 = cn[i];
-                const float xf[3] = {s4.x, s4.y, s4.z}, yf[3] = {d4.x, d4.y, d4.z}, nf[3] = {n4.x, n4.y, n4.z};
-                plane_row(xf, yf, nf, a, bb);
-                one = 1.0;
-            }
-        }
-        int k = 0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int c = r; c < 6; ++c) {
-                const double v = wave_total(a[r] * a[c]);
-                if (lane == 63) red[g][k] = v;
-                ++k;
-            }
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-            const double v = wave_total(a[r] * bb);
-            if (lane == 63) red[g][21 + r] = v;
-        }
-        const double v = wave_total(one);
-        if (lane == 63) red[g][27] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < kNormEq) {
-        double sum = 0.0;
-        for (int w = 0; w < kWaveBlock / 64; ++w) sum += red[w][threadIdx.x];
-        partial1[(size_t)bx * kNormEq + threadIdx.x] = sum;
-    }
-}
-
 // =============================================================================================
-// Per-lane exact traversal (fallback for uncertified queries; IMLS_TRAVERSAL=lane mode)
+// Per-lane exact traversal (fallback for uncertified queries; IMLS_TRAVERSAL_LANE mode)
 // =============================================================================================
 template <int KCAP>
 __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __restrict__ spt,
@@ -1919,10 +1660,8 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
                                                              float4* __restrict__ cs, float4* __restrict__ cd,
                                                              float4* __restrict__ cn, double* __restrict__ partial1,
                                                              imls_iter_trace* __restrict__ tr,
-                                                             unsigned long long* __restrict__ nbr_stats, int nlog,
-                                                             unsigned* __restrict__ fb_reset = nullptr,
-                                                             int arrivals = 0) {
-    // (done: the launch that fed qlist left at once too, so the counter is still zero)
+                                                             unsigned long long* __restrict__ nbr_stats, int nlog) {
+    // (done: the k_finish launch that listed the deferred queries left at once too)
     if (done && *done) return;
     __shared__ uint2 stack[kStackDepth][kProjBlock];
     __shared__ double red[kProjBlock / 64][kNormEq];
@@ -1931,15 +1670,33 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
     const int tid = threadIdx.x;
     if (tid < IMLS_NUM_REJ + 3) rej_s[tid] = 0;
     __syncthreads();
-    const int total = qlist ? (int)*qcount : N;
-    // nlog logical blocks (one pass-1 slab each, the rows base = lb·128 + k·nlog·128) taken by the
-    // physical blocks in turn: the slabs do not depend on the physical grid
+    // nlog logical blocks (one pass-1 slab each) taken by the physical blocks in turn: the slabs do
+    // not depend on the physical grid.  A logical block lb works in rounds of kProjBlock queries:
+    // every query (lane mode, qlist null) — rows lb·128 + k·nlog·128; deferred queries — the regions
+    // k_finish blocks lb, lb + nlog, … listed (qlist[b·256 …], qcount[b] entries each), in block order
+    const int nfb = (N + kWaveBlock - 1) / kWaveBlock;
     for (int lb = blockIdx.x; lb < nlog; lb += gridDim.x) {
     double acc_out = 0.0;   // thread tid < 28 accumulates its normal-equation term over rounds
-    for (int base = lb * kProjBlock; base < total; base += nlog * kProjBlock) {
-        const int q = base + tid;
+    int fbk = lb, off = 0, base = lb * kProjBlock;
+    for (;;) {
+        int q, total;
+        size_t at;
+        if (qlist) {
+            while (fbk < nfb && off >= (int)qcount[fbk]) { fbk += nlog; off = 0; }
+            if (fbk >= nfb) break;
+            q = off + tid;
+            total = (int)qcount[fbk];
+            at = (size_t)fbk * kWaveBlock + q;
+            off += kProjBlock;
+        } else {
+            if (base >= N) break;
+            q = base + tid;
+            total = N;
+            at = (size_t)q;
+            base += nlog * kProjBlock;
+        }
         const bool active = q < total;
-        const int i = active ? (qlist ? (int)qlist[q] : q) : 0;
+        const int i = active ? (qlist ? (int)qlist[at] : q) : 0;
         int cat = -2, kq = 0, nn_found = 0;
         float xf[3] = {0, 0, 0}, yf[3] = {0, 0, 0}, nf[3] = {0, 0, 0};
         if (active) {
@@ -2064,43 +1821,33 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
             if (kq) atomicAdd(&rej_s[IMLS_NUM_REJ], (unsigned)kq);
             if (nn_found) atomicAdd(&rej_s[IMLS_NUM_REJ + 1], 1u);
         }
-        double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
-        if (cat == -1) { plane_row(xf, yf, nf, a, bb); one = 1.0; }
-        block_normeq<kProjBlock>(a, bb, one, red, out);
-        if (tid < kNormEq) acc_out += out[tid];
+        if (N > kSmallRows) {           // slabs for the grid solve chain only (see finish_body)
+            double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
+            if (cat == -1) { plane_row(xf, yf, nf, a, bb); one = 1.0; }
+            block_normeq<kProjBlock>(a, bb, one, red, out);
+            if (tid < kNormEq) acc_out += out[tid];
+        }
     }
-    if (tid < kNormEq) partial1[(size_t)lb * kNormEq + tid] = acc_out;
+    if (N > kSmallRows && tid < kNormEq) partial1[(size_t)lb * kNormEq + tid] = acc_out;
     }
     __syncthreads();
     if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
-    if (fb_reset) {
-        // the last block to get here (every block has read *qcount and its qlist entries) zeroes the
-        // deferred-query counter [0] for the next fused launch, and the arrival counter [1]
-        __syncthreads();
-        if (tid == 0) {
-            __threadfence();
-            if (atomicAdd(&fb_reset[1], 1u) == (unsigned)arrivals - 1u) {
-                atomicExch(&fb_reset[0], 0u);
-                atomicExch(&fb_reset[1], 0u);
-            }
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------------------------
 // Kernels: one frame (arguments by value) and batched (frame = tab[blockIdx.y]; blocks past the
 // frame's own grid leave at once).  Both run the same bodies.
 // ---------------------------------------------------------------------------------------------
-template <int KL, bool LOCKSTEP, bool LDSL>
+template <int KL>
 __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(
         TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
         const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
         int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
-        int use_prev, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_count) {
-    knn_wave_body<KL, LOCKSTEP, LDSL>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev,
-                                      nbr_stats, fb_count, (int)blockIdx.x);
+        int use_prev, unsigned long long* __restrict__ nbr_stats) {
+    knn_wave_body<KL>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats,
+                      (int)blockIdx.x);
 }
 
 template <int KL>
@@ -2108,8 +1855,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(
         TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
         const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
         int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
-        int use_prev, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_count) {
-    knn_qwave_body<KL>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats, fb_count,
+        int use_prev, unsigned long long* __restrict__ nbr_stats) {
+    knn_qwave_body<KL>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats,
                        (int)blockIdx.x);
 }
 
@@ -2118,9 +1865,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave_f(
         TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
         const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
         int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
-        int use_prev, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_count, QFinishArgs fa) {
+        int use_prev, unsigned long long* __restrict__ nbr_stats, QFinishArgs fa) {
     knn_qwave_body<KL, true>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats,
-                             fb_count, (int)blockIdx.x, fa);
+                             (int)blockIdx.x, fa);
 }
 
 template <int KL>
@@ -2134,46 +1881,14 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(
                     fb_count, (int)blockIdx.x);
 }
 
-template <int KL>
-__global__ __launch_bounds__(kWaveBlock) void k_finish_q(
-        TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qperm,
-        int N, const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
-        const float* __restrict__ wlist, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
-        imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
-        unsigned* __restrict__ fb_count) {
-    finish_q_body<KL>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, tr, nbr_stats, fb_list, fb_count,
-                      (int)blockIdx.x);
-}
-
 template <int KCAP>
 __global__ __launch_bounds__(kProjBlock) void k_project_lane(
         TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qlist,
         const unsigned* __restrict__ qcount, int N, const double* __restrict__ pose, const int* __restrict__ done,
         KParams kp, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
-        double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats,
-        unsigned* __restrict__ fb_reset) {
-    project_lane_body<KCAP>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats,
-                            kFallbackBlocks, fb_reset, (int)gridDim.x);
-}
-
-// After the wave-per-query exact stage (k_finish_q / k_knn_qwave_f): blocks [0, kFallbackBlocks)
-// run the exact fallback of the deferred queries (their slabs, and the deferred counter's reset),
-// the blocks after them sum the wave slabs — one launch instead of two (round 4)
-template <int KCAP>
-__global__ __launch_bounds__(kProjBlock) void k_fallback_slab(
-        TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qlist,
-        unsigned* __restrict__ qcount, const unsigned* __restrict__ qperm, int N, const double* __restrict__ pose,
-        const int* __restrict__ done, KParams kp, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
         double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats) {
-    static_assert(kWaveBlock % kProjBlock == 0 && kProjBlock % 64 == 0, "slab groups per wave");
-    if ((int)blockIdx.x >= kFallbackBlocks) {
-        if (done && *done) return;
-        finish_slab_body(qperm, N, cs, cd, cn, partial1, (int)blockIdx.x - kFallbackBlocks);
-        return;
-    }
-    const int wb = (N + kWaveBlock - 1) / kWaveBlock;
-    project_lane_body<KCAP>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1 + (size_t)wb * kNormEq, tr,
-                            nbr_stats, kFallbackBlocks, qcount, kFallbackBlocks);
+    project_lane_body<KCAP>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1, tr, nbr_stats,
+                            kFallbackBlocks);
 }
 
 __device__ __forceinline__ int wave_blocks_of(int N) { return (N + kWaveBlock - 1) / kWaveBlock; }
@@ -2186,9 +1901,10 @@ __host__ __device__ __forceinline__ int knn_blocks_of(int N, int qp) {
 __host__ __device__ __forceinline__ bool use_qwave(const KParams& kp, int N) {
     return kp.qwave > 0 || (kp.qwave < 0 && N <= kQwaveAutoN);
 }
-// one-frame launches: the exact stage one wave per query (k_knn_qwave_f / k_finish_q), the slabs
-// and the fallback then in one k_fallback_slab launch
-__host__ __forceinline__ bool q_exact_stage(const KParams& kp, int N) { return use_qwave(kp, N) && kp.qfinish; }
+// one-frame launches of a small frame (≤ kSmallRows queries, solved by k_solve_small from its rows):
+// the exact stage fused into the wave-per-query traversal (k_knn_qwave_f), nothing deferred — one
+// projection launch per ICP iteration
+__host__ __forceinline__ bool fused_stage(const KParams& kp, int N) { return use_qwave(kp, N) && N <= kSmallRows; }
 // the list block of a frame (see launch_wave): positions [KL][N], worst keys [N], xref, nref
 template <int KL>
 __device__ __forceinline__ float* wlist_of(int* lists, int N) { return reinterpret_cast<float*>(lists + (size_t)KL * N); }
@@ -2213,7 +1929,7 @@ __device__ __forceinline__ void batch_block(int xcd, int& frame, int& bx) {
     bx = (int)(s % nx);
 }
 
-template <int KL, bool LOCKSTEP, bool LDSL>
+template <int KL>
 __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const PairDev* __restrict__ tab, KParams kp,
                                                                           int use_prev, int npairs) {
     int f, bx;
@@ -2222,9 +1938,9 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const P
     const PairDev A = tab[f];
     if (use_qwave(kp, A.N) || bx >= knn_blocks_of(A.N, kp.packet)) return;
     float4* xref = xref_dev(A.lists, A.N);
-    knn_wave_body<KL, LOCKSTEP, LDSL>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
+    knn_wave_body<KL>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
                                 wlist_of<KL>(A.lists, A.N), xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats,
-                                A.fb_count, bx);
+                                bx);
 }
 
 template <int KL>
@@ -2237,7 +1953,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave_b(const PairDev* __res
     if (!use_qwave(kp, A.N) || bx * (kWaveBlock / 64) >= A.N) return;
     float4* xref = xref_dev(A.lists, A.N);
     knn_qwave_body<KL>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists, wlist_of<KL>(A.lists, A.N),
-                       xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats, A.fb_count, bx);
+                       xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats, bx);
 }
 
 template <int KL>
@@ -2271,9 +1987,7 @@ void launch_wave_batch(hipStream_t s, const PairDev* tab, int npairs, int maxN, 
     }
     if (any_large) {
         const int kb = knn_blocks_of(maxN, kp.packet);
-        if (kp.lds_list) k_knn_wave_b<KL, true, true><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
-        else if (kp.lockstep) k_knn_wave_b<KL, true, false><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
-        else k_knn_wave_b<KL, false, false><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        k_knn_wave_b<KL><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
     }
     k_finish_b<KL><<<dim3(wb, gy), kWaveBlock, 0, s>>>(tab, kp, it, npairs);
 }
@@ -2282,9 +1996,8 @@ template <int KCAP>
 void launch_lane(hipStream_t s, int blocks, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qlist,
                  const unsigned* qcount, int N, const double* pose, const int* done, const KParams& kp, float4* cs,
                  float4* cd, float4* cn, double* partial1, imls_iter_trace* tr, unsigned long long* stats) {
-    // a deferred list (qlist): this launch also resets its counter for the next projection
     k_project_lane<KCAP><<<blocks, kProjBlock, 0, s>>>(t, spt, snr, qlist, qcount, N, pose, done, kp, cs, cd, cn, partial1,
-                                                       tr, stats, qlist ? const_cast<unsigned*>(qcount) : nullptr);
+                                                       tr, stats);
 }
 
 
@@ -2297,37 +2010,24 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
     float4* xref = xref_of(lists, N);
     float* nref = reinterpret_cast<float*>(xref + N);
     if (marks) (void)hipEventRecord(marks[0], s);
-    // sparse query sets (≤ kQwaveAutoN queries, e.g. FPS-sampled frames): one wave per query;
-    // dense scans: packets of 64 Morton-coherent queries
-    const bool small_q = q_exact_stage(kp, N);
-    if (small_q && kp.qfuse)
+    // sparse query sets (≤ kQwaveAutoN queries, e.g. FPS-sampled frames): one wave per query, with the
+    // exact stage in the same kernel for ≤ kSmallRows; dense scans: packets of 64 Morton-coherent
+    // queries, then k_finish
+    const bool fused = fused_stage(kp, N);
+    if (fused)
         k_knn_qwave_f<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(
-            t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, stats, fb_count,
-            QFinishArgs{snr, cs, cd, cn, tr, fb_list});
+            t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, stats,
+            QFinishArgs{snr, cs, cd, cn, tr});
     else if (use_qwave(kp, N))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
-                                                                                          delta, lists, wlist, xref, nref, use_prev, stats,
-                                                                                          fb_count);
-    else if (kp.lds_list)
-        k_knn_wave<KL, true, true><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
-                                                          nref, use_prev, stats, fb_count);
-    else if (kp.lockstep)
-        k_knn_wave<KL, true, false><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
-                                                          nref, use_prev, stats, fb_count);
+                                                                                          delta, lists, wlist, xref, nref, use_prev, stats);
     else
-        k_knn_wave<KL, false, false><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref,
-                                                           nref, use_prev, stats, fb_count);
+        k_knn_wave<KL><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist,
+                                                                          xref, nref, use_prev, stats);
     if (marks) (void)hipEventRecord(marks[1], s);
-    if (small_q && kp.qfuse) {
-        // the exact stage ran in the traversal kernel; slabs: k_fallback_slab
-    } else if (small_q) {
-        // a small frame alone: the exact stage one wave per query; slabs: k_fallback_slab
-        k_finish_q<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(
-            t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, tr, stats, fb_list, fb_count);
-    } else {
+    if (!fused)
         k_finish<KL><<<blocks, kWaveBlock, 0, s>>>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1,
                                                    tr, stats, fb_list, fb_count);
-    }
     if (marks) (void)hipEventRecord(marks[2], s);
 }
 
@@ -2356,8 +2056,6 @@ void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     const int K = kp.K;
     if (K <= 8) launch_wave_batch<12>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else if (K <= 16) launch_wave_batch<20>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
-    else if (K <= 20 && kp.kl20 == 24) launch_wave_batch<24>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
-    else if (K <= 20 && kp.kl20 == 26) launch_wave_batch<26>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else if (K <= 20) launch_wave_batch<22>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else launch_wave_batch<36>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     // exact fallback for uncertified queries: every frame's kFallbackBlocks slabs are written, by
@@ -2391,30 +2089,15 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
         else launch_lane<32>(s, kFallbackBlocks, t, spt, snr, nullptr, nullptr, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
         return;
     }
-    // (fb_count is re-zeroed by the traversal kernel's first thread)
     if (K <= 8) launch_wave<12>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     // K ≤ 20 (the shipped 20): two slack entries certify every query on config B (KL 21 left a few
     // uncertified → the slow exact fallback, −30 %; KL 22 vs 24 measured +6.7 % pairs/s, 4 in flight)
-    else if (K <= 20 && kp.kl20 == 24) launch_wave<24>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
-    else if (K <= 20 && kp.kl20 == 26) launch_wave<26>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else if (K <= 20) launch_wave<22>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
-    // exact fallback for uncertified queries (usually none; the launch exits at once then) — after
-    // the wave-per-query exact stage with the wave slabs' sums in the same launch
-    if (q_exact_stage(kp, N) && kp.qfuse && kp.qexact && N <= kSmallRows) {
-        // nothing deferred (uncertified queries got their exact list in the fused kernel) and no
-        // slabs needed (k_solve_small forms pass 1 from the rows): no launch
-        return;
-    }
-    if (q_exact_stage(kp, N)) {
-        const int g = kFallbackBlocks + wblocks;
-        if (K <= 8) k_fallback_slab<8><<<g, kProjBlock, 0, s>>>(t, spt, snr, fb_list, fb_count, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats);
-        else if (K <= 16) k_fallback_slab<16><<<g, kProjBlock, 0, s>>>(t, spt, snr, fb_list, fb_count, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats);
-        else if (K <= 20) k_fallback_slab<20><<<g, kProjBlock, 0, s>>>(t, spt, snr, fb_list, fb_count, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats);
-        else k_fallback_slab<32><<<g, kProjBlock, 0, s>>>(t, spt, snr, fb_list, fb_count, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats);
-        return;
-    }
+    // exact fallback for uncertified queries (usually none; the launch exits at once then); the
+    // fused small-frame kernel resolves them in place
+    if (fused_stage(kp, N)) return;
     if (K <= 8) launch_lane<8>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
     else if (K <= 16) launch_lane<16>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);
     else if (K <= 20) launch_lane<20>(s, kFallbackBlocks, t, spt, snr, fb_list, fb_count, N, pose, done, kp, cs, cd, cn, p_fb, tr, stats);

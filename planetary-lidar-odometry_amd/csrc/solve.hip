@@ -464,9 +464,12 @@ __device__ __forceinline__ void solve_final_body(const Rows& rows, int N, const 
 
 // Small systems (≤ kSmallRows rows, e.g. the ≤2000-query frames of the config-C stream): the whole
 // LS solve in ONE block — pass-1 normal equations from the rows, first solve, |r| keys of the valid rows into
-// LDS, bitonic sort by (|r| bits, row), ranks [lo, hi] re-reduced, second solve, pose update —
-// instead of five launches whose fixed latency dominates at this size.  Same arithmetic and the
-// same exact (|r|, row) order as the chain.
+// LDS, boundary bins ordered by (|r| bits, row), ranks [lo, hi] re-reduced, second solve, pose update —
+// instead of five launches whose fixed latency dominates at this size.  The same row arithmetic and
+// the same exact (|r|, row) trim as the chain; the SUMS are associated differently: each thread adds
+// its rows t + k·512 in k order, then block_sum28 — not the chain's 256-row slabs — so every frame of
+// ≤ kSmallRows rows (batched or alone, whichever projection kernels produced its rows) takes this
+// kernel and the projection writes no slabs for it (project.hip).
 constexpr int kSmallBlock = 512;     // 8 waves: ≤ kSmallPer rows per thread, kept in registers between passes
 constexpr int kSmallPer = kSmallRows / kSmallBlock;
 static_assert(kSmallRows % kSmallBlock == 0, "rows per thread");

@@ -323,6 +323,21 @@ class ImlsContext:
         """Count-less device loads read their buffer at first use (imls_set_defer)."""
         self._check(self.lib.imls_set_defer(self.ctx, int(bool(on))))
 
+    def set_option(self, name, value):
+        """A runtime option (imls_set_option): name from _abi.OPTION_IDS or an IMLS_OPT_* id."""
+        opt = _abi.OPTION_IDS[name] if isinstance(name, str) else int(name)
+        self._check(self.lib.imls_set_option(self.ctx, opt, float(value)))
+
+    def get_option(self, name) -> float:
+        opt = _abi.OPTION_IDS[name] if isinstance(name, str) else int(name)
+        v = C.c_double()
+        self._check(self.lib.imls_get_option(self.ctx, opt, C.byref(v)))
+        return v.value
+
+    def set_options(self, **opts):
+        for k, v in opts.items():
+            self.set_option(k, v)
+
     def capture_correspondences(self, on=True):
         """Keep every iteration's correspondences of register_frame (imls_capture_correspondences)."""
         self._check(self.lib.imls_capture_correspondences(self.ctx, int(bool(on))))
@@ -694,14 +709,23 @@ class LaserOdometry:
         self.close()
 
     def process(self, filtered_cloud, flat_cloud, timestamp: str = ""):
+        # the reference's step timers (laser_odometry.cpp:418-420, 461-475, 660, 677): with output_dir,
+        # "Frame time", "1. Preprocessing", "2. Matching and solving in flat points" (registered
+        # frames only) and "Total time" are appended to laser_odometry_times.txt
+        times = TimesLog(self.output_dir) if self.output_dir else None
         result = None
+        n_flat = len(flat_cloud)
+        registers = self.frame_count != 0 and n_flat != 0 and self.ctx.n_target != 0
+        if registers:
+            self.ctx.set_source(flat_cloud)            # the flat cloud's upload: this path's preprocessing
+        if times:
+            times.frame(timestamp)
+            times.step("1. Preprocessing")
         if self.frame_count != 0:
-            n_flat = len(flat_cloud)
-            if n_flat == 0 or self.ctx.n_target == 0:
+            if not registers:
                 # in_cloud / the map is empty: the first iteration's gate breaks with rPose = I (570-576)
                 result = dict(pose=np.eye(4), iters=0, status=_abi.IMLS_FRAME_TOO_FEW, trace=[])
             else:
-                self.ctx.set_source(flat_cloud)
                 result = self.ctx.register_frame()
                 if self.output_dir:
                     self._save_iterations(result, timestamp)
@@ -711,8 +735,12 @@ class LaserOdometry:
             self.results.append((timestamp, result["pose"], result["iters"], result["status"]))
             if self.pose_file:
                 savePoseToFile(now, self.pose_file, timestamp)
+            if times:
+                times.step("2. Matching and solving in flat points")
         self.ctx.map_push(filtered_cloud)
         self.frame_count += 1
+        if times:
+            times.total("Total time")
         return result
 
     def _save_iterations(self, result, timestamp: str):
@@ -725,6 +753,44 @@ class LaserOdometry:
             saveMatchedPointsToFile(x, y, os.path.join(self.output_dir, "matched_points", f"{timestamp}_{i}.txt"))
             savePoseToFile(np.array(result["trace"][i].pose).reshape(4, 4),
                            os.path.join(self.output_dir, "imls_iter_results.txt"), timestamp)
+
+
+class TimesLog:
+    """TicToc::tocAndLog (tic_toc.h:28-38) as processData uses it (laser_odometry.cpp:418-420,
+    461-475, 660, 677): two clocks started together (t_whole, t_step); a step line is the time since
+    t_step started (tocAndLog does not restart it, so "2." includes "1."), `<step>: <ms> ms` with
+    std::fixed and 3 decimals, appended to <dir>/laser_odometry_times.txt."""
+
+    FILE = "laser_odometry_times.txt"
+
+    def __init__(self, directory: str):
+        import os
+        import time
+        self.path = os.path.join(directory, self.FILE)
+        self._now = time.perf_counter
+        self.t_whole = self.t_step = self._now()
+
+    def _append(self, line: str):
+        with open(self.path, "a") as f:
+            f.write(line + "\n")
+
+    def frame(self, timestamp: str):
+        self._append(f"Frame time: {timestamp}")
+
+    def step(self, name: str) -> float:
+        ms = (self._now() - self.t_step) * 1000.0
+        self._append(format_time_line(name, ms))
+        return ms
+
+    def total(self, name: str) -> float:
+        ms = (self._now() - self.t_whole) * 1000.0
+        self._append(format_time_line(name, ms))
+        return ms
+
+
+def format_time_line(step: str, ms: float) -> str:
+    """tic_toc.h:34: `file << std::fixed << std::setprecision(3) << stepName << ": " << time << " ms"`."""
+    return f"{step}: {ms:.3f} ms"
 
 
 def _quat_xyzw(R) -> tuple:

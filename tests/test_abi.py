@@ -148,3 +148,24 @@ def test_product_path_fails_loudly_without_gpu():
 def test_missing_library_raises(tmp_path):
     with pytest.raises(RuntimeError, match="HIP extension missing"):
         _abi.load_library(tmp_path / "nope.so")
+
+
+def test_library_reads_no_tuning_environment():
+    """Runtime tuning goes through imls_set_option only (ADVICE/VERDICT r04): the only IMLS_*
+    environment name left in the product library is the host-side trace switch IMLS_DEBUG_HOST."""
+    data = _abi.LIB_PATH.read_bytes()
+    import re
+    names = set(re.findall(rb"IMLS_[A-Z0-9_]+", data))
+    assert names <= {b"IMLS_DEBUG_HOST"}, names
+
+
+def test_option_ids_match_header():
+    """imls_option / imls_traversal enum values in include/imls_gpu.h equal the Python mirror."""
+    text = HEADER.read_text()
+    import re
+    for name, val in _abi.OPTION_IDS.items():
+        m = re.search(rf"IMLS_OPT_{name.upper()}\s*=\s*(\d+)", text)
+        assert m and int(m.group(1)) == val, name
+    for name in ("AUTO", "PACKETS", "WAVE_PER_QUERY", "LANE"):
+        m = re.search(rf"IMLS_TRAVERSAL_{name}\s*=\s*(\d+)", text)
+        assert m and int(m.group(1)) == getattr(_abi, f"IMLS_TRAVERSAL_{name}"), name

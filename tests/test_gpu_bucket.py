@@ -1,7 +1,7 @@
-"""Leaves smaller than one wave (IMLS_BUCKET = 16 / 32 points per leaf) through the packet traversal.
+"""Leaves smaller than one wave (option leaf_size = 16 / 32 points per leaf) through the packet traversal.
 
 The lockstep leaf scan counts a lane's already-listed points of the leaf before it builds the
-listed-point mask (kp.lazy_listed).  That count must cover the leaf's own `cnt = min(B, M − base)`
+listed-point mask.  That count must cover the leaf's own `cnt = min(B, M − base)`
 points only: with B < 64 a 64-slot window also counts listed points of the FOLLOWING leaves, a lane
 with one new candidate then looks like it has none, the candidate is dropped and the list's bound W
 claims a point was searched when it was not.  The correspondences of every iteration
@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import oracle_ctypes as oc
-from planetary_lidar_odometry_amd import config, imls_icp, synth
+from planetary_lidar_odometry_amd import _abi, config, imls_icp, synth
 
 pytestmark = pytest.mark.gpu
 GOLDEN = pathlib.Path(__file__).resolve().parent / "golden"
@@ -24,15 +24,15 @@ GOLDEN = pathlib.Path(__file__).resolve().parent / "golden"
 @pytest.mark.parametrize("qwave", ["0", "1"], ids=["packets", "wave_per_query"])
 @pytest.mark.parametrize("bucket", ["16", "32"])
 @pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair"])
-def test_small_leaves_match_oracle(name, bucket, qwave, monkeypatch):
+def test_small_leaves_match_oracle(name, bucket, qwave):
     """packets: the lockstep leaf scan; wave per query: the frontier traversal, whose leaf groups
     measure B / 8 points per lane (2 at B = 16)."""
     g = dict(np.load(GOLDEN / f"{name}.npz"))
     src, tgt = np.ascontiguousarray(g["src"]), np.ascontiguousarray(g["tgt"])
-    monkeypatch.setenv("IMLS_BUCKET", bucket)       # read when the context is created
-    monkeypatch.setenv("IMLS_QWAVE", qwave)
     p = config.bench_params(8)
     with imls_icp.ImlsContext(p) as ctx:
+        ctx.set_options(leaf_size=int(bucket), traversal=_abi.IMLS_TRAVERSAL_PACKETS if qwave == "0"
+                        else _abi.IMLS_TRAVERSAL_WAVE_PER_QUERY)
         ctx.set_target(np.ascontiguousarray(tgt.T))
         ctx.set_source(np.ascontiguousarray(src.T))
         assert ctx.index_stats()["bucket"] == int(bucket)

@@ -43,8 +43,10 @@ def _single(p, frames):
     return out
 
 
-def _batched(p, frames, repeat=1):
+def _batched(p, frames, repeat=1, opts=None):
     ctxs = [imls_icp.ImlsContext(p) for _ in frames]
+    for c in ctxs:
+        c.set_options(**(opts or {}))
     try:
         res = None
         for _ in range(repeat):
@@ -337,18 +339,16 @@ class _DevSoa:
 
 
 @pytest.mark.parametrize("packet,iters", [(16, 20), (32, 3)])
-def test_traversal_packet_sizes_in_batches(hdl_pair, monkeypatch, packet, iters):
-    """The traversal packet size (queries per wave, IMLS_PACKET / IMLS_PACKET_ITERS; batched
-    launches too with IMLS_PACKET_BATCH) only changes which waves walk which queries: the lists it
+def test_traversal_packet_sizes_in_batches(hdl_pair, packet, iters):
+    """The traversal packet size (queries per wave, options first_packet / first_packet_iters;
+    batched launches too with first_packet_batched) only changes which waves walk which queries: the lists it
     hands k_finish are certified there, so every frame's pose, iterations and trace stay bit-equal
     to the default single-frame path (32-query packets in iteration 0 only)."""
     frames = [(hdl_pair.source, hdl_pair.target),
               (synth.fps_subsample(hdl_pair.source, 40000, seed=11), hdl_pair.target)]
     ref = _single(_params(6), frames)
-    monkeypatch.setenv("IMLS_PACKET", str(packet))
-    monkeypatch.setenv("IMLS_PACKET_ITERS", str(iters))
-    monkeypatch.setenv("IMLS_PACKET_BATCH", "1")
-    poses, its, status, traces = _batched(_params(6), frames)
+    poses, its, status, traces = _batched(_params(6), frames,
+                                          opts=dict(first_packet=packet, first_packet_iters=iters, first_packet_batched=1))
     for k, r in enumerate(ref):
         assert np.array_equal(r["pose"], poses[k]), (k, np.abs(r["pose"] - poses[k]).max())
         assert (r["iters"], r["status"]) == (its[k], status[k]), k

@@ -60,14 +60,13 @@ def check_projection(got, want_idx, want_rej, want_x, want_y, want_n):
 
 
 @pytest.fixture(params=["auto", "0", "1"], ids=["auto", "packets", "wave_per_query"])
-def traversal(request, monkeypatch):
+def traversal(request, ctx):
     """Both traversal kernels on the same inputs: packets of 64 queries (k_knn_wave) and one wave
-    per query (k_knn_qwave); the choice is read when the parameters are set."""
-    if request.param != "auto":
-        monkeypatch.setenv("IMLS_QWAVE", request.param)
-    else:
-        monkeypatch.delenv("IMLS_QWAVE", raising=False)
-    return request.param
+    per query (k_knn_qwave), through the option imls_set_option(IMLS_OPT_TRAVERSAL)."""
+    ctx.set_option("traversal", {"auto": _abi.IMLS_TRAVERSAL_AUTO, "0": _abi.IMLS_TRAVERSAL_PACKETS,
+                                 "1": _abi.IMLS_TRAVERSAL_WAVE_PER_QUERY}[request.param])
+    yield request.param
+    ctx.set_option("traversal", _abi.IMLS_TRAVERSAL_AUTO)
 
 
 @pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair"])

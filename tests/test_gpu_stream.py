@@ -218,3 +218,7 @@ def test_per_iteration_outputs(vlp_frames, tmp_path):
                 assert np.abs(np.array(r["trace"][i].pose) - np.array(want["trace"][i].pose)).max() < 1e-6
             assert not (out / "matched_points" / f"{ts}_{r['iters']}.txt").exists()
             n_lines += r["iters"]
+    # the reference's step timer log (laser_odometry.cpp:461-475, 660, 677; tic_toc.h:28-38)
+    from test_times_log import check_times_log
+    check_times_log((out / "laser_odometry_times.txt").read_text(),
+                    [f"{1317384506.0 + 0.1 * k:f}" for k in range(len(frames))], first_registers=False)

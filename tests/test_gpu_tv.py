@@ -168,19 +168,19 @@ def test_tv_frames_one_launch(g):
 
 
 @pytest.mark.parametrize("skin", ["0.01", "0.03", "0.3"])
-def test_tv_skin_lists_bit_identical(g, monkeypatch, skin):
+def test_tv_skin_lists_bit_identical(g, skin):
     """Skin lists (a walk stores the ball of ρ + skin; later iterations screen the stored set while
     the query moved ≤ skin) must not change a single bit: register_frame and the batched frames
-    path with lists on equal the walk-every-iteration run (IMLS_TV_SKIN=0).  0.3 m overflows the
+    path with lists on equal the walk-every-iteration run (option tv_skin 0).  0.3 m overflows the
     64-entry lists for most queries (the no-list path)."""
     p = tv_params()
     src = rows(g["src"])
     sources = [src, src[::2].copy()]
 
     def run(sk):
-        monkeypatch.setenv("IMLS_TV_SKIN", sk)
         out = []
         with imls_icp.ImlsContext(p) as c:
+            c.set_option("tv_skin", float(sk))
             for s in sources:
                 c.set_target(rows(g["tgt"]))
                 c.set_target_tensors(rows(g["ten"]))
@@ -189,6 +189,7 @@ def test_tv_skin_lists_bit_identical(g, monkeypatch, skin):
         ctxs = [imls_icp.ImlsContext(p) for _ in sources]
         try:
             for c, s in zip(ctxs, sources):
+                c.set_option("tv_skin", float(sk))
                 c.set_target(rows(g["tgt"]))
                 c.set_target_tensors(rows(g["ten"]))
                 c.set_source(s)

@@ -1,6 +1,6 @@
 """Verlet-list reuse (k_knn_wave / k_knn_qwave skip the traversal while a query's previous
 neighbour list stays certified) must not change a single correspondence: per-iteration valid
-counts and reject counters are compared exactly with the reuse switched off (IMLS_VERLET=0), and
+counts and reject counters are compared exactly with the reuse switched off (option list_reuse 0), and
 the poses to 1e-12 — the correspondences are identical, but a query whose reused bound fails the
 fp64 certificate is finished by the exact fallback kernel, which sums its normal-equation terms
 in a different slab (a different fp64 association).  The full config-B frame is also compared
@@ -31,9 +31,13 @@ def _params(iters=20, shipped_thresholds=True):
     return p
 
 
-def _frame(ctx, p, verlet, monkeypatch):
-    monkeypatch.setenv("IMLS_VERLET", "1" if verlet else "0")
-    ctx.set_params(p)          # KParams (incl. the reuse switch) are read when params are set
+TRAVERSAL = {"auto": _abi.IMLS_TRAVERSAL_AUTO, "0": _abi.IMLS_TRAVERSAL_PACKETS,
+             "1": _abi.IMLS_TRAVERSAL_WAVE_PER_QUERY}
+
+
+def _frame(ctx, p, verlet):
+    ctx.set_params(p)
+    ctx.set_option("list_reuse", 1 if verlet else 0)
     ctx.enable_stats(True)
     r = ctx.register_frame()
     r["stats"] = ctx.traversal_stats()
@@ -50,10 +54,17 @@ def _same_frame(a, b):
 
 
 @pytest.fixture(scope="module")
-def ctx():
+def _ctx():
     c = imls_icp.ImlsContext(_params())
     yield c
     c.close()
+
+
+@pytest.fixture
+def ctx(_ctx):
+    """The module's context with the default options at the start of every test."""
+    _ctx.set_options(traversal=_abi.IMLS_TRAVERSAL_AUTO, list_reuse=1, force_fallback=0)
+    return _ctx
 
 
 @pytest.fixture(scope="module")
@@ -63,38 +74,35 @@ def config_b():
 
 @pytest.mark.parametrize("qwave", ["0", "1"], ids=["packets", "wave_per_query"])
 @pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair"])
-def test_reuse_bit_identical_on_golden_pairs(ctx, name, qwave, monkeypatch):
+def test_reuse_bit_identical_on_golden_pairs(ctx, name, qwave):
     g = dict(np.load(GOLDEN / f"{name}.npz"))
-    monkeypatch.setenv("IMLS_QWAVE", qwave)
+    ctx.set_option("traversal", TRAVERSAL[qwave])
     ctx.set_target(np.ascontiguousarray(g["tgt"].T))
     ctx.set_source(np.ascontiguousarray(g["src"].T))
     p = _params(10, shipped_thresholds=False)
-    on = _frame(ctx, p, True, monkeypatch)
-    off = _frame(ctx, p, False, monkeypatch)
+    on = _frame(ctx, p, True)
+    off = _frame(ctx, p, False)
     _same_frame(on, off)
     assert off["stats"]["verlet_reused"] == 0
     assert on["stats"]["verlet_reused"] > 0, on["stats"]
 
 
-def test_config_b_reuse_bit_identical(ctx, config_b, monkeypatch):
-    monkeypatch.delenv("IMLS_QWAVE", raising=False)
+def test_config_b_reuse_bit_identical(ctx, config_b):
     ctx.set_target(config_b.target)
     ctx.set_source(config_b.source)
     p = _params(20, shipped_thresholds=False)
-    on = _frame(ctx, p, True, monkeypatch)
-    off = _frame(ctx, p, False, monkeypatch)
+    on = _frame(ctx, p, True)
+    off = _frame(ctx, p, False)
     _same_frame(on, off)
     q = on["stats"]
     # most lists are reused once the pose settles (iterations 1..19 offer N lanes each)
     assert q["verlet_reused"] > 0.3 * 19 * config_b.source.size, q
 
 
-def test_config_b_frame_matches_oracle(ctx, config_b, monkeypatch):
+def test_config_b_frame_matches_oracle(ctx, config_b):
     """The headline workload end to end (index build + up to 20 iterations, shipped convergence
     thresholds) against the oracle: iterations, status, per-iteration valid counts and reject
     counters exact; pose within POSE_TOL."""
-    monkeypatch.delenv("IMLS_QWAVE", raising=False)
-    monkeypatch.setenv("IMLS_VERLET", "1")
     p = _params(20)
     ctx.set_params(p)
     ctx.set_target(config_b.target)
@@ -109,12 +117,11 @@ def test_config_b_frame_matches_oracle(ctx, config_b, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["vlp16_pair", "planetary_pair", "config_b"])
-def test_forced_fallback_same_correspondences(ctx, config_b, name, monkeypatch):
-    """Every 3rd query deferred to the exact fallback kernel (test hook IMLS_FORCE_FALLBACK), which
+def test_forced_fallback_same_correspondences(ctx, config_b, name):
+    """Every 3rd query deferred to the exact fallback kernel (test hook option force_fallback), which
     searches the ball its k_finish list bounds (max(K-th listed key, listed NN-1)) instead of the
     whole radius: the same correspondences — valid counts and reject counters exact per iteration —
     and poses within 1e-12 of the run without deferrals (the fallback's rows sum in other slabs)."""
-    monkeypatch.delenv("IMLS_QWAVE", raising=False)
     if name == "config_b":
         ctx.set_target(config_b.target)
         ctx.set_source(config_b.source)
@@ -123,9 +130,9 @@ def test_forced_fallback_same_correspondences(ctx, config_b, name, monkeypatch):
         ctx.set_target(np.ascontiguousarray(g["tgt"].T))
         ctx.set_source(np.ascontiguousarray(g["src"].T))
     p = _params(10, shipped_thresholds=False)
-    monkeypatch.setenv("IMLS_FORCE_FALLBACK", "3")
-    forced = _frame(ctx, p, True, monkeypatch)
-    monkeypatch.delenv("IMLS_FORCE_FALLBACK")
-    plain = _frame(ctx, p, True, monkeypatch)
+    ctx.set_option("force_fallback", 3)
+    forced = _frame(ctx, p, True)
+    ctx.set_option("force_fallback", 0)
+    plain = _frame(ctx, p, True)
     _same_frame(forced, plain)
     assert forced["stats"]["uncertified"] > 0.3 * 10 * (config_b.source.size if name == "config_b" else 1), forced["stats"]

@@ -1,0 +1,71 @@
+"""CPU tests: the reference's step timer log, laser_odometry_times.txt (TicToc::tocAndLog,
+/root/reference/include/tic_toc.h:28-38, as processData calls it at laser_odometry.cpp:418-420,
+461-475, 660, 677): per frame a "Frame time: <ts>" line, then "1. Preprocessing: <ms> ms", on
+registered frames "2. Matching and solving in flat points: <ms> ms" (t_step is not restarted, so it
+includes step 1), and "Total time: <ms> ms" — std::fixed, 3 decimals.  The GPU stream test
+(tests/test_gpu_stream.py::test_per_iteration_outputs) checks the file LaserOdometry writes."""
+import re
+
+from planetary_lidar_odometry_amd import imls_icp
+
+STEP1 = "1. Preprocessing"
+STEP2 = "2. Matching and solving in flat points"
+TOTAL = "Total time"
+_LINE = re.compile(r"^(.*): (\d+\.\d{3}) ms$")
+
+
+def check_times_log(text: str, timestamps, first_registers: bool = False):
+    """Validate a laser_odometry_times.txt: one block per frame in order; the first frame only
+    seeds the map (no step 2) unless first_registers."""
+    lines = text.splitlines()
+    at = 0
+    for k, ts in enumerate(timestamps):
+        assert lines[at] == f"Frame time: {ts}", (k, lines[at])
+        at += 1
+        names = [STEP1] + ([STEP2] if (k > 0 or first_registers) else []) + [TOTAL]
+        vals = []
+        for name in names:
+            m = _LINE.match(lines[at])
+            assert m and m.group(1) == name, (k, lines[at])
+            vals.append(float(m.group(2)))
+            at += 1
+        assert all(v >= 0 for v in vals)
+        if len(vals) == 3:
+            assert vals[0] <= vals[1] + 1e-3      # "2." is cumulative from t_step's start
+        assert vals[-2] <= vals[-1] + 1e-3 or len(vals) == 2
+    assert at == len(lines)
+
+
+def test_format_line():
+    assert imls_icp.format_time_line(STEP1, 0.0) == "1. Preprocessing: 0.000 ms"
+    assert imls_icp.format_time_line(TOTAL, 12.3456) == "Total time: 12.346 ms"
+    assert imls_icp.format_time_line(STEP2, 1234.5) == "2. Matching and solving in flat points: 1234.500 ms"
+
+
+def test_times_log_sequence(tmp_path):
+    """The call order processData makes, against a fake clock: step times measured from t_step's
+    start (cumulative), the total from t_whole's."""
+    clock = iter([0.0, 0.0015, 0.0105, 0.0125])       # start, step 1, step 2, total (seconds)
+    log = imls_icp.TimesLog.__new__(imls_icp.TimesLog)
+    log.path = str(tmp_path / imls_icp.TimesLog.FILE)
+    log._now = lambda: next(clock)
+    log.t_whole = log.t_step = log._now()
+    log.frame("1317384506.100000")
+    assert log.step(STEP1) == 1.5
+    log.step(STEP2)
+    log.total(TOTAL)
+    text = (tmp_path / "laser_odometry_times.txt").read_text()
+    assert text == ("Frame time: 1317384506.100000\n1. Preprocessing: 1.500 ms\n"
+                    "2. Matching and solving in flat points: 10.500 ms\nTotal time: 12.500 ms\n")
+    check_times_log(text, ["1317384506.100000"], first_registers=True)
+
+
+def test_times_log_appends_and_checker(tmp_path):
+    for ts in ("1.000000", "2.000000"):
+        log = imls_icp.TimesLog(str(tmp_path))
+        log.frame(ts)
+        log.step(STEP1)
+        if ts != "1.000000":
+            log.step(STEP2)
+        log.total(TOTAL)
+    check_times_log((tmp_path / imls_icp.TimesLog.FILE).read_text(), ["1.000000", "2.000000"])
