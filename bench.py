@@ -51,6 +51,7 @@ plo_amd.load()
 from planetary_lidar_odometry_amd import _abi, config, imls_icp, sequences, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E nominal (MI355X_MICROARCH.md chip table)
+B_HOST_DEFAULT = False  # config B: host hand-over by default (else --host-inputs)
 
 
 def log(*a):
@@ -462,14 +463,19 @@ class PairRunner:
         return out
 
     def single_fresh(self, k: int, rot: int = 0):
-        """Pair k registered alone on a fresh context whose map is the pair's scans concatenated from
-        scan `rot` on (host mode: what the FIFO held for a load with that rotation): the single-frame
-        kernels, tagged like Pipeline."""
-        parts = self.parts[k] if self.host else [self.pairs[k].target]
+        """Pair k registered alone on a fresh context whose map is the pair's scans from scan `rot`
+        on (host mode: the same FIFO content — the scans pushed in that order, so its incremental
+        index is the one the timed context built; else the pair's target): the single-frame kernels,
+        tagged like Pipeline."""
         with imls_icp.ImlsContext(self.p, device=self.local) as c:
             if self.ransac:
                 c.set_rng_state(self.seed_state)
-            c.set_target(np.concatenate(parts[rot:] + parts[:rot]))
+            if self.host:
+                parts = self.parts[k]
+                for part in parts[rot:] + parts[:rot]:
+                    c.map_push(part, count=False)
+            else:
+                c.set_target(self.pairs[k].target)
             c.set_source(self.pairs[k].source)
             r = c.register_frame()
         return (k, r["pose"], r["iters"], r["status"], r["trace"])
@@ -777,6 +783,8 @@ def main():
                     help="inputs handed over in host memory, PCIe inside the timed region (stream: the new map "
                          "scan + flat cloud per frame; A/B: each pair's map is a device FIFO of its scans, the newest "
                          "scan + the source cross PCIe per registration, SURVEY §8(d) t_pair)")
+    ap.add_argument("--resident-inputs", action="store_true",
+                    help="B: inputs already resident in HBM (the default for B is the host hand-over: --host-inputs)")
     ap.add_argument("--latency-pairs", type=int, default=50, help="single-pair latency / roofline probe size")
     ap.add_argument("--busy-steps", type=int, default=5, help="steps of the HIP-event busy-time pass (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
@@ -786,6 +794,10 @@ def main():
     ap.add_argument("--workload", choices=["B", "stream", "A", "E"], default="B")
     ap.add_argument("--solver", choices=["LS", "RANSAC_DRPM"], default="LS")
     args = ap.parse_args()
+    # config B's headline includes SURVEY §8(d)'s t_pair hand-over: the newest map scan and the source
+    # cross PCIe per registration (the map a device FIFO with its incremental index)
+    if args.workload == "B" and B_HOST_DEFAULT and not args.resident_inputs:
+        args.host_inputs = True
 
     import torch
     import torch.distributed as dist

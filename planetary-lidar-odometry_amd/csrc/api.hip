@@ -61,9 +61,33 @@ struct imls_ctx {
     DevBuf spt, snr, sscratch, qperm, upload_s, skept;
     // map FIFO (accumulateTargetCloud, laser_odometry.cpp:116-136): the last max_queue_size filtered
     // scans, each SoA6 in its own slot, and their concatenation (oldest first) the index is built from
-    struct MapSlot { DevBuf buf; size_t n = 0; bool ghost = false; };
+    // a FIFO entry: its raw SoA6 scan (the concatenation path), and for the incremental index its
+    // filtered points (fpt / fnr, NaN filter at the push) and its sorted run (index.hip)
+    struct MapSlot {
+        DevBuf buf, fpt, fnr, run;
+        size_t n = 0;
+        bool ghost = false;
+        int id = -1;                      // run id (incremental index)
+        int nk = -1;                      // kept count after the NaN filter (−1: not read yet)
+        bool sorted = false;              // run built under the current quantisation frame
+    };
     std::deque<MapSlot> fifo;
-    std::vector<DevBuf> slot_pool;        // freed slots, reused (no allocation per frame)
+    std::vector<MapSlot> slot_pool;       // freed slots, their buffers reused (no allocation per frame)
+    // incremental FIFO index (max_queue_size 2..kMaxFifoRuns−1): each scan sorted once at its first
+    // build under a quantisation frame fixed for the FIFO, the previous merged order kept across
+    // registrations (finish_target → fifo_build)
+    bool fifo_inc = false;                // the current / pending target is the FIFO's incremental index
+    unsigned fifo_seq = 0;                // run ids: pushes mod kMaxFifoRuns
+    int* h_fifo_cnt = nullptr;            // pinned [kMaxFifoRuns]: kept count of each run's filter
+    unsigned* h_fifo_clamp = nullptr;     // pinned: points outside the frame at the last build
+    FifoRun* h_runtab = nullptr;          // pinned [kMaxFifoRuns]: the run table's upload source
+    DevBuf fifo_dev;                      // fq[4] | clamp counter | run table [kMaxFifoRuns]
+    bool fq_valid = false;
+    std::vector<int> merged_ids;          // runs in the merged order, oldest first
+    DevBuf mkey[2], mval[2];
+    int mcur = 0, m_n = 0;
+    DevBuf fscr;                          // FIFO build scratch
+    hipEvent_t ev_fifo = nullptr;         // after the last incremental build (batch joins)
     DevBuf macc;
     size_t map_points = 0;                // Σ n over the FIFO (before the NaN filter)
     DevBuf fb;                            // deferred-query counts per k_finish block + their lists
@@ -670,10 +694,13 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
 
 int gather_tensors(imls_ctx* c, hipStream_t s, const float* d_ten6, size_t n);
 
+int fifo_build(imls_ctx* c);
+
 // Phase B of a pending target build (waits for its filter's kept count).
 int finish_target(imls_ctx* c) {
     if (!c->tgt_pending) return IMLS_OK;
     c->tgt_pending = false;
+    if (c->fifo_inc) return fifo_build(c);
     if (c->tgt_filter_deferred) {
         c->tgt_filter_deferred = false;
         if (int rc = filter_async(c->stream, c->tf_soa, c->tf_n, c->tpt, c->tnr, c->tscratch, (unsigned*)c->tkept.p,
@@ -755,6 +782,15 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused, HostS
         timing |= ctxs[k]->timing == 1;
     }
     if (!any) return IMLS_OK;
+    // incremental FIFO targets (index.hip fifo_*): each member's own build on its stream (a merge of
+    // sorted runs, not the batch's one radix sort), joined by the lead's stream
+    for (size_t k = 0; k < n; ++k) {
+        imls_ctx* c = ctxs[k];
+        if (!c->tgt_pending || !c->fifo_inc) continue;
+        if (int rc = finish_target(c)) return fail(L, rc, "context " + std::to_string(k) + ": " + c->err);
+        if (c != L && c->has_target && hipStreamWaitEvent(L->stream, c->ev_fifo, 0) != hipSuccess)
+            return fail(L, IMLS_ERR_DEVICE, "FIFO build join");
+    }
     if (timing) {
         for (size_t k = 0; k < n; ++k)
             if (int rc = ensure_built(ctxs[k])) return fail(L, rc, "context " + std::to_string(k) + ": " + ctxs[k]->err);
@@ -879,6 +915,7 @@ bool defer_filter(const imls_ctx* c) { return c->defer; }
 
 int do_set_target(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_kept) {
     if (n == 0 || n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "target size out of range");
+    c->fifo_inc = false;
     if (!grow(c->tkept, n * 4 + 16)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (kept)");
     if (!c->ev_tgt && hipEventCreateWithFlags(&c->ev_tgt, hipEventDisableTiming) != hipSuccess)
         return fail(c, IMLS_ERR_DEVICE, "hipEventCreate");
@@ -949,6 +986,8 @@ int gather_tensors(imls_ctx* c, hipStream_t s, const float* d_ten6, size_t n) {
 // right after the build (alone, or with a batch's builds), reading d_ten6 then.
 int do_set_tensors(imls_ctx* c, const float* d_ten6, size_t n) {
     if (!c->has_target) return fail(c, IMLS_ERR_STATE, "set_target first");
+    // (the incremental FIFO index keeps no filtered → input index of the concatenation)
+    if (c->fifo_inc) return fail(c, IMLS_ERR_UNSUPPORTED, "tensor inputs need a set_target map, not the FIFO index");
     if (n != c->n_target_in) return fail(c, IMLS_ERR_ARG, "tensor count must equal the last set_target's point count");
     if (c->tgt_pending) {
         c->ten_src = d_ten6;
@@ -1084,8 +1123,13 @@ void imls_destroy(imls_ctx* c) {
                       &c->upload_s, &c->cs, &c->cd, &c->cn, &c->solve_mem, &c->trace_mem, &c->stats, &c->rows_d, &c->pose_tmp};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
-    for (auto& sl : c->fifo) if (sl.buf.p) (void)hipFree(sl.buf.p);
-    for (auto& b : c->slot_pool) if (b.p) (void)hipFree(b.p);
+    for (auto* v : {&c->fifo}) for (auto& sl : *v) for (DevBuf* b : {&sl.buf, &sl.fpt, &sl.fnr, &sl.run}) if (b->p) (void)hipFree(b->p);
+    for (auto& sl : c->slot_pool) for (DevBuf* b : {&sl.buf, &sl.fpt, &sl.fnr, &sl.run}) if (b->p) (void)hipFree(b->p);
+    for (DevBuf* b : {&c->fifo_dev, &c->mkey[0], &c->mkey[1], &c->mval[0], &c->mval[1], &c->fscr}) if (b->p) (void)hipFree(b->p);
+    if (c->h_fifo_cnt) (void)hipHostFree(c->h_fifo_cnt);
+    if (c->h_fifo_clamp) (void)hipHostFree(c->h_fifo_clamp);
+    if (c->h_runtab) (void)hipHostFree(c->h_runtab);
+    if (c->ev_fifo) (void)hipEventDestroy(c->ev_fifo);
     if (c->macc.p) (void)hipFree(c->macc.p);
     if (c->skept.p) (void)hipFree(c->skept.p);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -1263,6 +1307,157 @@ int imls_set_target_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n
 // PCIe traffic; else copied device-to-device), the oldest entry is dropped once when the FIFO holds
 // more than max_queue_size (the reference's `if`, not a loop), the entries are concatenated oldest
 // first into one SoA6 map in HBM (one 2-D device copy per entry) and the index is rebuilt over it.
+namespace {
+// ---- incremental FIFO index -----------------------------------------------------------------
+// Used for max_queue_size 2 … kMaxFifoRuns − 1 (queue 1 indexes its one scan in place; a run id
+// must be unique among the FIFO's entries).
+bool fifo_incremental(const imls_ctx* c) { return c->P.max_queue_size >= 2 && c->P.max_queue_size < kMaxFifoRuns; }
+
+int ensure_fifo(imls_ctx* c) {
+    if (c->h_fifo_cnt) return IMLS_OK;
+    if (hipHostMalloc((void**)&c->h_fifo_cnt, kMaxFifoRuns * sizeof(int), hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_fifo_clamp, 64) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_runtab, kMaxFifoRuns * sizeof(FifoRun)) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "hipHostMalloc (FIFO)");
+    *c->h_fifo_clamp = 0;
+    if (!grow(c->fifo_dev, 256 + kMaxFifoRuns * sizeof(FifoRun))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (FIFO)");
+    if (hipMemsetAsync(c->fifo_dev.p, 0, 256, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipMemset (FIFO)");
+    if (hipEventCreateWithFlags(&c->ev_fifo, hipEventDisableTiming) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipEventCreate");
+    return IMLS_OK;
+}
+float* fifo_fq(imls_ctx* c) { return (float*)c->fifo_dev.p; }
+unsigned* fifo_clamp(imls_ctx* c) { return (unsigned*)((char*)c->fifo_dev.p + 64); }
+FifoRun* fifo_runtab(imls_ctx* c) { return (FifoRun*)((char*)c->fifo_dev.p + 256); }
+
+// the target is the FIFO's incremental index: pending until its first use (or at once with n_map)
+int fifo_set_target(imls_ctx* c, size_t* n_map) {
+    c->has_tensors = false;
+    c->ten_pending = false;
+    c->tgt_filter_deferred = false;
+    c->has_corr = false;
+    c->rnr_valid = false;
+    if (c->map_points == 0) {             // empty map (max_queue_size 0 or empty scans): no target
+        c->tgt_pending = false;
+        c->has_target = false;
+        c->fifo_inc = false;
+        c->M = 0;
+        if (n_map) *n_map = 0;
+        return IMLS_OK;
+    }
+    if (!c->ev_tgt && hipEventCreateWithFlags(&c->ev_tgt, hipEventDisableTiming) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "hipEventCreate");
+    if (c->tgt_slot < 0) timed_begin(c, 1, c->tgt_slot);
+    if (hipEventRecord(c->ev_tgt, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "event record");
+    c->n_target_in = c->map_points;
+    c->fifo_inc = true;
+    c->tgt_pending = true;
+    c->has_target = true;                 // provisional: the build decides (an all-NaN map has none)
+    if (n_map) {
+        if (int rc = finish_target(c)) return rc;
+        *n_map = (size_t)c->M;
+    }
+    return IMLS_OK;
+}
+
+// The build: the kept counts (one wait for every pending filter), the frame (first build, or after
+// a scan fell outside it), the runs not sorted yet, the merged order (drop evicted runs, merge the
+// new ones after the kept ones: the FIFO is oldest first), the index from it.
+int fifo_build(imls_ctx* c) {
+    if (hipEventSynchronize(c->ev_tgt) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "map filter failed");
+    hipStream_t s = c->stream;
+    size_t M = 0;
+    for (auto& e : c->fifo) {
+        if (e.nk < 0) e.nk = e.n ? c->h_fifo_cnt[e.id] : 0;
+        M += (size_t)e.nk;
+    }
+    c->M = (int)M;
+    c->has_target = M > 0;
+    if (M == 0) {
+        timed_end(c, 1, c->tgt_slot);
+        c->tgt_slot = -1;
+        return IMLS_OK;
+    }
+    if (M > (size_t)0x7fffffff) return fail(c, IMLS_ERR_CAPACITY, "map too large");
+    // re-frame when the last build's new scans fell outside the frame (their keys were clamped)
+    if (c->fq_valid && *c->h_fifo_clamp != 0) c->fq_valid = false;
+    if (!c->fq_valid) {
+        // every entry's filtered points stay in its fpt / fnr while it is in the FIFO: re-key them all
+        std::vector<std::pair<const float4*, int>> pts;
+        for (auto& e : c->fifo)
+            if (e.nk > 0) {
+                pts.push_back({(const float4*)e.fpt.p, e.nk});
+                e.sorted = false;
+            }
+        if (int rc = fifo_frame(s, pts, fifo_fq(c), c->fscr, c->err)) return rc;
+        if (hipMemsetAsync(fifo_clamp(c), 0, 4, s) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "hipMemset (clamp)");
+        c->merged_ids.clear();
+        c->m_n = 0;
+        c->fq_valid = true;
+    }
+    for (auto& e : c->fifo)
+        if (e.nk > 0 && !e.sorted) {
+            if (int rc = fifo_run_build(s, (const float4*)e.fpt.p, (const float4*)e.fnr.p, e.nk, fifo_fq(c), fifo_clamp(c), e.run,
+                                        c->fscr, c->err))
+                return rc;
+            e.sorted = true;
+        }
+    // the merged order: its runs must be a prefix of the FIFO's (new runs are the newest) — else restart
+    auto merged = [&](int id) { return std::find(c->merged_ids.begin(), c->merged_ids.end(), id) != c->merged_ids.end(); };
+    bool seen_new = false, prefix = true;
+    unsigned live = 0;
+    int kept_n = 0;
+    for (auto& e : c->fifo) {
+        if (e.nk <= 0) continue;
+        if (!merged(e.id)) { seen_new = true; continue; }
+        if (seen_new) prefix = false;
+        live |= 1u << e.id;
+        kept_n += e.nk;
+    }
+    if (!prefix) { c->merged_ids.clear(); c->m_n = 0; live = 0; kept_n = 0; }
+    for (int k = 0; k < 2; ++k)
+        if (!grow(c->mkey[k], M * 8 + 64) || !grow(c->mval[k], M * 4 + 64)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (FIFO order)");
+    auto K = [&](int k) { return (unsigned long long*)c->mkey[k].p; };
+    auto V = [&](int k) { return (unsigned*)c->mval[k].p; };
+    if (c->m_n > 0 && kept_n != c->m_n) {            // evicted runs: stable compaction
+        if (int rc = fifo_keep(s, K(c->mcur), V(c->mcur), c->m_n, live, K(c->mcur ^ 1), V(c->mcur ^ 1), c->fscr, c->err)) return rc;
+        c->mcur ^= 1;
+    }
+    c->m_n = c->m_n > 0 ? kept_n : 0;
+    std::vector<int> ids;
+    for (auto& e : c->fifo)
+        if (e.nk > 0 && (live >> e.id & 1u)) ids.push_back(e.id);
+    for (auto& e : c->fifo) {
+        if (e.nk <= 0 || (live >> e.id & 1u)) continue;
+        if (int rc = fifo_merge(s, K(c->mcur), V(c->mcur), c->m_n, fifo_run_keys(e.run.p, e.nk), (unsigned)e.id, e.nk,
+                                K(c->mcur ^ 1), V(c->mcur ^ 1), c->fscr, c->err))
+            return rc;
+        c->mcur ^= 1;
+        c->m_n += e.nk;
+        ids.push_back(e.id);
+    }
+    c->merged_ids = ids;
+    // run table: each run's records and its offset in the concatenation (the libnabo tie order)
+    unsigned off = 0;
+    for (auto& e : c->fifo) {
+        if (e.nk <= 0) continue;
+        c->h_runtab[e.id] = FifoRun{fifo_run_pts(e.run.p, e.nk), fifo_run_nrm(e.run.p, e.nk), off, 0u};
+        off += (unsigned)e.nk;
+    }
+    if (hipMemcpyAsync(fifo_runtab(c), c->h_runtab, kMaxFifoRuns * sizeof(FifoRun), hipMemcpyHostToDevice, s) != hipSuccess)
+        return fail(c, IMLS_ERR_DEVICE, "run table upload");
+    int rc = fifo_index(s, K(c->mcur), V(c->mcur), c->M, fifo_runtab(c), fifo_fq(c), c->B, c->lkeys, c->mpt, c->nodes,
+                        c->treescratch, &c->Pl, &c->levels, c->err);
+    if (rc) return rc;
+    // this build's clamp count, read at the next build (its events order the copy before that read)
+    (void)hipMemcpyAsync(c->h_fifo_clamp, fifo_clamp(c), 4, hipMemcpyDeviceToHost, s);
+    (void)hipEventRecord(c->ev_fifo, s);
+    timed_end(c, 1, c->tgt_slot);
+    c->tgt_slot = -1;
+    return IMLS_OK;
+}
+
+}  // namespace
+
 static int map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, size_t stride, const float* d_soa6,
                     size_t* n_map) {
     if (n > (size_t)0x7fffffff) return fail(c, IMLS_ERR_ARG, "scan too large");
@@ -1271,8 +1466,10 @@ static int map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, s
     // stream, as the slot copy would), no FIFO copy
     if (d_soa6 && c->P.max_queue_size == 1) {
         for (auto& e : c->fifo)
-            if (!e.ghost) c->slot_pool.push_back(e.buf);
+            if (!e.ghost) c->slot_pool.push_back(e);
         c->fifo.clear();
+        c->merged_ids.clear();
+        c->m_n = 0;
         imls_ctx::MapSlot ghost;          // bookkeeping only: its data stays with the caller
         ghost.n = n;
         ghost.ghost = true;
@@ -1289,26 +1486,50 @@ static int map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, s
         return do_set_target(c, d_soa6, n, n_map);
     }
     imls_ctx::MapSlot sl;
-    if (!c->slot_pool.empty()) { sl.buf = c->slot_pool.back(); c->slot_pool.pop_back(); }
+    if (!c->slot_pool.empty()) { sl = c->slot_pool.back(); c->slot_pool.pop_back(); }
     sl.n = n;
-    if (n > 0) {
-        if (!grow(sl.buf, n * 24)) { c->slot_pool.push_back(sl.buf); return fail(c, IMLS_ERR_DEVICE, "hipMalloc (map slot)"); }
-        int rc = IMLS_OK;
-        if (d_soa6) {
-            if (hipMemcpyAsync(sl.buf.p, d_soa6, n * 24, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
-                rc = fail(c, IMLS_ERR_DEVICE, "map slot copy");
-        } else {
-            rc = upload_soa6(c, sl.buf, xyz, nrm, n, stride, 0);
+    sl.ghost = false;
+    sl.nk = -1;
+    sl.sorted = false;
+    const bool inc = fifo_incremental(c);
+    if (inc) {
+        for (const auto& e : c->fifo)     // a scan indexed in place (max_queue_size was 1) is not held
+            if (e.ghost && e.n > 0) return fail(c, IMLS_ERR_STATE, "map FIFO holds a scan pushed with max_queue_size 1 (not kept): push again");
+        sl.id = (int)(c->fifo_seq++ % kMaxFifoRuns);
+        // an id is reused after kMaxFifoRuns pushes: if the merged order still holds its old run
+        // (that many pushes without a build), the merged order restarts from the runs
+        if (std::find(c->merged_ids.begin(), c->merged_ids.end(), sl.id) != c->merged_ids.end()) {
+            c->merged_ids.clear();
+            c->m_n = 0;
         }
-        if (rc) { c->slot_pool.push_back(sl.buf); return rc; }
+    }
+    if (n > 0) {
+        int rc = IMLS_OK;
+        const float* raw = d_soa6;
+        if (!d_soa6 || !inc) {            // the incremental index filters a device scan where it lies
+            if (!grow(sl.buf, n * 24)) { c->slot_pool.push_back(sl); return fail(c, IMLS_ERR_DEVICE, "hipMalloc (map slot)"); }
+            if (d_soa6) {
+                if (hipMemcpyAsync(sl.buf.p, d_soa6, n * 24, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+                    rc = fail(c, IMLS_ERR_DEVICE, "map slot copy");
+            } else {
+                rc = upload_soa6(c, sl.buf, xyz, nrm, n, stride, 0);
+            }
+            raw = (const float*)sl.buf.p;
+        }
+        // incremental: this scan's NaN filter now, on the stream (its kept count into the pinned word
+        // of its run id); its run is sorted at the next build
+        if (!rc && inc && (rc = ensure_fifo(c)) == IMLS_OK)
+            rc = filter_async(c->stream, raw, n, sl.fpt, sl.fnr, c->tscratch, nullptr, &c->h_fifo_cnt[sl.id], c->err);
+        if (rc) { c->slot_pool.push_back(sl); return rc; }
     }
     c->fifo.push_back(sl);
     c->map_points += n;
     if (c->fifo.size() > (size_t)std::max(c->P.max_queue_size, 0)) {
         c->map_points -= c->fifo.front().n;
-        if (!c->fifo.front().ghost) c->slot_pool.push_back(c->fifo.front().buf);
+        if (!c->fifo.front().ghost) c->slot_pool.push_back(c->fifo.front());
         c->fifo.pop_front();
     }
+    if (inc) return fifo_set_target(c, n_map);
     for (const auto& e : c->fifo)     // a scan indexed in place (max_queue_size was 1) is not held
         if (e.ghost && e.n > 0) return fail(c, IMLS_ERR_STATE, "map FIFO holds a scan pushed with max_queue_size 1 (not kept): push again");
     const size_t M = c->map_points;
@@ -1350,9 +1571,12 @@ int imls_map_push_device(imls_ctx* c, const float* d_soa6, size_t n, size_t* n_m
 int imls_map_clear(imls_ctx* c) {
     if (!c) return IMLS_ERR_ARG;
     for (auto& e : c->fifo)
-        if (!e.ghost) c->slot_pool.push_back(e.buf);
+        if (!e.ghost) c->slot_pool.push_back(e);
     c->fifo.clear();
     c->map_points = 0;
+    c->merged_ids.clear();
+    c->m_n = 0;
+    c->fq_valid = false;
     return IMLS_OK;
 }
 

@@ -392,6 +392,9 @@ int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf
 
 }  // namespace
 
+void tree_rounds(hipStream_t s, const float4* mpt, int M, int B, int P, int levels, float4* nodes, float* leafbox,
+                 float* rootsA, float* rootsB);
+
 int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& tpt, DevBuf& tnr, DevBuf& mpt,
                       DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* P_out, int* levels_out,
                       std::string& err) {
@@ -413,8 +416,18 @@ int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& t
     float* rootsB = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
     k_gather<<<grid_for(M), kBlock, 0, s>>>((const float4*)tpt.p, (const float4*)tnr.p, (const unsigned*)permbuf.p, M,
                                             (float4*)mpt.p, (float4*)mpt.p + M, (unsigned*)((float4*)mpt.p + 2 * (size_t)M));
-    k_leaf_boxes<<<grid_for(P), kBlock, 0, s>>>((const float4*)mpt.p, M, B, P, leafbox);
-    // bottom-up subtree reduction, 256 boxes per block per launch
+    tree_rounds(s, (const float4*)mpt.p, M, B, P, levels, (float4*)nodes.p, leafbox, rootsA, rootsB);
+    if (hipGetLastError() != hipSuccess) { err = "index build launch failed"; return IMLS_ERR_DEVICE; }
+    *P_out = P;
+    *levels_out = levels;
+    return IMLS_OK;
+}
+
+// leaf boxes of the Morton-ordered points, then the bottom-up subtree reduction, 256 boxes per block
+// per launch (the node records of every internal level)
+void tree_rounds(hipStream_t s, const float4* mpt, int M, int B, int P, int levels, float4* nodes, float* leafbox,
+                 float* rootsA, float* rootsB) {
+    k_leaf_boxes<<<grid_for(P), kBlock, 0, s>>>(mpt, M, B, P, leafbox);
     const float* in = leafbox;
     float* outs[2] = {rootsA, rootsB};
     int count = P, D = levels, which = 0;
@@ -423,16 +436,12 @@ int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& t
         int lg = 0;
         while ((1 << lg) < width) ++lg;
         int blocks = count / width;
-        k_subtree<<<blocks, kBlock, 0, s>>>(in, count, D, (float4*)nodes.p, outs[which]);
+        k_subtree<<<blocks, kBlock, 0, s>>>(in, count, D, nodes, outs[which]);
         in = outs[which];
         which ^= 1;
         count = blocks;
         D -= lg;
     }
-    if (hipGetLastError() != hipSuccess) { err = "index build launch failed"; return IMLS_ERR_DEVICE; }
-    *P_out = P;
-    *levels_out = levels;
-    return IMLS_OK;
 }
 
 int source_order(hipStream_t s, int N, DevBuf& spt, DevBuf& scratch, DevBuf& qperm, std::string& err) {
@@ -714,6 +723,279 @@ int build_batch(hipStream_t s, std::vector<BuildJob>& jobs, DevBuf& scratch, Dev
         }
     }
     if (hipGetLastError() != hipSuccess) { err = "batched index build launch failed"; return IMLS_ERR_DEVICE; }
+    return IMLS_OK;
+}
+
+
+// =============================================================================================
+// Incremental index of the map FIFO (accumulateTargetCloud, laser_odometry.cpp:116-136: the last
+// max_queue_size filtered scans, oldest first; setTargetPointCloud rebuilds libnabo's tree over
+// their concatenation every frame, imls_icp.cpp:80-103).  With a quantisation frame fixed for the
+// FIFO, a scan's Morton keys never change: each scan is sorted ONCE (a run, fifo_run_build), and a
+// registration only merges — the previous merged order minus the evicted scans (a stable
+// compaction), merged with the new runs (merge path, older entries first on equal keys).  That is
+// exactly the stable sort of the concatenation by key, i.e. the order the full build gives under
+// the same quantisation; the records then get their concatenated filtered index (the libnabo tie
+// order, mpt[].w), ipos, the leaf keys and the tree (fifo_index).
+// =============================================================================================
+namespace {
+
+constexpr int kMergeTile = 2048;            // outputs per merge block (12 B each in LDS)
+
+// keys under the fixed quantisation fq; points outside its cube (clamped: still exact, the tree's
+// boxes come from the points) are counted, so the host can re-frame the FIFO at its next build
+__global__ void k_morton_fq(const float4* __restrict__ pt, int n, const float* __restrict__ fq,
+                            unsigned long long* __restrict__ key, unsigned* __restrict__ val, unsigned* __restrict__ clamp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool out = false;
+    if (i < n) {
+        const float4 p = pt[i];
+        key[i] = morton48(p.x, p.y, p.z, fq);
+        val[i] = (unsigned)i;
+        const float sc = fq[3], qmax = 65535.f;
+        const float u = (p.x - fq[0]) * sc, v = (p.y - fq[1]) * sc, w = (p.z - fq[2]) * sc;
+        out = !(u >= 0.f && u <= qmax && v >= 0.f && v <= qmax && w >= 0.f && w <= qmax);
+    }
+    const unsigned long long m = __ballot(out);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(clamp, (unsigned)__popcll(m));
+}
+
+// a run's Morton-ordered records: rpt = (xyz, bits(local filtered index)), rnr
+__global__ void k_run_gather(const float4* __restrict__ pt, const float4* __restrict__ nr, const unsigned* __restrict__ perm,
+                             int n, float4* __restrict__ rpt, float4* __restrict__ rnr) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const unsigned j = perm[k];
+    const float4 p = pt[j];
+    rpt[k] = make_float4(p.x, p.y, p.z, __uint_as_float(j));
+    rnr[k] = nr[j];
+}
+
+// the FIFO quantisation frame: a cube of side 1.5 × the runs' largest bbox extent around their
+// bbox centre (later scans of a moving sensor stay inside; the host re-frames if one does not)
+__global__ void k_fifo_frame(const float* __restrict__ part, int nparts, float* __restrict__ fq) {
+    __shared__ float red[6][kBlock];
+    float r[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int b = threadIdx.x; b < nparts; b += kBlock)
+        for (int d = 0; d < 3; ++d) {
+            r[d] = fminf(r[d], part[b * 6 + d]);
+            r[3 + d] = fmaxf(r[3 + d], part[b * 6 + 3 + d]);
+        }
+    for (int d = 0; d < 6; ++d) red[d][threadIdx.x] = r[d];
+    __syncthreads();
+    for (int st = kBlock / 2; st > 0; st >>= 1) {
+        if (threadIdx.x < st)
+            for (int d = 0; d < 3; ++d) {
+                red[d][threadIdx.x] = fminf(red[d][threadIdx.x], red[d][threadIdx.x + st]);
+                red[3 + d][threadIdx.x] = fmaxf(red[3 + d][threadIdx.x], red[3 + d][threadIdx.x + st]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        float ext = 1e-6f;
+        for (int d = 0; d < 3; ++d) ext = fmaxf(ext, red[3 + d][0] - red[d][0]);
+        const float side = 1.5f * ext;
+        for (int d = 0; d < 3; ++d) fq[d] = 0.5f * (red[d][0] + red[3 + d][0]) - 0.5f * side;
+        fq[3] = 65535.f / side;
+    }
+}
+
+// stable compaction of the merged order: entries whose run id (val >> 27) is live
+__device__ __forceinline__ bool live_entry(unsigned v, unsigned live) { return (live >> (v >> 27)) & 1u; }
+__global__ __launch_bounds__(kBlock) void k_keep_count(const unsigned* __restrict__ val, int n, unsigned live, int* __restrict__ blk) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    __shared__ int wc[kBlock / 64];
+    const unsigned long long m = __ballot(i < n && live_entry(val[i], live));
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int c = 0;
+        for (int k = 0; k < kBlock / 64; ++k) c += wc[k];
+        blk[blockIdx.x] = c;
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_keep_scatter(const unsigned long long* __restrict__ key, const unsigned* __restrict__ val,
+                                                         int n, unsigned live, const int* __restrict__ off,
+                                                         unsigned long long* __restrict__ okey, unsigned* __restrict__ oval) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __shared__ int wc[kBlock / 64];
+    const bool keep = i < n && live_entry(val[i], live);
+    const unsigned long long m = __ballot(keep);
+    if (lane == 0) wc[wv] = __popcll(m);
+    __syncthreads();
+    if (!keep) return;
+    int o = off[blockIdx.x];
+    for (int k = 0; k < wv; ++k) o += wc[k];
+    o += __popcll(m & ((1ull << lane) - 1ull));
+    okey[o] = key[i];
+    oval[o] = val[i];
+}
+
+// merge path: split[t] = entries of A among the first t·kMergeTile outputs of merge(A, B), A first on
+// equal keys (A: the older entries)
+__global__ void k_merge_split(const unsigned long long* __restrict__ a, int na, const unsigned long long* __restrict__ b, int nb,
+                              int tiles, int* __restrict__ split) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > tiles) return;
+    const long long d = std::min((long long)t * kMergeTile, (long long)na + nb);
+    int lo = (int)std::max(0ll, d - nb), hi = (int)std::min<long long>(d, na);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] <= b[d - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    split[t] = lo;
+}
+// one output tile: both input segments in LDS, each entry's output rank = its index in its own
+// segment + the other segment's entries before it (B: strictly smaller keys after A's equal ones).
+// B's values are (bid << 27) | index (a run's entries in its sorted order)
+__global__ __launch_bounds__(kBlock) void k_merge_tile(const unsigned long long* __restrict__ a, const unsigned* __restrict__ av,
+                                                       int na, const unsigned long long* __restrict__ b, unsigned bid, int nb,
+                                                       const int* __restrict__ split, unsigned long long* __restrict__ okey,
+                                                       unsigned* __restrict__ oval) {
+    __shared__ unsigned long long sk[kMergeTile];
+    __shared__ unsigned sv[kMergeTile];
+    const int t = blockIdx.x;
+    const long long d0 = (long long)t * kMergeTile, d1 = std::min(d0 + kMergeTile, (long long)na + nb);
+    const int i0 = split[t], i1 = split[t + 1];
+    const int j0 = (int)(d0 - i0), j1 = (int)(d1 - i1);
+    const int la = i1 - i0, lb = j1 - j0;
+    for (int k = threadIdx.x; k < la; k += kBlock) { sk[k] = a[i0 + k]; sv[k] = av[i0 + k]; }
+    for (int k = threadIdx.x; k < lb; k += kBlock) { sk[la + k] = b[j0 + k]; sv[la + k] = (bid << 27) | (unsigned)(j0 + k); }
+    __syncthreads();
+    for (int k = threadIdx.x; k < la + lb; k += kBlock) {
+        const unsigned long long key = sk[k];
+        int r;
+        if (k < la) {                          // # B keys < key
+            int lo = la, hi = la + lb;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (sk[mid] < key) lo = mid + 1; else hi = mid; }
+            r = k + (lo - la);
+        } else {                               // # A keys <= key
+            int lo = 0, hi = la;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (sk[mid] <= key) lo = mid + 1; else hi = mid; }
+            r = (k - la) + lo;
+        }
+        okey[d0 + r] = key;
+        oval[d0 + r] = sv[k];
+    }
+}
+
+// the index records from the merged order: mpt (xyz, bits(concatenated filtered index)), mnr, ipos,
+// and every B-th key (the leaves' first keys, for the seed search)
+__global__ void k_fifo_gather(const unsigned long long* __restrict__ mkey, const unsigned* __restrict__ mval, int M,
+                              const FifoRun* __restrict__ runs, int B, float4* __restrict__ mpt, float4* __restrict__ mnr,
+                              unsigned* __restrict__ ipos, unsigned long long* __restrict__ lkeys) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= M) return;
+    const unsigned v = mval[k];
+    const FifoRun r = runs[v >> 27];
+    const unsigned pos = v & ((1u << 27) - 1u);
+    const float4 p = r.rpt[pos];
+    const unsigned w = r.off + __float_as_uint(p.w);
+    mpt[k] = make_float4(p.x, p.y, p.z, __uint_as_float(w));
+    mnr[k] = r.rnr[pos];
+    ipos[w] = (unsigned)k;
+    if (k % B == 0) lkeys[k / B] = mkey[k];
+}
+
+}  // namespace
+
+int fifo_frame(hipStream_t s, const std::vector<std::pair<const float4*, int>>& runs, float* fq, DevBuf& scratch,
+               std::string& err) {
+    const int per = 64;                         // bbox partial blocks per run
+    if (!ensure(scratch, runs.size() * per * 24 + 1024, err)) return IMLS_ERR_DEVICE;
+    float* part = (float*)scratch.p;
+    int np = 0;
+    for (const auto& r : runs) {
+        if (r.second <= 0) continue;
+        const int nb = std::min(per, (int)grid_for(r.second));
+        k_bbox_partial<<<nb, kBlock, 0, s>>>(r.first, r.second, part + (size_t)np * 6);
+        np += nb;
+    }
+    if (np == 0) return IMLS_OK;
+    k_fifo_frame<<<1, kBlock, 0, s>>>(part, np, fq);
+    if (hipGetLastError() != hipSuccess) { err = "FIFO frame launch failed"; return IMLS_ERR_DEVICE; }
+    return IMLS_OK;
+}
+
+int fifo_run_build(hipStream_t s, const float4* fpt, const float4* fnr, int n, const float* fq, unsigned* clamp,
+                   DevBuf& run, DevBuf& scratch, std::string& err) {
+    if (n <= 0) return IMLS_OK;
+    if (n >= (1 << 27)) { err = "scan too large for the FIFO index"; return IMLS_ERR_CAPACITY; }
+    size_t cub_bytes = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                       (unsigned*)nullptr, (unsigned*)nullptr, n, 0, 48, s);
+    const size_t need = ((size_t)n * 8 + 255) / 256 * 256 + 2 * (((size_t)n * 4 + 255) / 256 * 256) + ((cub_bytes + 255) / 256) * 256 + 1024;
+    if (!ensure(scratch, need, err) || !ensure(run, fifo_run_bytes(n), err)) return IMLS_ERR_DEVICE;
+    char* p = (char*)scratch.p;
+    unsigned long long* k0 = carve<unsigned long long>(p, n);
+    unsigned* v0 = carve<unsigned>(p, n);
+    unsigned* v1 = carve<unsigned>(p, n);
+    void* cub_tmp = carve<char>(p, cub_bytes);
+    unsigned long long* rkey = fifo_run_keys(run.p, n);
+    k_morton_fq<<<grid_for(n), kBlock, 0, s>>>(fpt, n, fq, k0, v0, clamp);
+    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, rkey, v0, v1, n, 0, 48, s);
+    k_run_gather<<<grid_for(n), kBlock, 0, s>>>(fpt, fnr, v1, n, fifo_run_pts(run.p, n), fifo_run_nrm(run.p, n));
+    if (hipGetLastError() != hipSuccess) { err = "FIFO run build launch failed"; return IMLS_ERR_DEVICE; }
+    return IMLS_OK;
+}
+
+int fifo_keep(hipStream_t s, const unsigned long long* key, const unsigned* val, int n, unsigned live,
+              unsigned long long* okey, unsigned* oval, DevBuf& scratch, std::string& err) {
+    if (n <= 0) return IMLS_OK;
+    const int nb = (int)grid_for(n);
+    size_t cub_bytes = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (int*)nullptr, (int*)nullptr, nb, s);
+    if (!ensure(scratch, 2 * (((size_t)nb * 4 + 255) / 256 * 256) + cub_bytes + 1024, err)) return IMLS_ERR_DEVICE;
+    char* p = (char*)scratch.p;
+    int* blk = carve<int>(p, nb);
+    int* off = carve<int>(p, nb);
+    void* cub_tmp = carve<char>(p, cub_bytes);
+    k_keep_count<<<nb, kBlock, 0, s>>>(val, n, live, blk);
+    hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, blk, off, nb, s);
+    k_keep_scatter<<<nb, kBlock, 0, s>>>(key, val, n, live, off, okey, oval);
+    if (hipGetLastError() != hipSuccess) { err = "FIFO compaction launch failed"; return IMLS_ERR_DEVICE; }
+    return IMLS_OK;
+}
+
+int fifo_merge(hipStream_t s, const unsigned long long* a, const unsigned* av, int na, const unsigned long long* b,
+               unsigned bid, int nb, unsigned long long* okey, unsigned* oval, DevBuf& scratch, std::string& err) {
+    const int tiles = (int)(((long long)na + nb + kMergeTile - 1) / kMergeTile);
+    if (tiles == 0) return IMLS_OK;
+    if (!ensure(scratch, (size_t)(tiles + 1) * 4 + 256, err)) return IMLS_ERR_DEVICE;
+    int* split = (int*)scratch.p;
+    k_merge_split<<<grid_for(tiles + 1), kBlock, 0, s>>>(a, na, b, nb, tiles, split);
+    k_merge_tile<<<tiles, kBlock, 0, s>>>(a, av, na, b, bid, nb, split, okey, oval);
+    if (hipGetLastError() != hipSuccess) { err = "FIFO merge launch failed"; return IMLS_ERR_DEVICE; }
+    return IMLS_OK;
+}
+
+int fifo_index(hipStream_t s, const unsigned long long* mkey, const unsigned* mval, int M, const FifoRun* runs_dev,
+               const float* fq, int B, DevBuf& lkeys, DevBuf& mpt, DevBuf& nodes, DevBuf& treescratch, int* P_out,
+               int* levels_out, std::string& err) {
+    if (M <= 0) { *P_out = 0; *levels_out = 0; return IMLS_OK; }
+    const int L = (M + B - 1) / B;
+    int P = 1, levels = 0;
+    while (P < L) { P <<= 1; ++levels; }
+    if (levels > kStackDepth - 1) { err = "tree too deep for the traversal stack"; return IMLS_ERR_CAPACITY; }
+    const size_t need = ((size_t)P * 24 + 255) / 256 * 256 + 2 * (((size_t)P / kBlock + 1) * 24 + 256) + 1024;
+    if (!ensure(treescratch, need, err) || !ensure(mpt, (size_t)M * 36 + 64, err) || !ensure(nodes, (size_t)(P + 1) * 48, err) ||
+        !ensure(lkeys, (size_t)L * 8 + 16, err))
+        return IMLS_ERR_DEVICE;
+    char* p = (char*)treescratch.p;
+    float* leafbox = carve<float>(p, (size_t)P * 6);
+    float* rootsA = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
+    float* rootsB = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
+    float4* mp = (float4*)mpt.p;
+    k_fifo_gather<<<grid_for(M), kBlock, 0, s>>>(mkey, mval, M, runs_dev, B, mp, mp + M, (unsigned*)(mp + 2 * (size_t)M),
+                                                 (unsigned long long*)lkeys.p);
+    // the quantisation after the leaf keys (TreeView::qparams), as morton_perm places it
+    (void)hipMemcpyAsync((unsigned long long*)lkeys.p + L, fq, 16, hipMemcpyDeviceToDevice, s);
+    tree_rounds(s, mp, M, B, P, levels, (float4*)nodes.p, leafbox, rootsA, rootsB);
+    if (hipGetLastError() != hipSuccess) { err = "FIFO index launch failed"; return IMLS_ERR_DEVICE; }
+    *P_out = P;
+    *levels_out = levels;
     return IMLS_OK;
 }
 

@@ -244,6 +244,38 @@ int build_batch(hipStream_t s, std::vector<BuildJob>& jobs, DevBuf& scratch, Dev
                 size_t h_table_bytes, std::string& err);
 size_t build_job_bytes();              // bytes per job of the device job table
 
+// index.hip — incremental index of the map FIFO (api.hip map_push / finish_target).  A run = one
+// scan's filtered points Morton-sorted under the FIFO's fixed quantisation: [n] sorted keys, [n]
+// records (xyz, bits(local filtered index)), [n] normals, 256-B aligned parts of one buffer.
+struct FifoRun {
+    const float4* rpt;
+    const float4* rnr;
+    unsigned off;                      // concatenated filtered index of the run's first point
+    unsigned pad;
+};
+constexpr int kMaxFifoRuns = 32;       // run ids (5 bits of a merged entry's value; 27 bits of position)
+inline size_t fifo_part(size_t bytes) { return (bytes + 255) / 256 * 256; }
+inline size_t fifo_run_bytes(int n) { return fifo_part((size_t)n * 8) + 2 * fifo_part((size_t)n * 16); }
+inline unsigned long long* fifo_run_keys(void* run, int) { return (unsigned long long*)run; }
+inline float4* fifo_run_pts(void* run, int n) { return (float4*)((char*)run + fifo_part((size_t)n * 8)); }
+inline float4* fifo_run_nrm(void* run, int n) { return (float4*)((char*)run + fifo_part((size_t)n * 8) + fifo_part((size_t)n * 16)); }
+// the FIFO's quantisation frame (fq: lo xyz, scale) from the bboxes of filtered point sets
+int fifo_frame(hipStream_t s, const std::vector<std::pair<const float4*, int>>& runs, float* fq, DevBuf& scratch,
+               std::string& err);
+// one run from n filtered points (clamp: device counter of points outside fq's cube)
+int fifo_run_build(hipStream_t s, const float4* fpt, const float4* fnr, int n, const float* fq, unsigned* clamp,
+                   DevBuf& run, DevBuf& scratch, std::string& err);
+// stable compaction of a merged order to the entries of live runs (bit id of `live`)
+int fifo_keep(hipStream_t s, const unsigned long long* key, const unsigned* val, int n, unsigned live,
+              unsigned long long* okey, unsigned* oval, DevBuf& scratch, std::string& err);
+// merge(A, run B) by key, A first on equal keys; B's values become (bid << 27) | index
+int fifo_merge(hipStream_t s, const unsigned long long* a, const unsigned* av, int na, const unsigned long long* b,
+               unsigned bid, int nb, unsigned long long* okey, unsigned* oval, DevBuf& scratch, std::string& err);
+// the target index from the merged order (records, ipos, leaf keys + fq, leaf boxes, tree)
+int fifo_index(hipStream_t s, const unsigned long long* mkey, const unsigned* mval, int M, const FifoRun* runs_dev,
+               const float* fq, int B, DevBuf& lkeys, DevBuf& mpt, DevBuf& nodes, DevBuf& treescratch, int* P_out,
+               int* levels_out, std::string& err);
+
 // project.hip
 // k_knn_wave → k_finish (+ the exact k_project_lane fallback for uncertified queries); lane_mode
 // runs every query through k_project_lane.  partial1 receives project_blocks(N) slabs.
@@ -255,7 +287,7 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
 // delta: last pose increment (read when use_prev); lists: [KL][N] positions + [N] worst keys,
 // kept across ICP iterations (temporal seed); marks: 3 events recorded before k_knn_wave, between
 // it and k_finish, and after k_finish (timing), or null
-constexpr int kMaxKL = 36;
+constexpr int kMaxKL = 46;       // list entries per query at most (the lone-frame path: K + 12 for K ≤ 32, capped)
 // per-query reference position + list guarantee (float4 xref[N]) and the key the list's answer
 // relied on (float nref[N]), after the [kMaxKL+1][N] list block
 inline float4* xref_of(int* lists, int N) {

@@ -220,6 +220,9 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
         for (int j = 0; j < CAP; ++j) dsel = (j == target) ? ld[j] : dsel;
     }
     const double hmax = sqrt(dsel) / 3;
+    // exp(−‖x−p‖² / h / h) (imls_icp.cpp:470) with one reciprocal per query instead of two divisions
+    // per neighbour: w moves by ≤ 2 ulp, y (stored as float) almost never (the 1e-5 y contract)
+    const double ih2 = 1.0 / (hmax * hmax);
     double wsum = 0.0, psum = 0.0;
 #pragma unroll
     for (int j = 0; j < CAP; ++j) {
@@ -231,7 +234,7 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
             double dn = dx * dx;
             dn = dn + dy * dy;
             dn = dn + dz * dz;
-            const double w = exp(-dn / hmax / hmax);
+            const double w = exp(-dn * ih2);
             double pr = (w * dx) * (double)qn.x;
             pr = pr + (w * dy) * (double)qn.y;
             pr = pr + (w * dz) * (double)qn.z;
@@ -1605,13 +1608,14 @@ __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restri
             } else {
                 const int lt = lane_of_rank(nacc - 1);          // Q3: L[|S| − 1]
                 const double hmax = sqrt(rl_f64(ed, lt)) / 3;
+                const double ih2 = 1.0 / (hmax * hmax);          // as finish_query
                 double w = 0.0, pr = 0.0;
                 if (ok) {
                     const double dx = xd[0] - (double)q.x, dy = xd[1] - (double)q.y, dz = xd[2] - (double)q.z;
                     double dn = dx * dx;
                     dn = dn + dy * dy;
                     dn = dn + dz * dz;
-                    w = exp(-dn / hmax / hmax);
+                    w = exp(-dn * ih2);
                     pr = (w * dx) * (double)qn.x;
                     pr = pr + (w * dy) * (double)qn.y;
                     pr = pr + (w * dz) * (double)qn.z;
@@ -2001,6 +2005,16 @@ void launch_lane(hipStream_t s, int blocks, const TreeView& t, const float4* spt
 }
 
 
+// The lone small frame's list (k_knn_qwave_f): entry k in lane k, so a longer list costs the wave no
+// registers — K + 12 entries instead of K + 2 give the Verlet certificate a longer skin (√W − √need:
+// the 32nd vs the 20th neighbour's distance instead of the 22nd), so fewer steady-iteration queries
+// re-traverse (the slowest 2 % set each launch's length).  The list is read only by the same kernel.
+#ifndef IMLS_LONE_EXTRA
+#define IMLS_LONE_EXTRA 10
+#endif
+template <int KL>
+constexpr int lone_kl() { return KL + IMLS_LONE_EXTRA <= kMaxKL ? KL + IMLS_LONE_EXTRA : kMaxKL; }
+
 template <int KL>
 void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qperm,
                  int N, const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd, float4* cn,
@@ -2015,9 +2029,9 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
     // queries, then k_finish
     const bool fused = fused_stage(kp, N);
     if (fused)
-        k_knn_qwave_f<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(
-            t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, stats,
-            QFinishArgs{snr, cs, cd, cn, tr});
+        k_knn_qwave_f<lone_kl<KL>()><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(
+            t, spt, qperm, N, pose, done, kp, delta, lists, reinterpret_cast<float*>(lists + (size_t)lone_kl<KL>() * N), xref,
+            nref, use_prev, stats, QFinishArgs{snr, cs, cd, cn, tr});
     else if (use_qwave(kp, N))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
                                                                                           delta, lists, wlist, xref, nref, use_prev, stats);

@@ -547,10 +547,15 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
 #pragma unroll
     for (int k = 0; k < kSmallPer; ++k) {
         const int r = t + k * kSmallBlock;
-        rs[k] = r < N ? rows.cs[r] : make_float4(0.f, 0.f, 0.f, 0.f);
+        // the three loads issue together (y and n are read whatever the valid flag: a rejected row's
+        // are stale and replaced by zeros below — one memory round trip instead of two)
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        rs[k] = r < N ? rows.cs[r] : z4;
+        float4 d4 = r < N ? rows.cd[r] : z4;
+        rn[k] = r < N ? rows.cn[r] : z4;
         const bool v = r < N && rs[k].w != 0.f;
-        const float4 d4 = v ? rows.cd[r] : make_float4(0.f, 0.f, 0.f, 0.f);
-        rn[k] = v ? rows.cn[r] : make_float4(0.f, 0.f, 0.f, 0.f);
+        d4 = v ? d4 : z4;
+        rn[k] = v ? rn[k] : z4;
         rb[k] = small_b(rs[k], d4, rn[k]);
     }
     if (stopped) return;              // block-uniform, before any LDS write or barrier

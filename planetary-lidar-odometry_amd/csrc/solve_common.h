@@ -217,8 +217,9 @@ __device__ inline void delta_from_x(const double x[6], double D[16]) {
     sq = sq + wz * wz;
     const double ang = sqrt(sq);
     double ax = 0, ay = 0, az = 0;
-    if (sq > 0) { const double nr = sqrt(sq); ax = wx / nr; ay = wy / nr; az = wz / nr; }
-    const double s = sin(ang), c = cos(ang);
+    if (sq > 0) { ax = wx / ang; ay = wy / ang; az = wz / ang; }   // (ang = ‖ω‖: the same root)
+    double s, c;
+    sincos(ang, &s, &c);
     const double sx = s * ax, sy = s * ay, sz = s * az;
     const double c1x = (1 - c) * ax, c1y = (1 - c) * ay, c1z = (1 - c) * az;
     double R[9];
@@ -233,8 +234,10 @@ __device__ inline void delta_from_x(const double x[6], double D[16]) {
         const double cof[9] = {a[4] * a[8] - a[5] * a[7], a[5] * a[6] - a[3] * a[8], a[3] * a[7] - a[4] * a[6],
                                a[2] * a[7] - a[1] * a[8], a[0] * a[8] - a[2] * a[6], a[1] * a[6] - a[0] * a[7],
                                a[1] * a[5] - a[2] * a[4], a[2] * a[3] - a[0] * a[5], a[0] * a[4] - a[1] * a[3]};
+        // one division per step (its reciprocal scales the cofactors; round 5: was nine)
+        const double rdet = 1.0 / det;
         double maxd = 0, n[9];
-        for (int k = 0; k < 9; ++k) { n[k] = 0.5 * (a[k] + cof[k] / det); maxd = fmax(maxd, fabs(n[k] - a[k])); }
+        for (int k = 0; k < 9; ++k) { n[k] = 0.5 * (a[k] + cof[k] * rdet); maxd = fmax(maxd, fabs(n[k] - a[k])); }
         for (int k = 0; k < 9; ++k) R[k] = n[k];
         if (maxd < 1e-16) break;
     }
