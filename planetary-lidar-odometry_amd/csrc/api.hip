@@ -22,6 +22,12 @@
 
 #include "internal.h"
 
+// host → device copies of uploads on a per-context upload stream (upload_soa6); 0: on the context's
+// stream, behind its running registrations (the round-4 behaviour, kept for same-box A/B builds)
+#ifndef IMLS_UPLOAD_STREAM
+#define IMLS_UPLOAD_STREAM 1
+#endif
+
 using namespace imlsgpu;
 
 constexpr int kTimingKinds = 8;   // projection, index, solve chain, k_knn_wave, k_finish, k_ring_pca, k_major_avg, front end
@@ -134,6 +140,10 @@ struct imls_ctx {
     float* h_stage[2] = {nullptr, nullptr};
     size_t stage_cap[2] = {0, 0};
     hipEvent_t ev_stage[2] = {nullptr, nullptr};
+    // an upload of that kind whose NaN filter has not been consumed by a build yet (it may still be
+    // reading its device buffer): the next upload's copy is then ordered behind it
+    bool stage_pending[2] = {false, false};
+    hipStream_t ustream = nullptr;        // host → device copies of uploads (upload_soa6)
     // correspondences + solver state
     DevBuf cs, cd, cn, solve_mem, trace_mem, stats, rows_d, pose_tmp;
     DevBuf ransac_mem, rng;               // RANSAC scratch + the glibc rand() state (34 words)
@@ -303,11 +313,11 @@ int ensure_solve(imls_ctx* c, int N) {
     if (c->st_N >= N && c->st.trace) return IMLS_OK;
     size_t n = (size_t)std::max(N, 1);
     n += n / 4 + 64;                      // headroom (see grow): the next frames' N differ a little
-    // deferred (uncertified) queries: k_finish block b writes its count to word b and its queries,
-    // in slot order, to the region fb_off + b·256 (project.hip finish_body, k_project_lane)
-    const size_t nfb = (n + 255) / 256;
+    // deferred (uncertified) queries: k_finish's wave w writes its count to word w and its queries,
+    // in slot order, to the region fb_off + w·64 (project.hip finish_body, k_project_lane)
+    const size_t nfb = (n + 63) / 64;
     c->fb_off = (nfb + 63) / 64 * 64;
-    if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, (c->fb_off + nfb * 256) * 4))
+    if (!grow(c->cs, n * 16) || !grow(c->cd, n * 16) || !grow(c->cn, n * 16) || !grow(c->fb, (c->fb_off + nfb * 64) * 4))
         return fail(c, IMLS_ERR_DEVICE, "hipMalloc (correspondences)");
     if (!grow(c->prevnn, prevnn_bytes((int)n))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (prevnn)");
     if (!grow(c->tvn, n * kTvBytesPerQuery)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (tvn)");
@@ -686,9 +696,23 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
     };
     PackPool::get().run(n, n / 8192 + 1, pack);
     if (!grow(dst, 6 * n * 4)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (upload)");
-    if (hipMemcpyAsync(dst.p, h, 6 * n * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-        hipEventRecord(c->ev_stage[which], c->stream) != hipSuccess)
+    // the copy runs on the context's upload stream, not behind its running registrations: the
+    // buffer's previous reader — the NaN filter of the last upload of this kind — has finished once a
+    // build consumed its kept count (stage_pending false), else the copy is ordered after it on the
+    // context's stream.  The context's stream waits for the copy (its filter reads the buffer).
+    hipStream_t us = c->stream;
+#if IMLS_UPLOAD_STREAM
+    if (!c->stage_pending[which]) {
+        if (!c->ustream && hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess)
+            return fail(c, IMLS_ERR_DEVICE, "hipStreamCreate (upload)");
+        us = c->ustream;
+    }
+#endif
+    if (hipMemcpyAsync(dst.p, h, 6 * n * 4, hipMemcpyHostToDevice, us) != hipSuccess ||
+        hipEventRecord(c->ev_stage[which], us) != hipSuccess ||
+        (us != c->stream && hipStreamWaitEvent(c->stream, c->ev_stage[which], 0) != hipSuccess))
         return fail(c, IMLS_ERR_DEVICE, "upload failed");
+    c->stage_pending[which] = true;
     return IMLS_OK;
 }
 
@@ -709,6 +733,7 @@ int finish_target(imls_ctx* c) {
         if (hipEventRecord(c->ev_tgt, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "event record");
     }
     if (hipEventSynchronize(c->ev_tgt) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "target filter failed");
+    c->stage_pending[0] = false;
     c->M = c->h_cnt[0];
     int rc = build_target_tree(c->stream, c->M, c->B, c->lkeys, c->tpt, c->tnr, c->mpt, c->nodes, c->tscratch,
                                c->treescratch, c->permbuf, &c->Pl, &c->levels, c->err);
@@ -734,6 +759,7 @@ int finish_source(imls_ctx* c) {
         if (hipEventRecord(c->ev_src, c->stream) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "event record");
     }
     if (hipEventSynchronize(c->ev_src) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "source filter failed");
+    c->stage_pending[1] = false;
     c->N = c->h_cnt[1];
     c->has_source = false;
     if (int rc = source_order(c->stream, c->N, c->spt, c->sscratch, c->qperm, c->err)) return rc;
@@ -840,6 +866,7 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused, HostS
         if (c->tgt_pending) {
             c->tgt_pending = false;
             if (hipEventSynchronize(c->ev_tgt) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "target filter failed");
+            c->stage_pending[0] = false;
             c->M = c->h_cnt[0];
             c->Pl = c->levels = 0;
             c->has_target = c->M > 0;
@@ -860,6 +887,7 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused, HostS
         if (c->src_pending) {
             c->src_pending = false;
             if (hipEventSynchronize(c->ev_src) != hipSuccess) return fail(L, IMLS_ERR_DEVICE, "source filter failed");
+            c->stage_pending[1] = false;
             c->N = c->h_cnt[1];
             c->has_source = c->N > 0;
             c->src_kept_out = nullptr;
@@ -1156,6 +1184,7 @@ void imls_destroy(imls_ctx* c) {
     if (c->ftable.p) (void)hipFree(c->ftable.p);
     if (c->h_ftable) (void)hipHostFree(c->h_ftable);
     if (c->ev_build) (void)hipEventDestroy(c->ev_build);
+    if (c->ustream) (void)hipStreamSynchronize(c->ustream), (void)hipStreamDestroy(c->ustream);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -1364,6 +1393,7 @@ int fifo_set_target(imls_ctx* c, size_t* n_map) {
 // new ones after the kept ones: the FIFO is oldest first), the index from it.
 int fifo_build(imls_ctx* c) {
     if (hipEventSynchronize(c->ev_tgt) != hipSuccess) return fail(c, IMLS_ERR_DEVICE, "map filter failed");
+    c->stage_pending[0] = false;
     hipStream_t s = c->stream;
     size_t M = 0;
     for (auto& e : c->fifo) {

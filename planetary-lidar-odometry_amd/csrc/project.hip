@@ -1321,7 +1321,13 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
         }
         if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_OPT_FORCE_FALLBACK)
         if (!cert) {
-            cat = -3;                                         // deferred to k_project_lane (listed below)
+            // deferred to k_project_lane: listed in slot order in this wave's own region
+            // fb_list[w·64, …) (its count in fb_count[w], below) — no atomics, so the fallback's rows
+            // (and its slab sums) do not depend on timing
+            const unsigned long long dm = __ballot(true);     // the wave's deferring lanes
+            const int lanei = tid & 63;
+            fb_list[((size_t)bx * kWaveBlock + (tid & ~63)) + __popcll(dm & ((1ull << lanei) - 1ull))] = (unsigned)i;
+            cat = -3;
             // the list's own bound for the exact re-run: its points are real, so the exact answer
             // needs no point beyond max(K-th listed key within r, listed NN-1) (r² when either is
             // missing) — the fallback's search ball, instead of the whole radius r
@@ -1339,23 +1345,11 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
         if (i1 >= 0) atomicAdd(&rej_s[IMLS_NUM_REJ + 1], 1u);
     }
     if (cat == -3) atomicAdd(&rej_s[IMLS_NUM_REJ + 2], 1u);
-    // the deferred queries of this block, listed in slot order in its own region
-    // fb_list[bx·256, …) with their count in fb_count[bx] — no atomics: k_project_lane walks the
-    // regions in block order, so the fallback's rows (and its slab sums) do not depend on timing
     {
-        __shared__ unsigned wcnt[kWaveBlock / 64];
         const unsigned long long dm = __ballot(cat == -3);
-        if ((tid & 63) == 0) wcnt[tid >> 6] = (unsigned)__popcll(dm);
-        __syncthreads();
-        unsigned before = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < kWaveBlock / 64; ++w) {
-            before += w < (tid >> 6) ? wcnt[w] : 0u;
-            total += wcnt[w];
-        }
-        if (cat == -3) fb_list[(size_t)bx * kWaveBlock + before + __popcll(dm & ((1ull << (tid & 63)) - 1ull))] = (unsigned)i;
-        if (tid == 0) fb_count[bx] = total;
+        if ((tid & 63) == 0) fb_count[bx * (kWaveBlock / 64) + (tid >> 6)] = (unsigned)__popcll(dm);
     }
+    __syncthreads();                  // rej_s complete (the slab reduction below may be skipped)
     // pass-1 slabs only for the grid solve chain (frames of ≤ kSmallRows rows: k_solve_small forms
     // pass 1 from the rows); N is block-uniform
     if (N > kSmallRows) {
@@ -1677,8 +1671,8 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
     // nlog logical blocks (one pass-1 slab each) taken by the physical blocks in turn: the slabs do
     // not depend on the physical grid.  A logical block lb works in rounds of kProjBlock queries:
     // every query (lane mode, qlist null) — rows lb·128 + k·nlog·128; deferred queries — the regions
-    // k_finish blocks lb, lb + nlog, … listed (qlist[b·256 …], qcount[b] entries each), in block order
-    const int nfb = (N + kWaveBlock - 1) / kWaveBlock;
+    // k_finish's waves lb, lb + nlog, … listed (qlist[w·64 …], qcount[w] entries each), in wave order
+    const int nfb = (N + 63) / 64;
     for (int lb = blockIdx.x; lb < nlog; lb += gridDim.x) {
     double acc_out = 0.0;   // thread tid < 28 accumulates its normal-equation term over rounds
     int fbk = lb, off = 0, base = lb * kProjBlock;
@@ -1690,7 +1684,7 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
             if (fbk >= nfb) break;
             q = off + tid;
             total = (int)qcount[fbk];
-            at = (size_t)fbk * kWaveBlock + q;
+            at = (size_t)fbk * 64 + q;
             off += kProjBlock;
         } else {
             if (base >= N) break;

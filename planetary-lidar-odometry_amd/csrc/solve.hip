@@ -375,9 +375,10 @@ __device__ void final_block(const Rows& rows, int N, SolveState st, imls_iter_tr
         for (int k = 0; k < kNormEq; ++k) accA[k] += partial2[(size_t)q * kNormEq + k];
     block_sum28<NT>(accA, red, out);
     FSTAMP(3);
-    if (threadIdx.x != 0) return;
+    if (threadIdx.x >= 64) return;
     double x[6], D[16];
-    solve6(out, x);
+    solve6_wave(out, x);             // wave 0 (solve_common.h)
+    if (threadIdx.x != 0) return;
     FSTAMP(4);
     delta_from_x(x, D);
     FSTAMP(5);
@@ -547,15 +548,10 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
 #pragma unroll
     for (int k = 0; k < kSmallPer; ++k) {
         const int r = t + k * kSmallBlock;
-        // the three loads issue together (y and n are read whatever the valid flag: a rejected row's
-        // are stale and replaced by zeros below — one memory round trip instead of two)
-        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        rs[k] = r < N ? rows.cs[r] : z4;
-        float4 d4 = r < N ? rows.cd[r] : z4;
-        rn[k] = r < N ? rows.cn[r] : z4;
+        rs[k] = r < N ? rows.cs[r] : make_float4(0.f, 0.f, 0.f, 0.f);
         const bool v = r < N && rs[k].w != 0.f;
-        d4 = v ? d4 : z4;
-        rn[k] = v ? rn[k] : z4;
+        const float4 d4 = v ? rows.cd[r] : make_float4(0.f, 0.f, 0.f, 0.f);
+        rn[k] = v ? rows.cn[r] : make_float4(0.f, 0.f, 0.f, 0.f);
         rb[k] = small_b(rs[k], d4, rn[k]);
     }
     if (stopped) return;              // block-uniform, before any LDS write or barrier
@@ -570,22 +566,26 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     block_sum28<kSmallBlock>(loc, red, acc);
     DBG_STAMP(0);
     const double nvalid = acc[27];
-    if (t == 0) {
+    if (t < 64) {                     // wave 0: the 6×6 solve by its 64 lanes (solve6_wave)
         double x[6];
         if (update_pose && nvalid < (double)kp.correspond_number) {   // laser_odometry.cpp:570-576
-            *st.status = IMLS_FRAME_TOO_FEW;
-            *st.done = 1;
-            if (tr) tr->n_valid = (unsigned long long)nvalid;
-            stop = 1;
-        } else {
-            solve6(acc, x);
-            if (weighted) {
-                double D[16];
-                delta_from_x(x, D);
-                finish_iteration(st, tr, D, nvalid, nvalid, update_pose, kp);
+            if (t == 0) {
+                *st.status = IMLS_FRAME_TOO_FEW;
+                *st.done = 1;
+                if (tr) tr->n_valid = (unsigned long long)nvalid;
                 stop = 1;
             }
-            for (int k = 0; k < 6; ++k) xs[k] = x[k];
+        } else {
+            solve6_wave(acc, x);
+            if (t == 0) {
+                if (weighted) {
+                    double D[16];
+                    delta_from_x(x, D);
+                    finish_iteration(st, tr, D, nvalid, nvalid, update_pose, kp);
+                    stop = 1;
+                }
+                for (int k = 0; k < 6; ++k) xs[k] = x[k];
+            }
         }
     }
     __syncthreads();
@@ -697,9 +697,10 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     }
     block_sum28<kSmallBlock>(loc, red, acc);
     DBG_STAMP(4);
-    if (t != 0) return;
+    if (t >= 64) return;
     double x[6], D[16];
-    solve6(acc, x);
+    solve6_wave(acc, x);
+    if (t != 0) return;
     DBG_STAMP(5);
     delta_from_x(x, D);
     DBG_STAMP(6);

@@ -208,6 +208,101 @@ __device__ inline int solve6(const double* ne, double x[6]) {
     return rank;
 }
 
+// solve6 by one whole wave (all 64 lanes call it; every lane returns the same x and rank), element
+// (r, c) of the 6×6 system in lane 6r + c and g[r] in lane 36 + r: a pivot's row / column swap is one
+// lane permute, its column scale and trailing update one VALU operation each — where solve6's one
+// thread spends ~700 predicated selects on the swaps.  Every element sees exactly solve6's
+// operations in solve6's order (the update's product A[r][j]·A[c][j] is commutative, the upper
+// triangle is solve6's mirror copy), and the substitutions run on the same values, so x is solve6's
+// bit for bit.
+__device__ __forceinline__ double lane_f64(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl((int)(unsigned)(b & 0xffffffffll), src, 64);
+    const int hi = __shfl((int)(unsigned)((unsigned long long)b >> 32), src, 64);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double uni_f64(double v, int src) {   // wave-uniform read of lane src
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), src);
+    const int hi = __builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), src);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ int solve6_wave(const double* ne, double x[6]) {
+    const int lane = threadIdx.x & 63;
+    const int r = lane < 36 ? lane / 6 : (lane < 42 ? lane - 36 : 0), c = lane < 36 ? lane % 6 : 0;
+    const bool mat = lane < 36, rhs = lane >= 36 && lane < 42;
+    double a = 0.0;
+    if (mat) {
+        const int lo = r < c ? r : c, hi = r < c ? c : r;
+        a = ne[lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];       // upper-triangle row-major index of (lo, hi)
+    } else if (rhs) {
+        a = ne[21 + r];
+    }
+    int perm[6] = {0, 1, 2, 3, 4, 5};
+    const double eps = DBL_EPSILON;
+    double maxpiv = 0.0;
+    int rank = 6;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        int p = j;
+        double best = uni_f64(a, 7 * j);
+#pragma unroll
+        for (int q = j + 1; q < 6; ++q) {
+            const double dq = uni_f64(a, 7 * q);
+            if (dq > best) { best = dq; p = q; }
+        }
+        if (p != j) {                                           // rows and columns j ↔ p
+            const int sr = r == j ? p : (r == p ? j : r), sc = c == j ? p : (c == p ? j : c);
+            a = lane_f64(a, mat ? 6 * sr + sc : (rhs ? 36 + sr : lane));
+#pragma unroll
+            for (int q = j + 1; q < 6; ++q)           // (constant indices: perm stays in registers)
+                if (q == p) { const int t = perm[j]; perm[j] = perm[q]; perm[q] = t; }
+        }
+        const double d = uni_f64(a, 7 * j);
+        const double rkk = d > 0 ? sqrt(d) : 0.0;
+        if (rkk > maxpiv) maxpiv = rkk;
+        if (!(rkk > eps * 6.0 * maxpiv) || !(d > 0)) {
+            rank = j;
+            break;
+        }
+        const double inv = 1.0 / rkk;
+        if (lane == 7 * j) a = rkk;
+        if (mat && c == j && r > j) a = a * inv;
+        const double Lr = lane_f64(a, 6 * r + j), Lc = lane_f64(a, 6 * c + j);
+        if (mat && r > j && c > j) a = a - Lr * Lc;
+    }
+    // the substitutions of solve6 on the factor's values (wave-uniform)
+    double y[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        if (i < rank) {
+            double s = uni_f64(a, 36 + i);
+#pragma unroll
+            for (int k = 0; k < i; ++k) s -= uni_f64(a, 6 * i + k) * y[k];
+            y[i] = s / uni_f64(a, 7 * i);
+        }
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        if (i < rank) {
+            double s = y[i];
+#pragma unroll
+            for (int k = i + 1; k < 6; ++k)
+                if (k < rank) s -= uni_f64(a, 6 * k + i) * y[k];
+            y[i] = s / uni_f64(a, 7 * i);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+            if (i < rank && perm[i] == k) v = y[i];
+        x[k] = v;
+    }
+    return rank;
+}
+
 // Δ from x (solver.cpp:140-163): R = AngleAxis(‖ω‖, ω̂) (Eigen AngleAxis::toRotationMatrix), then
 // the JacobiSVD U·Vᵀ re-orthonormalisation as the polar factor (Newton iteration).
 __device__ inline void delta_from_x(const double x[6], double D[16]) {
@@ -218,8 +313,7 @@ __device__ inline void delta_from_x(const double x[6], double D[16]) {
     const double ang = sqrt(sq);
     double ax = 0, ay = 0, az = 0;
     if (sq > 0) { ax = wx / ang; ay = wy / ang; az = wz / ang; }   // (ang = ‖ω‖: the same root)
-    double s, c;
-    sincos(ang, &s, &c);
+    const double s = sin(ang), c = cos(ang);
     const double sx = s * ax, sy = s * ay, sz = s * az;
     const double c1x = (1 - c) * ax, c1y = (1 - c) * ay, c1z = (1 - c) * az;
     double R[9];
@@ -295,16 +389,19 @@ __device__ void solve_first_block(const double* __restrict__ partial, int blocks
         for (int k = 0; k < kNormEq; ++k) loc[k] += partial[(size_t)b * kNormEq + k];
     if (t < 2) st.cand_count[t] = 0u;
     block_sum28<NT>(loc, red, acc);
-    if (t != 0) return;
+    if (t >= 64) return;
     const double nvalid = acc[27];
     if (update_pose && nvalid < (double)kp.correspond_number) {
-        *st.status = IMLS_FRAME_TOO_FEW;
-        *st.done = 1;
-        if (tr) tr->n_valid = (unsigned long long)nvalid;
+        if (t == 0) {
+            *st.status = IMLS_FRAME_TOO_FEW;
+            *st.done = 1;
+            if (tr) tr->n_valid = (unsigned long long)nvalid;
+        }
         return;
     }
     double x[6];
-    solve6(acc, x);
+    solve6_wave(acc, x);              // wave 0
+    if (t != 0) return;
     if (weighted) {
         double D[16];
         delta_from_x(x, D);
