@@ -212,12 +212,33 @@ int fail(imls_ctx* c, int code, const std::string& m) {
 // work in flight and the host).
 bool grow(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes) return true;
-    if (b.p) (void)hipFree(b.p);
+    // work already enqueued on non-blocking streams may still read the old buffer: let it finish
+    // before the memory is released (a free under a pending kernel faults the card)
+    if (b.p) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(b.p);
+    }
     b.p = nullptr;
     b.bytes = 0;
     const size_t want = bytes + bytes / 4 + 256;
     if (hipMalloc(&b.p, want) != hipSuccess) return false;
     b.bytes = want;
+    return true;
+}
+
+// grow keeping the first `keep` bytes (copied on stream s; the old buffer is freed once s is past it)
+bool grow_keep(DevBuf& b, size_t bytes, size_t keep, hipStream_t s) {
+    if (b.bytes >= bytes) return true;
+    if (!b.p || keep == 0) return grow(b, bytes);
+    DevBuf nb;
+    if (!grow(nb, bytes)) return false;
+    if (hipMemcpyAsync(nb.p, b.p, std::min(keep, b.bytes), hipMemcpyDeviceToDevice, s) != hipSuccess) {
+        (void)hipFree(nb.p);
+        return false;
+    }
+    (void)hipDeviceSynchronize();
+    (void)hipFree(b.p);
+    b = nb;
     return true;
 }
 
@@ -1145,6 +1166,7 @@ imls_ctx* imls_create(int device, const imls_params* p) {
 void imls_destroy(imls_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->ustream) (void)hipStreamSynchronize(c->ustream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->cap_mem, &c->front_mem, &c->sample_mem, &c->pca_mem, &c->tkept, &c->mten, &c->upload_ten, &c->tvn, &c->rnr, &c->ransac_mem, &c->rng, &c->lkeys, &c->tpt, &c->tnr, &c->mpt, &c->nodes, &c->tscratch, &c->treescratch, &c->permbuf, &c->qperm, &c->fb, &c->prevnn,
                       &c->upload_t, &c->spt, &c->snr, &c->sscratch,
@@ -1184,7 +1206,7 @@ void imls_destroy(imls_ctx* c) {
     if (c->ftable.p) (void)hipFree(c->ftable.p);
     if (c->h_ftable) (void)hipHostFree(c->h_ftable);
     if (c->ev_build) (void)hipEventDestroy(c->ev_build);
-    if (c->ustream) (void)hipStreamSynchronize(c->ustream), (void)hipStreamDestroy(c->ustream);
+    if (c->ustream) (void)hipStreamDestroy(c->ustream);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -1408,6 +1430,11 @@ int fifo_build(imls_ctx* c) {
         return IMLS_OK;
     }
     if (M > (size_t)0x7fffffff) return fail(c, IMLS_ERR_CAPACITY, "map too large");
+    {   // the build's scratch, before anything is enqueued (its steps never reallocate it)
+        int max_run = 0, nruns = 0;
+        for (auto& e : c->fifo) { max_run = std::max(max_run, e.nk); nruns += e.nk > 0; }
+        if (!grow(c->fscr, fifo_scratch_bytes(max_run, nruns, (int)M))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (FIFO scratch)");
+    }
     // re-frame when the last build's new scans fell outside the frame (their keys were clamped)
     if (c->fq_valid && *c->h_fifo_clamp != 0) c->fq_valid = false;
     if (!c->fq_valid) {
@@ -1444,8 +1471,12 @@ int fifo_build(imls_ctx* c) {
         kept_n += e.nk;
     }
     if (!prefix) { c->merged_ids.clear(); c->m_n = 0; live = 0; kept_n = 0; }
-    for (int k = 0; k < 2; ++k)
-        if (!grow(c->mkey[k], M * 8 + 64) || !grow(c->mval[k], M * 4 + 64)) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (FIFO order)");
+    // the current order's buffers keep their m_n entries when they grow (a plain grow drops them:
+    // the merge would read stale run ids); the other pair is output only
+    if (!grow_keep(c->mkey[c->mcur], M * 8 + 64, (size_t)c->m_n * 8, s) ||
+        !grow_keep(c->mval[c->mcur], M * 4 + 64, (size_t)c->m_n * 4, s) || !grow(c->mkey[c->mcur ^ 1], M * 8 + 64) ||
+        !grow(c->mval[c->mcur ^ 1], M * 4 + 64))
+        return fail(c, IMLS_ERR_DEVICE, "hipMalloc (FIFO order)");
     auto K = [&](int k) { return (unsigned long long*)c->mkey[k].p; };
     auto V = [&](int k) { return (unsigned*)c->mval[k].p; };
     if (c->m_n > 0 && kept_n != c->m_n) {            // evicted runs: stable compaction

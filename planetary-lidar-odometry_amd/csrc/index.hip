@@ -22,7 +22,11 @@ T* carve(char*& p, size_t n) {
 
 bool ensure(DevBuf& b, size_t bytes, std::string& err) {
     if (b.bytes >= bytes) return true;
-    if (b.p) (void)hipFree(b.p);
+    // kernels already enqueued may still use the old buffer (a free under them faults the card)
+    if (b.p) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(b.p);
+    }
     b.p = nullptr;
     b.bytes = 0;
     size_t want = bytes + bytes / 4 + 4096;
@@ -900,6 +904,20 @@ __global__ void k_fifo_gather(const unsigned long long* __restrict__ mkey, const
 }
 
 }  // namespace
+
+size_t fifo_scratch_bytes(int max_run, int nruns, int M) {
+    size_t sort_b = 0, scan_b = 0;
+    const int nb = (int)grid_for((size_t)std::max(M, 1));
+    hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                       (unsigned*)nullptr, (unsigned*)nullptr, std::max(max_run, 1), 0, 48);
+    hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, (int*)nullptr, (int*)nullptr, nb);
+    const size_t n = (size_t)std::max(max_run, 1);
+    const size_t run = (n * 8 + 255) / 256 * 256 + 2 * ((n * 4 + 255) / 256 * 256) + (sort_b + 255) / 256 * 256 + 1024;
+    const size_t frame = (size_t)std::max(nruns, 1) * 64 * 24 + 1024;
+    const size_t keep = 2 * (((size_t)nb * 4 + 255) / 256 * 256) + scan_b + 1024;
+    const size_t merge = ((size_t)M / kMergeTile + 2) * 4 + 256;
+    return std::max(std::max(run, frame), std::max(keep, merge));
+}
 
 int fifo_frame(hipStream_t s, const std::vector<std::pair<const float4*, int>>& runs, float* fq, DevBuf& scratch,
                std::string& err) {

@@ -259,6 +259,9 @@ inline size_t fifo_run_bytes(int n) { return fifo_part((size_t)n * 8) + 2 * fifo
 inline unsigned long long* fifo_run_keys(void* run, int) { return (unsigned long long*)run; }
 inline float4* fifo_run_pts(void* run, int n) { return (float4*)((char*)run + fifo_part((size_t)n * 8)); }
 inline float4* fifo_run_nrm(void* run, int n) { return (float4*)((char*)run + fifo_part((size_t)n * 8) + fifo_part((size_t)n * 16)); }
+// scratch every fifo_* step of one build fits in (sized before the build enqueues anything: the
+// steps share it in stream order and never reallocate it under a pending kernel)
+size_t fifo_scratch_bytes(int max_run, int nruns, int M);
 // the FIFO's quantisation frame (fq: lo xyz, scale) from the bboxes of filtered point sets
 int fifo_frame(hipStream_t s, const std::vector<std::pair<const float4*, int>>& runs, float* fq, DevBuf& scratch,
                std::string& err);
