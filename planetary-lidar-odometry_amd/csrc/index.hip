@@ -775,8 +775,14 @@ __global__ void k_run_gather(const float4* __restrict__ pt, const float4* __rest
     rnr[k] = nr[j];
 }
 
-// the FIFO quantisation frame: a cube of side 1.5 × the runs' largest bbox extent around their
-// bbox centre (later scans of a moving sensor stay inside; the host re-frames if one does not)
+// the FIFO quantisation frame: a cube of side 2 × the runs' largest bbox extent, its origin half an
+// extent below their bbox on every axis (later scans of a moving sensor stay inside; the host
+// re-frames if one does not).  Side and offset are powers of two times the full build's cell
+// (origin = bbox min, side = extent): the grid lines are the full build's, one level up, so the
+// Morton order — and the tree — is the full build's up to the top-level block order and the last
+// bit (on config B's map the query-ball overlaps of leaves / nodes are 8.03 / 74.1 per query vs the
+// full build's 7.80 / 73.5; a 1.5× cube centred on the bbox gave 8.85 / 86.4:
+// tools/fifo_frame_probe.py)
 __global__ void k_fifo_frame(const float* __restrict__ part, int nparts, float* __restrict__ fq) {
     __shared__ float red[6][kBlock];
     float r[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -798,8 +804,8 @@ __global__ void k_fifo_frame(const float* __restrict__ part, int nparts, float* 
     if (threadIdx.x == 0) {
         float ext = 1e-6f;
         for (int d = 0; d < 3; ++d) ext = fmaxf(ext, red[3 + d][0] - red[d][0]);
-        const float side = 1.5f * ext;
-        for (int d = 0; d < 3; ++d) fq[d] = 0.5f * (red[d][0] + red[3 + d][0]) - 0.5f * side;
+        const float side = 2.0f * ext;
+        for (int d = 0; d < 3; ++d) fq[d] = red[d][0] - 0.5f * ext;
         fq[3] = 65535.f / side;
     }
 }

@@ -68,6 +68,12 @@ constexpr int kSparseLanes = 32;    // a leaf wanted by ≤ this many lanes is s
 constexpr int kWide = 3;            // binary levels descended per traversal step (8 boxes per step)
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
 constexpr double kCertSlack = 1.0 + 4e-7;
+#ifndef IMLS_DIST_CHUNK
+#define IMLS_DIST_CHUNK 11
+#endif
+#ifndef IMLS_IMLS_CHUNK
+#define IMLS_IMLS_CHUNK 4
+#endif
 
 __device__ __forceinline__ bool lessp(double da, int ia, double db, int ib) {
     return da < db || (da == db && ia < ib);
@@ -145,6 +151,11 @@ __device__ __forceinline__ void insert_top(float (&lk)[KL], int (&lp)[KL], float
 // min(a, b) of non-NaN floats (a plain select: fminf canonicalises both operands first)
 __device__ __forceinline__ float fmin_nn(float a, float b) { return a < b ? a : b; }
 
+// Keeps a gather where it is issued: the empty asm consumes the loaded registers, so the compiler
+// cannot sink the load into the conditional block that uses it (and wait on it there, one
+// dependent round trip per gather) — the loads of a chunk all issue before any is waited on.
+__device__ __forceinline__ void pin_loaded(const float4& v) { asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z)); }
+
 // Keys-only sorted insertion (precondition d < lk[KL−1]): one v_med3 per slot.
 template <int KL>
 __device__ __forceinline__ void insert_key(float (&lk)[KL], float d) {
@@ -208,16 +219,43 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
     }
     if (nacc < 3) return IMLS_REJ_MLS_FAIL;                   // imls_icp.cpp:463-466
     const int target = first + nacc - 1;                      // Q3: index into L, not into S
+    // the accepted neighbours' points and normals in chunks of 8, every load of a chunk issued (and
+    // pinned) before any term is formed — the first chunk with the bandwidth point L[target]; a term
+    // is added as `accepted ? term : 0`, the same bits as skipping it (both sums start at +0 and so
+    // are never −0: s + 0 = s)
+    constexpr int kIChunk = IMLS_IMLS_CHUNK;
+    float4 qp[kIChunk], qn[kIChunk];
+    auto load_chunk = [&](int j0) {
+#pragma unroll
+        for (int u = 0; u < kIChunk; ++u) {
+            const int j = j0 + u;
+            const int pj = (j < CAP && (acc & (1ull << j))) ? lpos[j < CAP ? j : 0] : p1;
+            qp[u] = t.mpt[pj];
+            qn[u] = t.mnr[pj];
+        }
+    };
+    auto pin_chunk = [&]() {
+#pragma unroll
+        for (int u = 0; u < kIChunk; ++u) {
+            pin_loaded(qp[u]);
+            pin_loaded(qn[u]);
+        }
+    };
     double dsel = 0.0;
     if (LAZY_D) {
         int ptg = p1;
 #pragma unroll
         for (int j = 0; j < CAP; ++j) ptg = (j == target) ? lpos[j] : ptg;
         const float4 q = t.mpt[ptg];
+        load_chunk(0);
+        pin_loaded(q);
+        pin_chunk();
         dsel = exact_d2(xd, q.x, q.y, q.z);
     } else {
 #pragma unroll
         for (int j = 0; j < CAP; ++j) dsel = (j == target) ? ld[j] : dsel;
+        load_chunk(0);
+        pin_chunk();
     }
     const double hmax = sqrt(dsel) / 3;
     // exp(−‖x−p‖² / h / h) (imls_icp.cpp:470) with one reciprocal per query instead of two divisions
@@ -225,21 +263,29 @@ __device__ int finish_query(const float xf[3], const double ns[3], const double 
     const double ih2 = 1.0 / (hmax * hmax);
     double wsum = 0.0, psum = 0.0;
 #pragma unroll
-    for (int j = 0; j < CAP; ++j) {
-        const int pj = (acc & (1ull << j)) ? lpos[j] : p1;
-        const float4 qp = t.mpt[pj];
-        const float4 qn = t.mnr[pj];
-        if (acc & (1ull << j)) {
-            const double dx = xd[0] - (double)qp.x, dy = xd[1] - (double)qp.y, dz = xd[2] - (double)qp.z;
+    for (int j0 = 0; j0 < CAP; j0 += kIChunk) {
+        if (j0 > 0) {
+            if (!__ballot((acc >> j0) != 0ull)) break;          // no lane has a later neighbour
+            if (!__ballot((acc >> j0) & ((1ull << kIChunk) - 1ull))) continue;     // none in this chunk
+            load_chunk(j0);
+            pin_chunk();
+        }
+#pragma unroll
+        for (int u = 0; u < kIChunk; ++u) {
+            const int j = j0 + u;
+            if (j >= CAP) break;
+            const bool a = (acc >> j) & 1ull;
+            if (!__ballot(a)) continue;                         // wave-uniform
+            const double dx = xd[0] - (double)qp[u].x, dy = xd[1] - (double)qp[u].y, dz = xd[2] - (double)qp[u].z;
             double dn = dx * dx;
             dn = dn + dy * dy;
             dn = dn + dz * dz;
             const double w = exp(-dn * ih2);
-            double pr = (w * dx) * (double)qn.x;
-            pr = pr + (w * dy) * (double)qn.y;
-            pr = pr + (w * dz) * (double)qn.z;
-            wsum += w;
-            psum += pr;
+            double pr = (w * dx) * (double)qn[u].x;
+            pr = pr + (w * dy) * (double)qn[u].y;
+            pr = pr + (w * dz) * (double)qn[u].z;
+            wsum += a ? w : 0.0;
+            psum += a ? pr : 0.0;
         }
     }
     const double height = psum / (wsum + 1e-5);               // Q4
@@ -1233,7 +1279,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
 // =============================================================================================
 // 4 waves/SIMD (≤ 128 VGPRs): the exact stage waits on its gathers, resident waves hide them
 #ifndef IMLS_FINISH_WPE
-#define IMLS_FINISH_WPE 4
+#define IMLS_FINISH_WPE 3
 #endif
 #define IMLS_FINISH_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 24 ? IMLS_FINISH_WPE : 1)))
 template <int KL>
@@ -1269,13 +1315,27 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
         const float W = wlist[slot];
         double ed[KL];
         int ep[KL];
-        // all positions, then all points, before any is consumed (two memory round trips)
+        // all positions, then the points in two chunks whose loads all issue before any is consumed
+        // (three memory round trips).  The loads are unconditional and pinned (pin_loaded): with
+        // `ep ≥ 0 ? exact_d2(…) : ∞` the compiler sank each load into its own branch and waited on
+        // it there — 22 dependent round trips per lane, most of this kernel's time
 #pragma unroll
         for (int j = 0; j < KL; ++j) ep[j] = lists[(size_t)j * N + slot];
+        constexpr int kCh = IMLS_DIST_CHUNK;
 #pragma unroll
-        for (int j = 0; j < KL; ++j) {
-            const float4 q = t.mpt[max(ep[j], 0)];
-            ed[j] = ep[j] >= 0 ? exact_d2(xd, q.x, q.y, q.z) : kInfD;
+        for (int j0 = 0; j0 < KL; j0 += kCh) {
+            float4 q[kCh];
+#pragma unroll
+            for (int u = 0; u < kCh; ++u)
+                if (j0 + u < KL) q[u] = t.mpt[max(ep[j0 + u], 0)];
+#pragma unroll
+            for (int u = 0; u < kCh; ++u)
+                if (j0 + u < KL) pin_loaded(q[u]);
+#pragma unroll
+            for (int u = 0; u < kCh; ++u) {
+                const int j = j0 + u;
+                if (j < KL) ed[j] = exact_d2(xd, q[u].x, q[u].y, q[u].z) + (ep[j] >= 0 ? 0.0 : kInfD);
+            }
         }
         // odd-even transposition sort by (d², index); the fp32 order is already nearly exact.  The
         // index (the filtered index in mpt[].w, libnabo's tie order) is read only for an exact tie
