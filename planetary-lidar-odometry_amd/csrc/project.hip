@@ -68,6 +68,10 @@ constexpr int kSparseLanes = 32;    // a leaf wanted by ≤ this many lanes is s
 constexpr int kWide = 3;            // binary levels descended per traversal step (8 boxes per step)
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
 constexpr double kCertSlack = 1.0 + 4e-7;
+// list length for K ≤ 20 (the shipped K = 20)
+#ifndef IMLS_B_KL
+#define IMLS_B_KL 22
+#endif
 #ifndef IMLS_DIST_CHUNK
 #define IMLS_DIST_CHUNK 11
 #endif
@@ -479,7 +483,7 @@ __device__ __forceinline__ float need_key_ids(const float (&lk)[KL], float r2, i
 
 // Slot-id keys in registers, positions in LDS: ~96 VGPRs and ~29 KB of LDS per 4-wave block — 5
 // waves/SIMD (round 4: the register list needed 160 VGPRs, 3 waves/SIMD; config B 331 → 406 pairs/s)
-#define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 24 ? 5 : 2)))
+#define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 26 ? 5 : 2)))
 template <int KL>
 __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
@@ -1169,18 +1173,16 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
             const bool ginner = gact && gnode < P, gleaf = gact && gnode >= P;
             n_inner += __popcll(__ballot(ginner && gl == 0));
             n_leaf += __popcll(__ballot(gleaf && gl == 0));
+            // every lane's loads of the step issue together — its node record (inner groups) and its
+            // B / 8 leaf points (leaf groups) — from clamped addresses, the values selected after:
+            // loads behind the group / count tests became one branch and one wait per load
             float cdist = kInfF;
             int child = 0;
-            if (ginner) {
-                const int lev = 31 - __builtin_clz(gnode);
-                const int sw = min(kWide, t.levels - lev);     // ≤ 8 descendants: one per lane
-                if (gl < (1 << sw)) {
-                    const float4* rec = t.nodes + 3 * (((size_t)gnode << (sw - 1)) + (gl >> 1));
-                    const float4 a = rec[0], b = rec[1], c = rec[2];
-                    cdist = (gl & 1) ? box_d2(xf, b.z, b.w, c.x, c.y, c.z, c.w) : box_d2(xf, a.x, a.y, a.z, a.w, b.x, b.y);
-                    child = (gnode << sw) + gl;
-                }
-            }
+            int sw = 0;
+            if (ginner) sw = min(kWide, t.levels - (31 - __builtin_clz(gnode)));   // ≤ 8 descendants: one per lane
+            const bool gbox = ginner && gl < (1 << sw);
+            const float4* rec = t.nodes + 3 * (gbox ? (((size_t)gnode << (sw - 1)) + (gl >> 1)) : (size_t)1);
+            const float4 ra = rec[0], rb = rec[1], rc = rec[2];
             int lbase = 0, lcnt = 0;
             if (gleaf) {
                 const int leaf = gnode - P;
@@ -1189,16 +1191,28 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
                     lcnt = min(B, M - lbase);
                 }
             }
+            float4 lq[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int j = gl + 8 * k;
+                lq[k] = t.mpt[(k < ppl && j < lcnt) ? lbase + j : 0];
+            }
+            pin_loaded(ra);
+            pin_loaded(rb);
+            pin_loaded(rc);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pin_loaded(lq[k]);
+            if (gbox) {
+                cdist = (gl & 1) ? box_d2(xf, rb.z, rb.w, rc.x, rc.y, rc.z, rc.w) : box_d2(xf, ra.x, ra.y, ra.z, ra.w, rb.x, rb.y);
+                child = (gnode << sw) + gl;
+            }
             float pd[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                pd[k] = kInfF;
                 const int j = gl + 8 * k;
-                if (k < ppl && j < lcnt) {
-                    const float4 q = t.mpt[lbase + j];
-                    const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
-                    pd[k] = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-                }
+                const float ex = lq[k].x - xf[0], ey = lq[k].y - xf[1], ez = lq[k].z - xf[2];
+                const float d = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                pd[k] = (k < ppl && j < lcnt) ? d : kInfF;
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -1281,7 +1295,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
 #ifndef IMLS_FINISH_WPE
 #define IMLS_FINISH_WPE 3
 #endif
-#define IMLS_FINISH_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 24 ? IMLS_FINISH_WPE : 1)))
+#define IMLS_FINISH_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 26 ? IMLS_FINISH_WPE : 1)))
 template <int KL>
 __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict__ spt,
                                                        const float4* __restrict__ snr,
@@ -2124,7 +2138,7 @@ void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     const int K = kp.K;
     if (K <= 8) launch_wave_batch<12>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else if (K <= 16) launch_wave_batch<20>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
-    else if (K <= 20) launch_wave_batch<22>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
+    else if (K <= 20) launch_wave_batch<IMLS_B_KL>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     else launch_wave_batch<36>(s, tab, npairs, maxN, any_small, any_large, kp, it, use_prev);
     // exact fallback for uncertified queries: every frame's kFallbackBlocks slabs are written, by
     // fewer physical blocks per frame when many frames share the launch (uncertified queries are
@@ -2161,7 +2175,7 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
     else if (K <= 16) launch_wave<20>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     // K ≤ 20 (the shipped 20): two slack entries certify every query on config B (KL 21 left a few
     // uncertified → the slow exact fallback, −30 %; KL 22 vs 24 measured +6.7 % pairs/s, 4 in flight)
-    else if (K <= 20) launch_wave<22>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
+    else if (K <= 20) launch_wave<IMLS_B_KL>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     else launch_wave<36>(s, wblocks, t, spt, snr, qperm, N, pose, done, kp, cs, cd, cn, partial1, tr, stats, fb_list, fb_count, delta, lists, use_prev, marks);
     // exact fallback for uncertified queries (usually none; the launch exits at once then); the
     // fused small-frame kernel resolves them in place

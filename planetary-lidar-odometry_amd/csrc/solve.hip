@@ -545,14 +545,42 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     // alone, whatever exact stage produced its rows — sums them in this one order
     float4 rs[kSmallPer], rn[kSmallPer];
     double rb[kSmallPer];
+    static_assert(kSmallPer % 2 == 0, "two row groups");
+    // the rows in two groups of kSmallPer/2 per thread, each group's s, y and n loaded together
+    // (unconditional loads from a clamped row index, values selected after: a load behind `r < N`
+    // or the valid flag became a branch with its own wait — 24 dependent round trips per thread);
+    // the second group only when the frame has rows there (block-uniform), its loads ordered after
+    // the first group's by an asm dependency (all rows in flight at once spilled ~60 VGPRs)
+    const int rmax = N > 0 ? N - 1 : 0;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int kGrp = kSmallPer / 2;
+    int tg = t;
+    auto load_group = [&](int k0) {
+        float4 c[kGrp], d[kGrp], n[kGrp];
 #pragma unroll
-    for (int k = 0; k < kSmallPer; ++k) {
-        const int r = t + k * kSmallBlock;
-        rs[k] = r < N ? rows.cs[r] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const bool v = r < N && rs[k].w != 0.f;
-        const float4 d4 = v ? rows.cd[r] : make_float4(0.f, 0.f, 0.f, 0.f);
-        rn[k] = v ? rows.cn[r] : make_float4(0.f, 0.f, 0.f, 0.f);
-        rb[k] = small_b(rs[k], d4, rn[k]);
+        for (int u = 0; u < kGrp; ++u) {
+            const int rr = min(tg + (k0 + u) * kSmallBlock, rmax);
+            c[u] = rows.cs[rr];
+            d[u] = rows.cd[rr];
+            n[u] = rows.cn[rr];
+        }
+#pragma unroll
+        for (int u = 0; u < kGrp; ++u) {
+            const int k = k0 + u;
+            const int r = t + k * kSmallBlock;
+            rs[k] = r < N ? c[u] : z4;
+            const bool v = r < N && rs[k].w != 0.f;
+            rn[k] = v ? n[u] : z4;
+            rb[k] = small_b(rs[k], v ? d[u] : z4, rn[k]);
+        }
+    };
+    load_group(0);
+    if (N > kGrp * kSmallBlock) {
+        asm volatile("" : "+v"(tg) : "v"(rb[0]), "v"(rb[kGrp - 1]));
+        load_group(kGrp);
+    } else {
+#pragma unroll
+        for (int k = kGrp; k < kSmallPer; ++k) { rs[k] = z4; rn[k] = z4; rb[k] = 0.0; }
     }
     if (stopped) return;              // block-uniform, before any LDS write or barrier
 #pragma unroll
