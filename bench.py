@@ -858,22 +858,32 @@ def main():
     # (host-input pairs: the FIFO rotation of each result's load)
     frames_at_launch = {}
     tag_loads = stream or (args.host_inputs and not stream)
-    if tag_loads:
+    if tag_loads and stream:
         orig_prep = runner._prep
 
         def tagging_prep(idx):
             orig_prep(idx)
             for q in idx:
-                frames_at_launch.setdefault(q, []).append(runner.last[q] if stream else runner.rot[q])
+                frames_at_launch.setdefault(q, []).append(runner.last[q])
         runner._prep = tagging_prep
         if runner.pipe:
             runner.pipe.prep = tagging_prep
+    elif tag_loads:
+        # host-input pairs: every load (pipelined or single-frame) records its FIFO rotation
+        orig_load = runner._load
+
+        def tagging_load(c, k, count):
+            orig_load(c, k, count)
+            frames_at_launch.setdefault(k, []).append(runner.rot[k])
+        runner._load = tagging_load
     elapsed, per_step, res = timed_steps(runner.step, args.steps, world, dev, torch.cuda.synchronize)
     res += runner.drain()                 # the batches still in flight (already finished: synchronized)
-    if tag_loads:
+    if tag_loads and stream:
         runner._prep = orig_prep
         if runner.pipe:
             runner.pipe.prep = orig_prep
+    elif tag_loads:
+        runner._load = orig_load
     if hasattr(runner, "t_prep"):
         log(f"[rank {rank}] host time per step: uploads (+ filters) {runner.t_prep / args.steps * 1e3:.2f} ms, "
             f"rest (builds, launches, waits) {runner.t_reg / args.steps * 1e3:.2f} ms")

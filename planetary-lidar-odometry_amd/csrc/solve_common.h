@@ -313,7 +313,8 @@ __device__ inline void delta_from_x(const double x[6], double D[16]) {
     const double ang = sqrt(sq);
     double ax = 0, ay = 0, az = 0;
     if (sq > 0) { ax = wx / ang; ay = wy / ang; az = wz / ang; }   // (ang = ‖ω‖: the same root)
-    const double s = sin(ang), c = cos(ang);
+    double s, c;
+    sincos(ang, &s, &c);              // one shared argument reduction (round 5: sin + cos)
     const double sx = s * ax, sy = s * ay, sz = s * az;
     const double c1x = (1 - c) * ax, c1y = (1 - c) * ay, c1z = (1 - c) * az;
     double R[9];
