@@ -764,6 +764,55 @@ def stats_pass(runner):
     return out
 
 
+def host_leg(pairs, p, dev, local, args, world, fuse):
+    """Config B's host hand-over leg beside the headline (SURVEY §8(d) t_pair): the same pairs, each
+    context's map a device FIFO of the pair's 10 scans with its incremental index, and every
+    registration taking the NEWEST scan and the source from host memory (pack + PCIe inside the
+    timed region).  The headline `value` stays the resident-input rate (inputs in HBM when the timed
+    region starts); this is the PCIe-inclusive rate of the same workload, every timed result checked
+    bit for bit against its pair registered alone on a fresh context holding the same FIFO content."""
+    import torch
+    hr = PairRunner(pairs, p, dev, local, fuse=fuse, groups=args.groups, host=True)
+    loads = {}
+    orig_load = hr._load
+
+    def tagging_load(c, k, count):
+        orig_load(c, k, count)
+        loads.setdefault(k, []).append(hr.rot[k])
+    for _ in range(args.warmup):
+        hr.step()
+    hr.drain()
+    torch.cuda.synchronize()
+    hr._load = tagging_load
+    elapsed, per_step, res = timed_steps(hr.step, args.steps, world, dev, torch.cuda.synchronize)
+    res += hr.drain()
+    hr._load = orig_load
+    seen, cache, mism = {}, {}, 0
+    for r in res:
+        k = r[0]
+        j = seen.get(k, 0)
+        seen[k] = j + 1
+        if args.no_verify:
+            continue
+        key = (k, loads[k][j])
+        if key not in cache:
+            cache[key] = hr.single_fresh(*key)
+        mism += 0 if same_result(r, cache[key]) else 1
+    probe = latency_probe(lambda: hr.single([0]), hr.ctxs[0], max(1, min(args.latency_pairs, 20)), args.iters)
+    hr.close()
+    if mism:
+        raise SystemExit(f"bench: host leg: {mism} timed result(s) differ from the single-frame path")
+    n = args.steps * len(pairs)
+    return {"value": world * n / elapsed, "unit": "scan-pairs/s",
+            "inputs": "host memory (PCIe inside the timed region)",
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "index_ms_per_registration": probe["kernel_avg_ms"].get("index"),
+            "single_pair_median_ms": probe["median_ms"],
+            "verify": {"timed_results": len(res), "checked": 0 if args.no_verify else len(res), "mismatches": mism,
+                       "rule": "every timed result vs its pair registered alone on a fresh context holding the same "
+                               "FIFO content (single-frame kernels), bit for bit"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -788,6 +837,7 @@ def main():
     ap.add_argument("--latency-pairs", type=int, default=50, help="single-pair latency / roofline probe size")
     ap.add_argument("--busy-steps", type=int, default=5, help="steps of the HIP-event busy-time pass (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
+    ap.add_argument("--no-host-leg", action="store_true", help="config B: skip the host hand-over leg")
     ap.add_argument("--no-verify", action="store_true", help="skip the bit-equality check of the timed results")
     ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
@@ -978,9 +1028,20 @@ def main():
     bytes_per_step = float(sum(fb.values())) if not stream else float(np.mean(list(fb.values()))) * P
     busy = busy_pass(runner, args.busy_steps, torch.cuda.synchronize) if args.busy_steps > 0 else None
     trav = probe_ctx.traversal_stats()
+    want_leg = args.workload == "B" and not args.host_inputs and not args.no_host_leg
+
+    def run_leg():
+        # after the resident runner is closed: with its contexts (and their streams) alive, the leg's
+        # launch sequences shared hardware queues and measured ~45 % slower
+        leg = host_leg(runner.pairs, p, dev, local, args, world, fuse)
+        log(f"[rank {rank}] host hand-over leg: {leg['value']:.1f} pairs/s, index {leg['index_ms_per_registration']} ms "
+            f"per registration, {leg['verify']['checked']} results checked")
+        return leg
 
     if rank != 0:
         runner.close()
+        if want_leg:
+            run_leg()
         if _grouped():
             dist.destroy_process_group()
         return
@@ -1126,9 +1187,12 @@ def main():
         "sequences": len(trajs),
         "trajectory_end_seq0": first_traj[1][-1][:3, 3].tolist() if first_traj is not None and len(first_traj[1]) else None,
         "cpu_baseline": cpu,
+        "host_handover": None,
     }
-    print(json.dumps(out), flush=True)
     runner.close()
+    if want_leg:
+        out["host_handover"] = run_leg()
+    print(json.dumps(out), flush=True)
     if _grouped():
         dist.destroy_process_group()
 
