@@ -570,17 +570,32 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         // (the list is full and the bound tight before the traversal starts; a later leaf insert
         // must then skip points already listed).  Slot j keeps entry j's position; its key carries
         // id j (the keys alone get sorted)
+        // The points in two chunks, each chunk's loads issued (pinned) before any of its slot writes:
+        // in the batched kernel the table's pointers are generic, so a point load after a slot write
+        // (an LDS store it might alias) waited for it — one round trip per entry
         int pj[KL];
 #pragma unroll
         for (int j = 0; j < KL; ++j) pj[j] = lists[(size_t)j * N + slot];
+        constexpr int kPCh = (KL + 1) / 2;
 #pragma unroll
-        for (int j = 0; j < KL; ++j) {
-            const float4 q = t.mpt[max(pj[j], 0)];
-            const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
-            const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
-            const bool keep = pj[j] >= 0 && d32 <= r2s;
-            lk[j] = keep ? IK::make(d32, j) : IK::empty(j);
-            mypos[j * kWaveBlock] = keep ? pj[j] : -1;
+        for (int j0 = 0; j0 < KL; j0 += kPCh) {
+            float4 q[kPCh];
+#pragma unroll
+            for (int u = 0; u < kPCh; ++u)
+                if (j0 + u < KL) q[u] = t.mpt[max(pj[j0 + u], 0)];
+#pragma unroll
+            for (int u = 0; u < kPCh; ++u)
+                if (j0 + u < KL) pin_loaded(q[u]);
+#pragma unroll
+            for (int u = 0; u < kPCh; ++u) {
+                const int j = j0 + u;
+                if (j >= KL) break;
+                const float ex = q[u].x - xf[0], ey = q[u].y - xf[1], ez = q[u].z - xf[2];
+                const float d32 = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                const bool keep = pj[j] >= 0 && d32 <= r2s;
+                lk[j] = keep ? IK::make(d32, j) : IK::empty(j);
+                mypos[j * kWaveBlock] = keep ? pj[j] : -1;
+            }
         }
         bool swapped = true;
         while (swapped) {
