@@ -25,9 +25,13 @@ __device__ __forceinline__ double exact_d2(const double xd[3], float px, float p
 // x = float(rPose·[p;1]) and the (optionally rotated) source normal (laser_odometry.cpp:527-549)
 __device__ __forceinline__ void transform_query(const double* __restrict__ pose, float4 p, float4 nsv, int rot_normal,
                                                 float xf[3], double ns[3]) {
+    // the pose through the constant address space: one set of scalar loads for the wave (a pointer
+    // read from the batched kernels' frame table is generic, and was loaded per lane, 96 B each)
+    typedef __attribute__((address_space(4))) const double kconst_d;
+    const kconst_d* cp = (const kconst_d*)pose;
     double T[12];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = pose[k];
+    for (int k = 0; k < 12; ++k) T[k] = cp[k];
     const double pd[3] = {p.x, p.y, p.z};
 #pragma unroll
     for (int r = 0; r < 3; ++r) {

@@ -44,6 +44,10 @@ constexpr int kWaveBlock = 256;
 // constant address space view of read-only device data: wave-uniform loads through it are scalar
 typedef float kf4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(4))) const kf4v kconst_f4;
+// a value an earlier launch wrote and the whole wave reads (the done flag, the last Δ): through the
+// constant address space, i.e. scalar loads — not a per-lane (flat, in the batched kernels) load
+__device__ __forceinline__ int ld_const(const int* p) { return *(const __attribute__((address_space(4))) int*)p; }
+__device__ __forceinline__ double ld_const(const double* p) { return *(const __attribute__((address_space(4))) double*)p; }
 constexpr int kFallbackBlocks = 64;
 constexpr int kFallbackBlocksBatched = 4;   // physical blocks per frame of a large batch (same slabs)
 static_assert(kWaveBlock == kPass1Block && kFallbackBlocks == kPass1Fallback, "pass-1 slab layout (solve.hip)");
@@ -494,7 +498,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                                                          float4* __restrict__ xref, float* __restrict__ nref,
                                                          int use_prev, unsigned long long* __restrict__ nbr_stats,
                                                          int bx) {
-    if (done && *done) return;
+    if (done && ld_const(done)) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float4 sboxa[kWaveBlock / 64][kWaveStack];   // stacked node boxes: lo.xyz, hi.x
     __shared__ float2 sboxb[kWaveBlock / 64][kWaveStack];   //                     hi.yz
@@ -511,10 +515,20 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     const int slot = (bx * (kWaveBlock / 64) + wv) * qp + lane;
     const bool active = lane < qp && slot < N;
     float xf[3] = {0.f, 0.f, 0.f};
+    // the stored list's bound and reference (slot-indexed) load beside the query's point: one round
+    // trip after the query index, not one more after the transform
+    float w_prev = 0.f, n_prev = 0.f;
+    float4 x_prev = make_float4(0.f, 0.f, 0.f, 0.f);
     if (active) {
         double ns[3];
         const int i = (int)qperm[slot];
-        transform_query(pose, spt[i], make_float4(0.f, 0.f, 0.f, 0.f), 0, xf, ns);
+        const float4 sp4 = spt[i];
+        if (use_prev) {
+            w_prev = wlist[slot];
+            x_prev = xref[slot];
+            n_prev = nref[slot];
+        }
+        transform_query(pose, sp4, make_float4(0.f, 0.f, 0.f, 0.f), 0, xf, ns);
     }
     float lk[KL];
 #pragma unroll
@@ -554,15 +568,16 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         for (int r = 0; r < 3; ++r)
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                const double e = delta[r * 4 + c] - (r == c ? 1.0 : 0.0);
+                const double e = ld_const(delta + r * 4 + c) - (r == c ? 1.0 : 0.0);
                 rf += e * e;
             }
-        const float tn = (float)sqrt(delta[3] * delta[3] + delta[7] * delta[7] + delta[11] * delta[11]);
+        const double d3 = ld_const(delta + 3), d7 = ld_const(delta + 7), d11 = ld_const(delta + 11);
+        const float tn = (float)sqrt(d3 * d3 + d7 * d7 + d11 * d11);
         const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
-        greedy = disp * disp > kReseed * wlist[slot];
+        greedy = disp * disp > kReseed * w_prev;
     }
     float wlow = -1.0f;              // W' of the stored list at xf (prefill certificate below)
-    if (active && !greedy && kp.reuse) skip = verlet_skip(xref[slot], nref[slot], xf, r2s, wskip, wlow);
+    if (active && !greedy && kp.reuse) skip = verlet_skip(x_prev, n_prev, xf, r2s, wskip, wlow);
     if (active && !greedy && !skip) {
         // prefill from the previous iteration's list re-measured at the new pose: all positions,
         // then all points are loaded before any is consumed (two memory round trips, not 2·KL),
@@ -988,7 +1003,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
                                                           int use_prev, unsigned long long* __restrict__ nbr_stats,
                                                           int bx, const QFinishArgs& fa = QFinishArgs{}) {
     static_assert(KL <= 64, "one list entry per lane");
-    if (done && *done) return;
+    if (done && ld_const(done)) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float sdist[kWaveBlock / 64][kWaveStack];
     __shared__ int fnode[kWaveBlock / 64][kFStack];      // frontier traversal
@@ -1037,10 +1052,11 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         for (int r = 0; r < 3; ++r)
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                const double e = delta[r * 4 + c] - (r == c ? 1.0 : 0.0);
+                const double e = ld_const(delta + r * 4 + c) - (r == c ? 1.0 : 0.0);
                 rf += e * e;
             }
-        const float tn = (float)sqrt(delta[3] * delta[3] + delta[7] * delta[7] + delta[11] * delta[11]);
+        const double d3 = ld_const(delta + 3), d7 = ld_const(delta + 7), d11 = ld_const(delta + 11);
+        const float tn = (float)sqrt(d3 * d3 + d7 * d7 + d11 * d11);
         const float disp = tn + (float)sqrt(rf) * sqrtf(xf[0] * xf[0] + xf[1] * xf[1] + xf[2] * xf[2]);
         greedy = disp * disp > kReseed * wlist[slot];
     }
@@ -1324,7 +1340,7 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
                                                        unsigned long long* __restrict__ nbr_stats,
                                                        unsigned* __restrict__ fb_list, unsigned* __restrict__ fb_count,
                                                        int bx) {
-    if (done && *done) return;
+    if (done && ld_const(done)) return;
     __shared__ double red[kWaveBlock / 64][kNormEq];
     __shared__ double out[kNormEq];
     __shared__ unsigned rej_s[IMLS_NUM_REJ + 3];
@@ -1339,17 +1355,20 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
     int cat = -2, kq = 0, i1 = -1, p1 = -1;
     float yf[3] = {0, 0, 0}, nf[3] = {0, 0, 0};
     if (active) {
-        transform_query(pose, spt[i], snr[i], kp.transform_normal, xf, ns);
-        const double xd[3] = {xf[0], xf[1], xf[2]};
-        const float W = wlist[slot];
+        // the query's point and normal, then the list (and its bound) beside them: one round trip
+        // for both after the query index (the list depends on the slot only)
+        const float4 sp4 = spt[i], sn4 = snr[i];
         double ed[KL];
         int ep[KL];
-        // all positions, then the points in two chunks whose loads all issue before any is consumed
-        // (three memory round trips).  The loads are unconditional and pinned (pin_loaded): with
-        // `ep ≥ 0 ? exact_d2(…) : ∞` the compiler sank each load into its own branch and waited on
-        // it there — 22 dependent round trips per lane, most of this kernel's time
 #pragma unroll
         for (int j = 0; j < KL; ++j) ep[j] = lists[(size_t)j * N + slot];
+        const float W = wlist[slot];
+        transform_query(pose, sp4, sn4, kp.transform_normal, xf, ns);
+        const double xd[3] = {xf[0], xf[1], xf[2]};
+        // the points in two chunks whose loads all issue before any is consumed (the list's round
+        // trip, then two).  The loads are unconditional and pinned (pin_loaded): with
+        // `ep ≥ 0 ? exact_d2(…) : ∞` the compiler sank each load into its own branch and waited on
+        // it there — 22 dependent round trips per lane, most of this kernel's time
         constexpr int kCh = IMLS_DIST_CHUNK;
 #pragma unroll
         for (int j0 = 0; j0 < KL; j0 += kCh) {
@@ -1749,7 +1768,7 @@ __device__ __forceinline__ void project_lane_body(TreeView t, const float4* __re
                                                              imls_iter_trace* __restrict__ tr,
                                                              unsigned long long* __restrict__ nbr_stats, int nlog) {
     // (done: the k_finish launch that listed the deferred queries left at once too)
-    if (done && *done) return;
+    if (done && ld_const(done)) return;
     __shared__ uint2 stack[kStackDepth][kProjBlock];
     __shared__ double red[kProjBlock / 64][kNormEq];
     __shared__ double out[kNormEq];
