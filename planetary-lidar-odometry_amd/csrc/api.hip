@@ -2003,8 +2003,17 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
     // every member's deferred build: its filter count (one wait each, all filters already enqueued)
     // then all the members' index builds in one launch sequence on the lead's stream
     hs.mark("checks");
-    if (int rc = batch_builds(L, ctxs, n, batch_fusable(L) && (L->P.solve_method != IMLS_SOLVE_RANSAC || n <= (size_t)kMaxRansacBatch), &hs))
+    bool fuse = batch_fusable(L) && (L->P.solve_method != IMLS_SOLVE_RANSAC || n <= (size_t)kMaxRansacBatch);
+    if (int rc = batch_builds(L, ctxs, n, fuse, &hs))
         return rc;
+    // a batch of ONE small frame takes the single-frame launches — the lone-frame path with the exact
+    // stage fused into the wave-per-query traversal (two launches per ICP iteration, not three; the
+    // same results): the 2000-query config B variant 1450 → 1835 pairs/s (profiles/r05_ab/r05n_q).
+    // A large frame keeps the table-driven kernels, measured faster in flight (435-445 vs 430-433
+    // pairs/s on config B, though each launch alone is slower: profiles/r05_ab/r05n)
+    if (n == 1 && L->has_source && L->N <= kSmallRows && (L->kp.qwave > 0 || (L->kp.qwave < 0 && L->N <= kQwaveAutoN))) {
+        fuse = false;                     // (its builds ran on its own stream: nothing to join)
+    }
     hs.mark("filters+builds");
     (void)hipSetDevice(L->device);
     for (size_t k = 0; k < n; ++k) {
@@ -2013,7 +2022,7 @@ int frames_async(imls_ctx* const* ctxs, size_t n) {
             return fail(L, IMLS_ERR_STATE, "context " + std::to_string(k) + ": set_target and set_source first");
     }
     L->members.assign(ctxs, ctxs + n);
-    L->batch_fused = batch_fusable(L) && (L->P.solve_method != IMLS_SOLVE_RANSAC || n <= (size_t)kMaxRansacBatch);
+    L->batch_fused = fuse;
     if (!L->batch_fused) {
         // one launch sequence per frame, each on its own context stream
         for (size_t k = 0; k < n; ++k) {

@@ -312,6 +312,7 @@ void launch_solve_chain(hipStream_t s, int N, int blocks1, const KParams& kp, co
                         SolveState& st, imls_iter_trace* tr, int update_pose, int rows_are_double,
                         const int* count = nullptr, const double* wsum = nullptr);
 // N above which the float-row LS takes the grid chain (below: one block, k_solve_small)
+constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query up to this many queries
 constexpr int kSmallRows = 4096;
 int solve_blocks(int N);
 // Batched LS / weighted-LS solve + pose update for all frames of tab (float rows from the batched

@@ -51,7 +51,6 @@ __device__ __forceinline__ double ld_const(const double* p) { return *(const __a
 constexpr int kFallbackBlocks = 64;
 constexpr int kFallbackBlocksBatched = 4;   // physical blocks per frame of a large batch (same slabs)
 static_assert(kWaveBlock == kPass1Block && kFallbackBlocks == kPass1Fallback, "pass-1 slab layout (solve.hip)");
-constexpr int kQwaveAutoN = 16384;  // auto traversal choice: one wave per query up to this many queries
 constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
 constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
 constexpr int kFStack = 256;        // frontier traversal's stack per wave (see knn_qwave_body)
