@@ -682,8 +682,21 @@ class LaserOdometry:
     scan crosses PCIe each frame.  The context (and its RANSAC rand() stream) persists across frames."""
 
     def __init__(self, params: Optional[_abi.ImlsParams] = None, device: int = 0, pose_file: Optional[str] = None,
-                 output_dir: Optional[str] = None):
+                 output_dir: Optional[str] = None, pipelined: Optional[bool] = None):
         self.ctx = ImlsContext(params, device)
+        # pipelined (default for max_queue_size 1, the shipped config): two contexts alternate.  Frame
+        # k registers on the one holding scan k−1's index while its own filtered scan goes to the
+        # other — that push's pack, upload, NaN filter and index build run beside the registration.
+        # The reference's work per frame is unchanged (accumulateTargetCloud after matching,
+        # laser_odometry.cpp:663-664: only its start moves earlier, and the map the next frame sees is
+        # the same scan); the RANSAC rand() stream is handed from one context to the other, so the
+        # draws continue as in one context (tests/test_gpu_stream.py: poses bit-equal to one context)
+        self._ctxs = [self.ctx]
+        if pipelined is None:
+            pipelined = self.ctx.params.max_queue_size == 1
+        if pipelined and self.ctx.params.max_queue_size == 1:
+            self._ctxs.append(ImlsContext(params, device))
+        self._cur = 0                   # the context holding the map the next frame registers against
         # output_dir (opt-in): the reference's per-iteration outputs (laser_odometry.cpp:621-625) —
         # matched_points/<ts>_<i>.txt and imls_iter_results.txt under it, from the device trace and
         # the captured correspondences (the subdirectory is created here; the reference needs it
@@ -692,7 +705,8 @@ class LaserOdometry:
         if output_dir:
             import os
             os.makedirs(os.path.join(output_dir, "matched_points"), exist_ok=True)
-            self.ctx.capture_correspondences(True)
+            for c in self._ctxs:
+                c.capture_correspondences(True)
         self.prev_pose = np.eye(4)
         self.frame_count = 0
         self.pose_file = pose_file
@@ -700,7 +714,12 @@ class LaserOdometry:
         self.results: list = []         # (timestamp, rPose, iterations, status) per registered frame
 
     def close(self):
-        self.ctx.close()
+        for c in self._ctxs:
+            c.close()
+
+    @property
+    def pipelined(self) -> bool:
+        return len(self._ctxs) == 2
 
     def __enter__(self):
         return self
@@ -715,9 +734,12 @@ class LaserOdometry:
         times = TimesLog(self.output_dir) if self.output_dir else None
         result = None
         n_flat = len(flat_cloud)
-        registers = self.frame_count != 0 and n_flat != 0 and self.ctx.n_target != 0
+        ctx = self.ctx = self._ctxs[self._cur]
+        nxt = self._ctxs[1 - self._cur] if self.pipelined else ctx   # where this frame's scan goes
+        pushed = False
+        registers = self.frame_count != 0 and n_flat != 0 and ctx.n_target != 0
         if registers:
-            self.ctx.set_source(flat_cloud)            # the flat cloud's upload: this path's preprocessing
+            ctx.set_source(flat_cloud)                 # the flat cloud's upload: this path's preprocessing
         if times:
             times.frame(timestamp)
             times.step("1. Preprocessing")
@@ -725,10 +747,16 @@ class LaserOdometry:
             if not registers:
                 # in_cloud / the map is empty: the first iteration's gate breaks with rPose = I (570-576)
                 result = dict(pose=np.eye(4), iters=0, status=_abi.IMLS_FRAME_TOO_FEW, trace=[])
+            elif nxt is not ctx:
+                ctx.register_frame_async()
+                nxt.map_push(filtered_cloud)           # this frame's accumulateTargetCloud, overlapped
+                pushed = True
+                pose, iters, status = ctx.register_frame_result()
+                result = dict(pose=pose, iters=iters, status=status, trace=ctx.last_trace)
             else:
-                result = self.ctx.register_frame()
-                if self.output_dir:
-                    self._save_iterations(result, timestamp)
+                result = ctx.register_frame()
+            if registers and self.output_dir:
+                self._save_iterations(result, timestamp)
             now = chain_pose(self.prev_pose, result["pose"])
             self.prev_pose = now
             self.poses.append((timestamp, now))
@@ -737,7 +765,12 @@ class LaserOdometry:
                 savePoseToFile(now, self.pose_file, timestamp)
             if times:
                 times.step("2. Matching and solving in flat points")
-        self.ctx.map_push(filtered_cloud)
+        if not pushed:
+            nxt.map_push(filtered_cloud)
+        if nxt is not ctx:
+            if ctx.params.solve_method == _abi.IMLS_SOLVE_RANSAC:
+                nxt.set_rng_state(ctx.rng_state())      # one rand() stream across the frames
+            self._cur = 1 - self._cur
         self.frame_count += 1
         if times:
             times.total("Total time")

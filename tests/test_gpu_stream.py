@@ -140,6 +140,28 @@ def test_vlp16_stream_shipped_ransac_drpm(vlp_frames, tmp_path):
     _check_stream(run_gpu(frames, p, tmp_path, "ransac"), oracle_stream(frames, p, rand_state=st), 1e-5)
 
 
+@pytest.mark.parametrize("solver", ["LS", "RANSAC"])
+def test_pipelined_equals_one_context(vlp_frames, solver):
+    """LaserOdometry's pipelined mode (max_queue_size 1: two contexts alternate, each frame's scan
+    pushed to the other while it registers) gives the one-context loop's results bit for bit — the
+    same maps, the same kernels, and for RANSAC the rand() stream handed over between the contexts."""
+    p = config.params_from_config(config.load())
+    if solver == "LS":
+        p.solve_method = _abi.IMLS_SOLVE_LS
+    p.max_queue_size = 1
+    frames = vlp_frames[:6]
+    out = {}
+    for pipelined in (False, True):
+        with imls_icp.LaserOdometry(p, device=0, pipelined=pipelined) as lo:
+            assert lo.pipelined == pipelined
+            for filtered, flat in frames:
+                lo.process(filtered, flat)
+            out[pipelined] = list(lo.results)
+    assert len(out[False]) == len(out[True]) == len(frames) - 1
+    for (t0, p0, i0, s0), (t1, p1, i1, s1) in zip(out[False], out[True]):
+        assert (i0, s0) == (i1, s1) and np.array_equal(p0, p1)
+
+
 def test_device_fifo_equals_host_concatenation(hdl_frames):
     """a18: the map assembled in HBM by map_push (only the new scan uploaded) gives bit-identical
     registrations to set_target on the host-concatenated map, as the FIFO rolls over."""
