@@ -10,6 +10,7 @@
 //   correspondences, per source index (uncompacted): cs[N] = (x, valid), cd[N] = (y, ·),
 //                              cn[N] = (n, ·) float4 — source order is implicit in the index.
 #pragma once
+#include <cstddef>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <string>
@@ -203,6 +204,42 @@ struct PairDev {
     RansacFrame rf;                    // RANSAC scratch (solve_method RANSAC), else zero
     int recompute_normals;             // map normals (count mode) to compute into t.mnr before the batch
 };
+
+// The batched kernels' view of their frame's record.  A pointer loaded from the frame table is
+// generic to the compiler, so every access through it was a FLAT load — counted on vmcnt and lgkmcnt
+// alike, so consuming one also waits for the kernel's LDS traffic, and a flat load after an LDS store
+// it might alias waits for that store (k_knn_wave_b 181 vs k_knn_wave 166 µs per launch on config
+// B's pair, profiles/r05_flat/).  The table holds HBM pointers only: device_view loads each pointer
+// field as a global-address-space value, and the address-space inference turns every access through
+// it into a global load.  (Host code never sees the qualifier: it is defined for the device pass only.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define IMLS_GAS __attribute__((address_space(1)))
+#else
+#define IMLS_GAS
+#endif
+__device__ __forceinline__ const void* gfield(const void* base, size_t off) {
+    typedef const void IMLS_GAS* gvp;
+    return (const void*)*reinterpret_cast<const gvp*>(reinterpret_cast<const char*>(base) + off);
+}
+#define IMLS_GLOBAL_FIELD(A, pa, f) (A).f = (decltype((A).f))gfield((pa), offsetof(PairDev, f))
+__device__ __forceinline__ PairDev device_view(const PairDev* pa) {
+    PairDev A = *pa;
+    IMLS_GLOBAL_FIELD(A, pa, t.mpt); IMLS_GLOBAL_FIELD(A, pa, t.mnr); IMLS_GLOBAL_FIELD(A, pa, t.ipos);
+    IMLS_GLOBAL_FIELD(A, pa, t.nodes); IMLS_GLOBAL_FIELD(A, pa, t.tpt); IMLS_GLOBAL_FIELD(A, pa, t.tnr);
+    IMLS_GLOBAL_FIELD(A, pa, t.lkeys); IMLS_GLOBAL_FIELD(A, pa, t.qparams); IMLS_GLOBAL_FIELD(A, pa, t.mten);
+    IMLS_GLOBAL_FIELD(A, pa, t.tvn);
+    IMLS_GLOBAL_FIELD(A, pa, spt); IMLS_GLOBAL_FIELD(A, pa, snr); IMLS_GLOBAL_FIELD(A, pa, qperm);
+    IMLS_GLOBAL_FIELD(A, pa, cs); IMLS_GLOBAL_FIELD(A, pa, cd); IMLS_GLOBAL_FIELD(A, pa, cn);
+    IMLS_GLOBAL_FIELD(A, pa, lists); IMLS_GLOBAL_FIELD(A, pa, trace); IMLS_GLOBAL_FIELD(A, pa, stats);
+    IMLS_GLOBAL_FIELD(A, pa, fb_list); IMLS_GLOBAL_FIELD(A, pa, fb_count);
+    IMLS_GLOBAL_FIELD(A, pa, st.pose); IMLS_GLOBAL_FIELD(A, pa, st.delta); IMLS_GLOBAL_FIELD(A, pa, st.x0);
+    IMLS_GLOBAL_FIELD(A, pa, st.done); IMLS_GLOBAL_FIELD(A, pa, st.status); IMLS_GLOBAL_FIELD(A, pa, st.iters);
+    IMLS_GLOBAL_FIELD(A, pa, st.hist); IMLS_GLOBAL_FIELD(A, pa, st.coarse); IMLS_GLOBAL_FIELD(A, pa, st.cand_count);
+    IMLS_GLOBAL_FIELD(A, pa, st.cand_lo); IMLS_GLOBAL_FIELD(A, pa, st.cand_lo_row); IMLS_GLOBAL_FIELD(A, pa, st.cand_hi);
+    IMLS_GLOBAL_FIELD(A, pa, st.cand_hi_row); IMLS_GLOBAL_FIELD(A, pa, st.sel); IMLS_GLOBAL_FIELD(A, pa, st.partial1);
+    IMLS_GLOBAL_FIELD(A, pa, st.partial2); IMLS_GLOBAL_FIELD(A, pa, st.keys); IMLS_GLOBAL_FIELD(A, pa, st.trace);
+    return A;
+}
 
 // index.hip — two phases, so many frames' uploads and filters can be enqueued before one wait:
 // (A) filter_async: NaN filter + order-keeping compaction (kept: filtered → input index, nullable),

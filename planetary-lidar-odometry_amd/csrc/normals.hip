@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kNrmBlock) void k_map_normals(TreeView t, int K, do
 // batched (imls_register_frames): the maps of the frames flagged recompute_normals, grid y = frame
 template <int KC>
 __global__ __launch_bounds__(kNrmBlock) void k_map_normals_b(const PairDev* __restrict__ tab, int K, double r2) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if (!A.recompute_normals || (int)blockIdx.x * kNrmBlock >= A.t.M) return;
     map_normals_body<KC>(A.t, K, r2, const_cast<float4*>(A.t.mnr), (int)blockIdx.x);
 }

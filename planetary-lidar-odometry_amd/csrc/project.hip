@@ -2049,7 +2049,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const P
     int f, bx;
     batch_block(kp.xcd, f, bx);
     if (f >= npairs) return;
-    const PairDev A = tab[f];
+    const PairDev A = device_view(tab + f);
     if (use_qwave(kp, A.N) || bx >= knn_blocks_of(A.N, kp.packet)) return;
     float4* xref = xref_dev(A.lists, A.N);
     knn_wave_body<KL>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
@@ -2063,7 +2063,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave_b(const PairDev* __res
     int f, bx;
     batch_block(kp.xcd, f, bx);
     if (f >= npairs) return;
-    const PairDev A = tab[f];
+    const PairDev A = device_view(tab + f);
     if (!use_qwave(kp, A.N) || bx * (kWaveBlock / 64) >= A.N) return;
     float4* xref = xref_dev(A.lists, A.N);
     knn_qwave_body<KL>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists, wlist_of<KL>(A.lists, A.N),
@@ -2076,7 +2076,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish_b(const 
     int f, bx;
     batch_block(kp.xcd, f, bx);
     if (f >= npairs) return;
-    const PairDev A = tab[f];
+    const PairDev A = device_view(tab + f);
     if (bx >= wave_blocks_of(A.N)) return;
     finish_body<KL>(A.t, A.spt, A.snr, A.qperm, A.N, A.st.pose, A.st.done, kp, A.lists, wlist_of<KL>(A.lists, A.N), A.cs,
                     A.cd, A.cn, A.st.partial1, A.trace + it, A.stats, A.fb_list, A.fb_count, bx);
@@ -2084,7 +2084,7 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish_b(const 
 
 template <int KCAP>
 __global__ __launch_bounds__(kProjBlock) void k_project_lane_b(const PairDev* __restrict__ tab, KParams kp, int it) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     project_lane_body<KCAP>(A.t, A.spt, A.snr, A.fb_list, A.fb_count, A.N, A.st.pose, A.st.done, kp, A.cs, A.cd, A.cn,
                             A.st.partial1 + (size_t)wave_blocks_of(A.N) * kNormEq, A.trace + it, A.stats,
                             kFallbackBlocks);

@@ -348,7 +348,7 @@ __device__ __forceinline__ int frame_compact(const PairDev& A, int mode, double 
 }
 __global__ __launch_bounds__(kBlock) void k_compact_count_b(const PairDev* __restrict__ tab, int mode, double dist_thr,
                                                             double h2) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     Source src;
     CompactOut out;
     const int n = frame_compact(A, mode, dist_thr, h2, src, out);
@@ -360,7 +360,7 @@ __device__ __forceinline__ CompactPost frame_post(const PairDev& A, int mode, in
 }
 __global__ __launch_bounds__(1024) void k_compact_scan_b(const PairDev* __restrict__ tab, int mode, int correspond_number,
                                                          int it) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     const CompactPost P = frame_post(A, mode, correspond_number, it);
     if (compact_skip(P)) return;
     Source src;
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(1024) void k_compact_scan_b(const PairDev* __restri
 }
 __global__ __launch_bounds__(1024) void k_compact_one_b(const PairDev* __restrict__ tab, int mode, double dist_thr, double h2,
                                                         int correspond_number, int it) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     const CompactPost P = frame_post(A, mode, correspond_number, it);
     if (compact_skip(P)) return;
     Source src;
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(1024) void k_compact_one_b(const PairDev* __restric
 }
 __global__ __launch_bounds__(kBlock) void k_compact_scatter_b(const PairDev* __restrict__ tab, int mode, double dist_thr,
                                                               double h2) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     Source src;
     CompactOut out;
     const int n = frame_compact(A, mode, dist_thr, h2, src, out);
@@ -949,36 +949,36 @@ __global__ __launch_bounds__(NT) void k_ransac_hyp_b(const PairDev* __restrict__
     for (long long q = blockIdx.x; q < items; q += gridDim.x) {
         const int fr = __builtin_amdgcn_readfirstlane(sact[q % na]);
         const int h = (int)(q / na);
-        const PairDev A = tab[fr];
+        const PairDev A = device_view(tab + fr);
         const size_t c3 = 3 * (size_t)A.rf.cap;
         ransac_hyp_one<NT>(A.rf.all, A.rf.all + c3, A.rf.all + 2 * c3, *A.rf.cnt_all, A.rf.R, dist_thr, h);
     }
 }
 __global__ __launch_bounds__(64) void k_ransac_select_b(const PairDev* __restrict__ tab, int chunk, int max_iterations,
                                                         double min_pct) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if (*A.st.done || *A.rf.R.rdone) return;
     ransac_select_body(A.rf.cnt_all, A.rf.R, chunk, max_iterations, min_pct);
 }
 // trace of a RANSAC iteration as the oracle records it (n_valid = correspondences, n_kept = 0) —
 // LS / weighted-LS finals; the DRPM final writes it itself
 __global__ void k_ransac_trace_b(const PairDev* __restrict__ tab, int it) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if (threadIdx.x || !*A.rf.R.active) return;
     A.trace[it].n_valid = (unsigned long long)*A.rf.cnt_all;
     A.trace[it].n_kept = 0;
 }
 __global__ __launch_bounds__(256) void k_drpm_eig_b(const PairDev* __restrict__ tab) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     drpm_eig_body(A.st.partial1, solve_blocks_of(A.rf.cap), A.st, A.rf.Dv);
 }
 __global__ __launch_bounds__(kBlock) void k_drpm_noise_b(const PairDev* __restrict__ tab, double sp, double sn) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if ((int)blockIdx.x >= solve_blocks_of(A.rf.cap)) return;
     drpm_noise_body(frame_rows(A, 1, 1), A.rf.cap, A.st, A.rf.Dv, sp, sn);
 }
 __global__ __launch_bounds__(256) void k_drpm_final_b(const PairDev* __restrict__ tab, KParams kp, double threshold, int it) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     drpm_final_body(solve_blocks_of(A.rf.cap), A.st, A.rf.Dv, A.trace + it, kp, threshold, A.rf.cnt_all, A.rf.cnt_in, 1);
     ransac_trace_t0(A.rf.R, A.rf.cnt_all, A.trace + it);
 }

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(NT) void k_rows_pass1(Rows rows, int N, double* __r
 }
 // batched: every frame's RANSAC inlier rows (grid y = frame)
 __global__ __launch_bounds__(kBlock) void k_rows_pass1_b(const PairDev* __restrict__ tab, int weighted) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if ((int)blockIdx.x >= solve_blocks_of(A.rf.cap)) return;
     rows_pass1_body<kBlock>(frame_rows(A, 1, weighted), A.rf.cap, A.st.partial1);
 }
@@ -778,33 +778,33 @@ __device__ __forceinline__ bool frame_big(const PairDev& A, int src) { return sr
 
 __global__ __launch_bounds__(kSmallBlock) void k_solve_small_b(const PairDev* __restrict__ tab, KParams kp, int weighted,
                                                               int it) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if (A.N > kSmallRows) return;
     solve_small_body(frame_rows(A, 0, 0), A.N, A.st, A.trace + it, kp, weighted, 1);
 }
 __global__ __launch_bounds__(256) void k_solve_first_b(const PairDev* __restrict__ tab, KParams kp, int weighted, int it,
                                                        int src) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if (!frame_big(A, src)) return;
     solve_first_body(A.st.partial1, src ? solve_blocks_of(A.rf.cap) : pass1_blocks_of(A.N), A.st, A.trace + it, kp,
                      weighted, 1);
 }
 __global__ __launch_bounds__(kResidBlock) void k_resid_hist_b(const PairDev* __restrict__ tab, int src) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     const int N = frame_rows_n(A, src);
     const int nb = resid_blocks_of(N);
     if (!frame_big(A, src) || (int)blockIdx.x >= nb || *A.st.done) return;
     resid_hist_core(frame_rows(A, src, 0), N, A.st, nb, A.st.x0);
 }
 __global__ __launch_bounds__(kBlock) void k_collect_b(const PairDev* __restrict__ tab, int src) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     const int N = frame_rows_n(A, src);
     const int nb = collect_blocks_of(N);
     if (!frame_big(A, src) || (int)blockIdx.x >= nb) return;
     collect_body<kBlock>(frame_rows(A, src, 0), N, A.st, A.st.partial2, nb);
 }
 __global__ __launch_bounds__(kFinalBlock) void k_solve_final_b(const PairDev* __restrict__ tab, KParams kp, int it, int src) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if (!frame_big(A, src)) return;
     const int N = frame_rows_n(A, src);
     solve_final_body(frame_rows(A, src, 0), N, A.st, A.trace + it, A.st.partial2, collect_blocks_of(N), kp, 1);

@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256) void k_tv_tangent(int N, const int* __restrict
 }
 
 __global__ __launch_bounds__(256) void k_tv_tangent_b(const PairDev* __restrict__ tab) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if (A.t.M <= 0) return;
     tv_tangent_body(A.N, A.st.done, const_cast<double4*>(A.t.tvn), (int)(blockIdx.x * blockDim.x + threadIdx.x));
 }
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(kTvBlock) void k_tv_vote(TreeView t, const float4* 
 
 // batched (imls_register_frames): frame = tab[blockIdx.y], the same body
 __global__ __launch_bounds__(kTvBlock) void k_tv_vote_b(const PairDev* __restrict__ tab, KParams kp, int use_prev) {
-    const PairDev A = tab[blockIdx.y];
+    const PairDev A = device_view(tab + blockIdx.y);
     if (A.t.M <= 0 || (int)blockIdx.x * kTvWaves >= A.N) return;
     tv_vote_body(A.t, A.spt, A.N, A.st.pose, A.st.done, kp, const_cast<double4*>(A.t.tvn), use_prev, (int)blockIdx.x);
 }
