@@ -131,6 +131,35 @@ __device__ __forceinline__ double wave_total(double v) {
     return v;
 }
 
+// The wave's totals of 28 values per lane (a[28..31] = 0): recursive halving — at lane bit 2h each
+// lane keeps one half of its 2h values and adds the partner's copy of that half (32 fp64 exchanges,
+// where 28 wave_total reductions issue 168 DPP steps); lane 2k returns value k's total.  A fixed
+// association, shared by the solve kernels' normal-equation reductions (block_sum28 and block_normeq
+// of solve_common.h, k_collect); the projection kernels keep wave_total (their 64 extra VGPRs spill
+// the traversal's 96-register budget).
+__device__ __forceinline__ double xor_f64(double v, int m) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl_xor((int)(unsigned)(b & 0xffffffffll), m, 64);
+    const int hi = __shfl_xor((int)(unsigned)((unsigned long long)b >> 32), m, 64);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <int H>
+__device__ __forceinline__ void wave_halve(double (&a)[32], int lane) {
+    const bool up = (lane & (2 * H)) != 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        const double send = up ? a[i] : a[H + i];
+        const double keep = up ? a[H + i] : a[i];
+        a[i] = keep + xor_f64(send, 2 * H);
+    }
+    if constexpr (H > 1) wave_halve<H / 2>(a, lane);   // static indices at every level (no stack array)
+}
+__device__ __forceinline__ double wave_sum28(double (&a)[32]) {
+    const int lane = threadIdx.x & 63;
+    wave_halve<16>(a, lane);
+    return a[0] + xor_f64(a[0], 1);
+}
+
 // Solver scratch living in device memory (one per context).
 struct SolveState {
     double* pose;             // [16] current rPose

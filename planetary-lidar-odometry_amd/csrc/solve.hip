@@ -377,7 +377,7 @@ __device__ void final_block(const Rows& rows, int N, SolveState st, imls_iter_tr
     FSTAMP(3);
     if (threadIdx.x >= 64) return;
     double x[6], D[16];
-    solve6_wave(out, x);             // wave 0 (solve_common.h)
+    solve6_u(out, x);             // wave 0 (solve_common.h)
     if (threadIdx.x != 0) return;
     FSTAMP(4);
     delta_from_x(x, D);
@@ -425,9 +425,12 @@ __device__ __forceinline__ void collect_body(const Rows& rows, int N, const Solv
     }
     // block reduction of the 28 partial sums
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int k = 0; k < kNormEq; ++k) {
-        const double v = wave_total(acc[k]);
-        if (lane == 63) red[wv * kNormEq + k] = v;
+    {
+        double v[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) v[k] = k < kNormEq ? acc[k] : 0.0;
+        const double s = wave_sum28(v);      // internal.h
+        if (!(lane & 1) && (lane >> 1) < kNormEq) red[wv * kNormEq + (lane >> 1)] = s;
     }
     __syncthreads();
     if (threadIdx.x < kNormEq) {
@@ -594,7 +597,7 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     block_sum28<kSmallBlock>(loc, red, acc);
     DBG_STAMP(0);
     const double nvalid = acc[27];
-    if (t < 64) {                     // wave 0: the 6×6 solve by its 64 lanes (solve6_wave)
+    if (t < 64) {                     // wave 0: the 6×6 solve by its 64 lanes (solve6_u)
         double x[6];
         if (update_pose && nvalid < (double)kp.correspond_number) {   // laser_odometry.cpp:570-576
             if (t == 0) {
@@ -604,7 +607,7 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
                 stop = 1;
             }
         } else {
-            solve6_wave(acc, x);
+            solve6_u(acc, x);
             if (t == 0) {
                 if (weighted) {
                     double D[16];
@@ -727,7 +730,7 @@ __device__ __forceinline__ void solve_small_body(const Rows& rows, int N, const 
     DBG_STAMP(4);
     if (t >= 64) return;
     double x[6], D[16];
-    solve6_wave(acc, x);
+    solve6_u(acc, x);
     if (t != 0) return;
     DBG_STAMP(5);
     delta_from_x(x, D);

@@ -71,24 +71,19 @@ __device__ __forceinline__ double wave_sum(double v) {
 template <int NT>
 __device__ void block_normeq(const double a[6], double b, double cnt, double* red, double out[kNormEq]) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double v[32];
     int k = 0;
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int c = r; c < 6; ++c) {
-            const double v = wave_total(a[r] * a[c]);
-            if (lane == 63) red[wv * kNormEq + k] = v;
-            ++k;
-        }
+        for (int c = r; c < 6; ++c) v[k++] = a[r] * a[c];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-        const double v = wave_total(a[r] * b);
-        if (lane == 63) red[wv * kNormEq + 21 + r] = v;
-    }
-    {
-        const double v = wave_total(cnt);
-        if (lane == 63) red[wv * kNormEq + 27] = v;
-    }
+    for (int r = 0; r < 6; ++r) v[21 + r] = a[r] * b;
+    v[27] = cnt;
+#pragma unroll
+    for (int q = kNormEq; q < 32; ++q) v[q] = 0.0;
+    const double s = wave_sum28(v);
+    if (!(lane & 1) && (lane >> 1) < kNormEq) red[wv * kNormEq + (lane >> 1)] = s;
     __syncthreads();
     if (threadIdx.x < kNormEq) {
         double s = 0.0;
@@ -99,14 +94,16 @@ __device__ void block_normeq(const double a[6], double b, double cnt, double* re
 }
 
 // Block-sum 28 per-thread values (all threads call); result in out[0..27] (LDS) after the call.
+// Within a wave by wave_sum28 (internal.h): k_solve_small's two block sums 4.8 / 3.9 → 4.0 / 2.7 µs
+// on a 1949-row frame (28 wave_total reductions before).
 template <int NT>
 __device__ void block_sum28(const double (&v)[kNormEq], double* red, double* out) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double a[32];
 #pragma unroll
-    for (int k = 0; k < kNormEq; ++k) {
-        const double s = wave_total(v[k]);
-        if (lane == 63) red[wv * kNormEq + k] = s;
-    }
+    for (int k = 0; k < 32; ++k) a[k] = k < kNormEq ? v[k] : 0.0;
+    const double s = wave_sum28(a);
+    if (!(lane & 1) && (lane >> 1) < kNormEq) red[wv * kNormEq + (lane >> 1)] = s;
     __syncthreads();
     if (threadIdx.x < kNormEq) {
         double s = 0.0;
@@ -208,96 +205,90 @@ __device__ inline int solve6(const double* ne, double x[6]) {
     return rank;
 }
 
-// solve6 by one whole wave (all 64 lanes call it; every lane returns the same x and rank), element
-// (r, c) of the 6×6 system in lane 6r + c and g[r] in lane 36 + r: a pivot's row / column swap is one
-// lane permute, its column scale and trailing update one VALU operation each — where solve6's one
-// thread spends ~700 predicated selects on the swaps.  Every element sees exactly solve6's
-// operations in solve6's order (the update's product A[r][j]·A[c][j] is commutative, the upper
-// triangle is solve6's mirror copy), and the substitutions run on the same values, so x is solve6's
-// bit for bit.
-__device__ __forceinline__ double lane_f64(double v, int src) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __shfl((int)(unsigned)(b & 0xffffffffll), src, 64);
-    const int hi = __shfl((int)(unsigned)((unsigned long long)b >> 32), src, 64);
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-__device__ __forceinline__ double uni_f64(double v, int src) {   // wave-uniform read of lane src
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), src);
-    const int hi = __builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), src);
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-__device__ __forceinline__ int solve6_wave(const double* ne, double x[6]) {
-    const int lane = threadIdx.x & 63;
-    const int r = lane < 36 ? lane / 6 : (lane < 42 ? lane - 36 : 0), c = lane < 36 ? lane % 6 : 0;
-    const bool mat = lane < 36, rhs = lane >= 36 && lane < 42;
-    double a = 0.0;
-    if (mat) {
-        const int lo = r < c ? r : c, hi = r < c ? c : r;
-        a = ne[lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];       // upper-triangle row-major index of (lo, hi)
-    } else if (rhs) {
-        a = ne[21 + r];
+// solve6 with the pivot made wave-uniform (readfirstlane): the row / column swap of pivot p is a
+// scalar branch to one static swap (a few dozen moves), not solve6's ~700 predicated selects over
+// every candidate row, and not the one-wave form's chain of LDS permutes per pivot (element (r, c) in
+// lane 6r + c: 3.6 µs per solve vs 2.8 here, tools/frame_probe.py phases).  Every lane (or the one
+// calling lane) holds the whole system and performs exactly solve6's operations: x is solve6's bit for bit.
+__device__ __forceinline__ int solve6_u(const double* ne, double x[6]) {
+    double A[6][6], g[6];
+    int perm[6];
+    {
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = r; c < 6; ++c) { A[r][c] = ne[k]; A[c][r] = ne[k]; ++k; }
     }
-    int perm[6] = {0, 1, 2, 3, 4, 5};
+#pragma unroll
+    for (int r = 0; r < 6; ++r) { g[r] = ne[21 + r]; perm[r] = r; }
     const double eps = DBL_EPSILON;
     double maxpiv = 0.0;
     int rank = 6;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
         int p = j;
-        double best = uni_f64(a, 7 * j);
+        double best = A[j][j];
+#pragma unroll
+        for (int q = j + 1; q < 6; ++q)
+            if (A[q][q] > best) { best = A[q][q]; p = q; }
+        p = __builtin_amdgcn_readfirstlane(p);
 #pragma unroll
         for (int q = j + 1; q < 6; ++q) {
-            const double dq = uni_f64(a, 7 * q);
-            if (dq > best) { best = dq; p = q; }
-        }
-        if (p != j) {                                           // rows and columns j ↔ p
-            const int sr = r == j ? p : (r == p ? j : r), sc = c == j ? p : (c == p ? j : c);
-            a = lane_f64(a, mat ? 6 * sr + sc : (rhs ? 36 + sr : lane));
+            if (q == p) {                 // uniform: one taken branch per pivot
 #pragma unroll
-            for (int q = j + 1; q < 6; ++q)           // (constant indices: perm stays in registers)
-                if (q == p) { const int t = perm[j]; perm[j] = perm[q]; perm[q] = t; }
+                for (int c = 0; c < 6; ++c) { const double t = A[j][c]; A[j][c] = A[q][c]; A[q][c] = t; }
+#pragma unroll
+                for (int r = 0; r < 6; ++r) { const double t = A[r][j]; A[r][j] = A[r][q]; A[r][q] = t; }
+                const double t = g[j]; g[j] = g[q]; g[q] = t;
+                const int ti = perm[j]; perm[j] = perm[q]; perm[q] = ti;
+            }
         }
-        const double d = uni_f64(a, 7 * j);
+        const double d = A[j][j];
         const double rkk = d > 0 ? sqrt(d) : 0.0;
         if (rkk > maxpiv) maxpiv = rkk;
-        if (!(rkk > eps * 6.0 * maxpiv) || !(d > 0)) {
+        if (__builtin_amdgcn_readfirstlane((!(rkk > eps * 6.0 * maxpiv) || !(d > 0)) ? 1 : 0)) {
             rank = j;
             break;
         }
+        A[j][j] = rkk;
         const double inv = 1.0 / rkk;
-        if (lane == 7 * j) a = rkk;
-        if (mat && c == j && r > j) a = a * inv;
-        const double Lr = lane_f64(a, 6 * r + j), Lc = lane_f64(a, 6 * c + j);
-        if (mat && r > j && c > j) a = a - Lr * Lc;
+#pragma unroll
+        for (int r = j + 1; r < 6; ++r) A[r][j] = A[r][j] * inv;
+#pragma unroll
+        for (int r = j + 1; r < 6; ++r)
+#pragma unroll
+            for (int c = j + 1; c <= r; ++c) {
+                A[r][c] = A[r][c] - A[r][j] * A[c][j];
+                A[c][r] = A[r][c];
+            }
     }
-    // the substitutions of solve6 on the factor's values (wave-uniform)
     double y[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        if (i < rank) {
-            double s = uni_f64(a, 36 + i);
+    for (int r = 0; r < 6; ++r) {
+        if (r < rank) {
+            double s = g[r];
 #pragma unroll
-            for (int k = 0; k < i; ++k) s -= uni_f64(a, 6 * i + k) * y[k];
-            y[i] = s / uni_f64(a, 7 * i);
+            for (int c = 0; c < r; ++c) s -= A[r][c] * y[c];
+            y[r] = s / A[r][r];
         }
     }
 #pragma unroll
-    for (int i = 5; i >= 0; --i) {
-        if (i < rank) {
-            double s = y[i];
+    for (int r = 5; r >= 0; --r) {
+        if (r < rank) {
+            double s = y[r];
 #pragma unroll
-            for (int k = i + 1; k < 6; ++k)
-                if (k < rank) s -= uni_f64(a, 6 * k + i) * y[k];
-            y[i] = s / uni_f64(a, 7 * i);
+            for (int c = r + 1; c < 6; ++c)
+                if (c < rank) s -= A[c][r] * y[c];
+            y[r] = s / A[r][r];
         }
     }
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         double v = 0.0;
 #pragma unroll
-        for (int i = 0; i < 6; ++i)
-            if (i < rank && perm[i] == k) v = y[i];
+        for (int r = 0; r < 6; ++r)
+            if (r < rank && perm[r] == k) v = y[r];
         x[k] = v;
     }
     return rank;
@@ -401,7 +392,7 @@ __device__ void solve_first_block(const double* __restrict__ partial, int blocks
         return;
     }
     double x[6];
-    solve6_wave(acc, x);              // wave 0
+    solve6_u(acc, x);              // wave 0
     if (t != 0) return;
     if (weighted) {
         double D[16];
