@@ -313,6 +313,12 @@ __device__ inline void delta_from_x(const double x[6], double D[16]) {
     tmp = c1x * az; R[2] = tmp + sy; R[6] = tmp - sy;
     tmp = c1y * az; R[5] = tmp - sx; R[7] = tmp + sx;
     R[0] = c1x * ax + c; R[4] = c1y * ay + c; R[8] = c1z * az + c;
+    // A step that reproduces the iterate before last has entered a 2-cycle (an element alternating by
+    // an ulp: |Δ| ≥ 1e-16 forever — 35 % of small rotations run all 20 steps): the 20th iterate is
+    // then known from the parity of the steps left, bit for bit what the remaining steps would give
+    // (the cycle repeats its maxd and det, so neither exit fires in it).
+    double P[9];
+    bool have_prev = false;
     for (int it = 0; it < 20; ++it) {
         const double* a = R;
         const double det = a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) + a[2] * (a[3] * a[7] - a[4] * a[6]);
@@ -323,9 +329,23 @@ __device__ inline void delta_from_x(const double x[6], double D[16]) {
         // one division per step (its reciprocal scales the cofactors; round 5: was nine)
         const double rdet = 1.0 / det;
         double maxd = 0, n[9];
-        for (int k = 0; k < 9; ++k) { n[k] = 0.5 * (a[k] + cof[k] * rdet); maxd = fmax(maxd, fabs(n[k] - a[k])); }
-        for (int k = 0; k < 9; ++k) R[k] = n[k];
-        if (maxd < 1e-16) break;
+        bool cyc = have_prev;
+        for (int k = 0; k < 9; ++k) {
+            n[k] = 0.5 * (a[k] + cof[k] * rdet);
+            maxd = fmax(maxd, fabs(n[k] - a[k]));
+            cyc = cyc && __double_as_longlong(n[k]) == __double_as_longlong(P[k]);
+        }
+        if (maxd < 1e-16) {
+            for (int k = 0; k < 9; ++k) R[k] = n[k];
+            break;
+        }
+        if (cyc) {                    // n = the iterate before last: 19 − it steps remain
+            if ((19 - it) % 2 == 0)
+                for (int k = 0; k < 9; ++k) R[k] = n[k];
+            break;
+        }
+        for (int k = 0; k < 9; ++k) { P[k] = R[k]; R[k] = n[k]; }
+        have_prev = true;
     }
     for (int k = 0; k < 16; ++k) D[k] = 0.0;
     for (int r = 0; r < 3; ++r) for (int cc = 0; cc < 3; ++cc) D[r * 4 + cc] = R[r * 3 + cc];
