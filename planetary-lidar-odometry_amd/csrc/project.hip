@@ -1064,7 +1064,11 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
     if (skip) {
         // the list stays in place
     } else if (!greedy) {
-        // prefill: previous list re-measured at the new pose
+        // prefill: previous list re-measured at the new pose.  Its ≤ KL distinct points all fit, so
+        // inserting them one by one (the list empty, the bound r² until the last) leaves exactly
+        // those within r² in (key, position) order: a bitonic sort of the lanes gives that order in
+        // log²(KL)/2 exchange steps instead of KL dependent insertions (the re-traversing waves that
+        // set a steady iteration's launch time all start here)
         const int pos = lane < KL ? lists[(size_t)lane * N + slot] : -1;
         float d = kInfF;
         if (pos >= 0) {
@@ -1072,11 +1076,24 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
             const float ex = q.x - xf[0], ey = q.y - xf[1], ez = q.z - xf[2];
             d = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
         }
-        for (int k = 0; k < KL; ++k) {
-            const int cp = __builtin_amdgcn_readlane(pos, k);
-            const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), k));
-            if (cp >= 0 && c <= bnd && c < worst()) insert(c, cp);
+        const bool in = pos >= 0 && d <= bnd;
+        float sk = in ? d : kInfF;
+        int sp = in ? pos : -1;
+        constexpr int W = KL <= 32 ? 32 : 64;
+#pragma unroll
+        for (int size = 2; size <= W; size <<= 1) {
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                const float ok = __shfl_xor(sk, stride, 64);
+                const int op = __shfl_xor(sp, stride, 64);
+                const bool asc = (lane & size) == 0, low = (lane & stride) == 0;
+                const bool other_less = ok < sk || (ok == sk && op < sp);
+                const bool other_more = sk < ok || (sk == ok && sp < op);
+                if (asc == low ? other_less : other_more) { sk = ok; sp = op; }
+            }
         }
+        if (lane < KL) { lkey = sk; lpos = sp; }
+        bnd = fminf(r2s, worst());
     } else {
         // seed: the leaf of the query's own Morton key ± seed_half Morton neighbours
         const unsigned long long qk = morton48(xf[0], xf[1], xf[2], t.qparams);
