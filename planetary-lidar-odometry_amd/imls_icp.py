@@ -739,7 +739,10 @@ class LaserOdometry:
         pushed = False
         registers = self.frame_count != 0 and n_flat != 0 and ctx.n_target != 0
         if registers:
-            ctx.set_source(flat_cloud)                 # the flat cloud's upload: this path's preprocessing
+            # the flat cloud's upload: this path's preprocessing.  Count-less: the registration waits
+            # for the filter's count itself, so the host does not also wait here for the count and the
+            # kept-index download (one stream synchronisation fewer before the first launch)
+            ctx.set_source(flat_cloud, count=False)
         if times:
             times.frame(timestamp)
             times.step("1. Preprocessing")

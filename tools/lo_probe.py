@@ -16,6 +16,9 @@ p = config.bench_params(20)
 runner = bench.StreamRunner(1, p, 0, 0, frames_per_seq=6, fuse=False, unique=1, dev=None, resident=False, groups=1)
 fr = runner.seqs[0]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+if "counted" in sys.argv[2:]:          # A/B: the flat cloud loaded with its count (host waits for it)
+    _orig = imls_icp.ImlsContext.set_source
+    imls_icp.ImlsContext.set_source = lambda self, cloud, count=True: _orig(self, cloud, True)
 lat = []
 with imls_icp.LaserOdometry(p, device=0) as lo:
     for j in range(n + 3):
@@ -24,6 +27,6 @@ with imls_icp.LaserOdometry(p, device=0) as lo:
         lo.process(fr[k][0], fr[k][1])
         if j >= 3:
             lat.append((time.perf_counter() - t0) * 1e3)
-    print(f"LaserOdometry.process: median {np.median(lat):.3f} ms  p90 {np.percentile(lat, 90):.3f} ms "
+    print(f"LaserOdometry.process{' (counted)' if 'counted' in sys.argv[2:] else ''}: median {np.median(lat):.3f} ms  p90 {np.percentile(lat, 90):.3f} ms "
           f"(pipelined {lo.pipelined}, {len(fr[0][1])} queries vs {len(fr[0][0])}-pt scan)")
 runner.close()
