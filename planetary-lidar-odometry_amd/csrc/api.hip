@@ -914,9 +914,16 @@ int batch_builds(imls_ctx* L, imls_ctx* const* ctxs, size_t n, bool fused, HostS
             c->src_kept_out = nullptr;
             if (c->N > 0) {
                 if (!grow(c->qperm, (size_t)c->N * 4 + 16)) return fail(L, IMLS_ERR_DEVICE, "hipMalloc (source order)");
-                jobs.push_back(BuildJob{(const float4*)c->spt.p, nullptr, c->N, 0, nullptr, nullptr, nullptr,
-                                        (unsigned*)c->qperm.p, 0, 0});
-                who.push_back({c, 1});
+                if (n == 1 && c == L && c->N <= kSmallOrderN) {
+                    // a lone small frame: its source order in one launch (index.hip), not the
+                    // batched build's 6-8 — the same permutation
+                    if (int rc = small_source_order(L->stream, (const float4*)c->spt.p, c->N, (unsigned*)c->qperm.p, L->err))
+                        return fail(L, rc, L->err);
+                } else {
+                    jobs.push_back(BuildJob{(const float4*)c->spt.p, nullptr, c->N, 0, nullptr, nullptr, nullptr,
+                                            (unsigned*)c->qperm.p, 0, 0});
+                    who.push_back({c, 1});
+                }
             }
             if (int rc = ensure_solve(c, c->N)) return fail(L, rc, c->err);
         }

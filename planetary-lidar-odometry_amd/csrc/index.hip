@@ -448,8 +448,85 @@ void tree_rounds(hipStream_t s, const float4* mpt, int M, int B, int P, int leve
     }
 }
 
+namespace {
+// The source order of a small frame (≤ kSmallOrderN points) in ONE launch: the bbox and quantisation
+// (k_bbox_partial / k_bbox_final's min / max and arithmetic), the 48-bit Morton keys, and a bitonic
+// sort of (key, index) in LDS — the permutation the stable radix sort gives (equal keys keep index
+// order), where morton_perm / the batched build take 6-8 launches (a lone frame's critical path:
+// the source is ordered after its filter's count arrives, before the first traversal)
+__global__ __launch_bounds__(kSmallOrderN / 2) void k_small_order(const float4* __restrict__ pt, int n,
+                                                                unsigned* __restrict__ perm) {
+    constexpr int T = kSmallOrderN / 2;
+    __shared__ unsigned long long sk[kSmallOrderN];
+    __shared__ unsigned sv[kSmallOrderN];
+    __shared__ float red[6][T];
+    __shared__ float qp[4];
+    const int t = threadIdx.x;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    float4 p[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = t + u * T;
+        p[u] = i < n ? pt[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < n) {
+            lo[0] = fminf(lo[0], p[u].x); lo[1] = fminf(lo[1], p[u].y); lo[2] = fminf(lo[2], p[u].z);
+            hi[0] = fmaxf(hi[0], p[u].x); hi[1] = fmaxf(hi[1], p[u].y); hi[2] = fmaxf(hi[2], p[u].z);
+        }
+    }
+    for (int d = 0; d < 3; ++d) { red[d][t] = lo[d]; red[3 + d][t] = hi[d]; }
+    __syncthreads();
+    for (int st = T / 2; st > 0; st >>= 1) {
+        if (t < st)
+            for (int d = 0; d < 3; ++d) {
+                red[d][t] = fminf(red[d][t], red[d][t + st]);
+                red[3 + d][t] = fmaxf(red[3 + d][t], red[3 + d][t + st]);
+            }
+        __syncthreads();
+    }
+    if (t == 0) {                     // k_bbox_final's quantisation
+        const float ext = fmaxf(fmaxf(fmaxf(red[3][0] - red[0][0], red[4][0] - red[1][0]), red[5][0] - red[2][0]), 1e-6f);
+        qp[0] = red[0][0]; qp[1] = red[1][0]; qp[2] = red[2][0];
+        qp[3] = 65535.f / ext;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = t + u * T;
+        sk[i] = i < n ? morton48(p[u].x, p[u].y, p[u].z, qp) : ~0ull;
+        sv[i] = i < n ? (unsigned)i : ~0u;
+    }
+    __syncthreads();
+    for (int size = 2; size <= kSmallOrderN; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const int i = ((t & ~(stride - 1)) << 1) | (t & (stride - 1)), j = i + stride;
+            const unsigned long long ki = sk[i], kj = sk[j];
+            const unsigned vi = sv[i], vj = sv[j];
+            const bool gt = ki > kj || (ki == kj && vi > vj);
+            if (gt == ((i & size) == 0)) { sk[i] = kj; sk[j] = ki; sv[i] = vj; sv[j] = vi; }
+            __syncthreads();
+        }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = t + u * T;
+        if (i < n) perm[i] = sv[i];
+    }
+}
+}  // namespace
+
+int small_source_order(hipStream_t s, const float4* pts, int N, unsigned* perm, std::string& err) {
+    if (N <= 0) return IMLS_OK;
+    if (N > kSmallOrderN) { err = "small source order: too many points"; return IMLS_ERR_CAPACITY; }
+    k_small_order<<<1, kSmallOrderN / 2, 0, s>>>(pts, N, perm);
+    if (hipGetLastError() != hipSuccess) { err = "source order launch failed"; return IMLS_ERR_DEVICE; }
+    return IMLS_OK;
+}
+
 int source_order(hipStream_t s, int N, DevBuf& spt, DevBuf& scratch, DevBuf& qperm, std::string& err) {
     if (N <= 0) return IMLS_OK;
+    if (N <= kSmallOrderN) {
+        if (!ensure(qperm, (size_t)N * 4 + 16, err)) return IMLS_ERR_DEVICE;
+        return small_source_order(s, (const float4*)spt.p, N, (unsigned*)qperm.p, err);
+    }
     return morton_perm(s, (const float4*)spt.p, N, scratch, qperm, err);
 }
 

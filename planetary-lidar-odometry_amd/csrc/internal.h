@@ -293,6 +293,9 @@ int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& t
                       DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* P_out, int* levels_out,
                       std::string& err);
 int source_order(hipStream_t s, int N, DevBuf& spt, DevBuf& scratch, DevBuf& qperm, std::string& err);
+// a small frame's source order (≤ kSmallOrderN points) in one launch — the same permutation
+constexpr int kSmallOrderN = 2048;
+int small_source_order(hipStream_t s, const float4* pts, int N, unsigned* perm, std::string& err);
 // (B) for many frames at once, one launch sequence: each job a target tree (B > 0: lkeys [L + 2]
 // words, mpt [3·n] records, nodes [(P+1)·3] float4, sized by the caller; P / levels returned in the
 // job) or a source order (B = 0: perm [n]).  h_table: pinned host memory for the job table.
