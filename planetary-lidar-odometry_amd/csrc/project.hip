@@ -76,7 +76,7 @@ constexpr double kCertSlack = 1.0 + 4e-7;
 #define IMLS_B_KL 22
 #endif
 #ifndef IMLS_DIST_CHUNK
-#define IMLS_DIST_CHUNK 11
+#define IMLS_DIST_CHUNK 22
 #endif
 #ifndef IMLS_IMLS_CHUNK
 #define IMLS_IMLS_CHUNK 4
