@@ -131,6 +131,50 @@ def exchange_poses(results, world: int, rank: int = 0):
     return (seq, order, poses), sequences.chain_per_sequence(seq, order, poses)
 
 
+RANK_ROOF_FIELDS = ("algorithmic_bytes_per_step", "busy_projection_ms_per_step", "ms_per_step",
+                    "serialised_launch_ms", "algorithmic_bytes_per_launch")
+
+
+def rank_roofline(bytes_per_step: float, busy, busy_steps: int, per_step, probe, bytes_per_launch: float) -> list:
+    """This rank's roofline inputs (RANK_ROOF_FIELDS order): its own step's algorithmic bytes, the
+    time its projection kernels were busy per step (HIP-event union, busy pass; 0 without one), its
+    own mean timed step, and its serialised single-pair launch (k_knn_wave + k_finish, 0 without)."""
+    busy_ms = busy["projection_busy_ms"] / busy_steps if busy and busy_steps > 0 else 0.0
+    dom = 0.0
+    if probe:
+        kd = probe["kernel_avg_ms"]
+        dom = kd.get("k_knn_wave", 0.0) + kd.get("k_finish", 0.0)
+    return [float(bytes_per_step), float(busy_ms), float(np.mean(per_step) * 1e3) if len(per_step) else 0.0,
+            float(dom), float(bytes_per_launch)]
+
+
+def gather_rank_roofline(vals: list, world: int, dev) -> list:
+    """All-gather of every rank's rank_roofline() values (one collective, every rank calls it — before
+    any rank leaves main), expanded per rank with its achieved HBM GB/s and fraction of the peak: the
+    busy-pass figure (bytes per step / busy projection time) and the serialised single-pair one.
+    SURVEY §8(e): the per-GPU achieved HBM fraction of the multi-GPU run."""
+    import torch
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    if _grouped() and world > 1:
+        import torch.distributed as dist
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        rows = [o.cpu().tolist() for o in out]
+    else:
+        rows = [t.cpu().tolist()]
+    recs = []
+    for r, row in enumerate(rows):
+        d = dict(zip(RANK_ROOF_FIELDS, row), rank=r)
+        busy = d["busy_projection_ms_per_step"]
+        d["achieved"] = d["algorithmic_bytes_per_step"] / (busy / 1e3) / 1e9 if busy > 0 else None
+        d["frac"] = d["achieved"] / HBM_PEAK_GBS if d["achieved"] is not None else None
+        ser = d["serialised_launch_ms"]
+        d["serialised_achieved"] = d["algorithmic_bytes_per_launch"] / (ser / 1e3) / 1e9 if ser > 0 else None
+        d["serialised_frac"] = d["serialised_achieved"] / HBM_PEAK_GBS if ser > 0 else None
+        recs.append(d)
+    return recs
+
+
 # ------------------------------------------------------------------------------------------------
 # CPU baseline (oracle: test infrastructure, used here only as the timed reported baseline)
 # ------------------------------------------------------------------------------------------------
@@ -853,7 +897,9 @@ def main():
                          "scan + flat cloud per frame; A/B: each pair's map is a device FIFO of its scans, the newest "
                          "scan + the source cross PCIe per registration, SURVEY §8(d) t_pair)")
     ap.add_argument("--resident-inputs", action="store_true",
-                    help="B: inputs already resident in HBM (the default for B is the host hand-over: --host-inputs)")
+                    help="B: inputs already resident in HBM" + (" (the default for B is the host hand-over: "
+                         "--host-inputs)" if B_HOST_DEFAULT else " (already the default for B; the host "
+                         "hand-over is --host-inputs, and the headline line carries it as host_handover)"))
     ap.add_argument("--latency-pairs", type=int, default=50, help="single-pair latency / roofline probe size")
     ap.add_argument("--busy-steps", type=int, default=5, help="steps of the HIP-event busy-time pass (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
@@ -1049,6 +1095,10 @@ def main():
     busy = busy_pass(runner, args.busy_steps, torch.cuda.synchronize) if args.busy_steps > 0 else None
     trav = probe_ctx.traversal_stats()
     want_leg = args.workload == "B" and not args.host_inputs and not args.no_host_leg
+    # every rank's roofline inputs, gathered before ranks ≠ 0 leave (per-GPU fraction)
+    per_rank = gather_rank_roofline(
+        rank_roofline(bytes_per_step, busy, args.busy_steps, per_step, probe,
+                      (fb[0] / max(args.iters, 1)) if not stream and fb else 0.0), world, dev)
 
     def run_leg():
         # after the resident runner is closed: with its contexts (and their streams) alive, the leg's
@@ -1130,6 +1180,10 @@ def main():
         roof["frac"] = roof["achieved"] / HBM_PEAK_GBS
     else:
         roof.update(achieved=agg, frac=agg / HBM_PEAK_GBS)
+    roof["per_rank"] = per_rank
+    if world > 1:
+        fr = [d["frac"] for d in per_rank if d["frac"] is not None]
+        roof["per_rank_frac_min_max"] = [min(fr), max(fr)] if fr else None
     if probe:
         kd = probe["kernel_avg_ms"]
         dom_ms = kd["k_knn_wave"] + kd["k_finish"]

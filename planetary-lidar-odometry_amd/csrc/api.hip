@@ -30,6 +30,115 @@
 
 using namespace imlsgpu;
 
+// ---- device buffers: retire instead of free (internal.h devbuf_grow) ------------------------------
+namespace imlsgpu {
+namespace {
+struct Retired {
+    void* p;
+    size_t bytes;
+    int device;
+    std::vector<hipEvent_t> ev;       // one per stream that still had work when it was retired
+};
+std::mutex g_mem_mu;
+struct StreamRef {
+    hipStream_t s;
+    int device, refs;
+};
+std::vector<StreamRef> g_streams;
+std::vector<Retired> g_retired;
+
+bool retired_ready(Retired& r) {
+    for (size_t k = 0; k < r.ev.size(); ++k)
+        if (hipEventQuery(r.ev[k]) != hipSuccess) return false;
+    for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
+    r.ev.clear();
+    return true;
+}
+}  // namespace
+
+void register_stream(hipStream_t s, int device) {
+    if (!s) return;
+    std::lock_guard<std::mutex> lk(g_mem_mu);
+    for (auto& r : g_streams)
+        if (r.s == s) { ++r.refs; return; }
+    g_streams.push_back({s, device, 1});
+}
+
+void unregister_stream(hipStream_t s) {
+    if (!s) return;
+    std::lock_guard<std::mutex> lk(g_mem_mu);
+    for (size_t k = 0; k < g_streams.size(); ++k)
+        if (g_streams[k].s == s && --g_streams[k].refs == 0) {
+            g_streams.erase(g_streams.begin() + (long)k);
+            return;
+        }
+}
+
+void devbuf_retire(DevBuf& b) {
+    if (!b.p) return;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_mem_mu);
+    Retired r{b.p, b.bytes, dev, {}};
+    for (const auto& sr : g_streams) {
+        if (sr.device != dev || hipStreamQuery(sr.s) == hipSuccess) continue;   // idle: all its work has run
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess && hipEventRecord(e, sr.s) == hipSuccess) {
+            r.ev.push_back(e);
+        } else {
+            // no event to wait for (never expected): wait for that stream here instead
+            if (e) (void)hipEventDestroy(e);
+            (void)hipStreamSynchronize(sr.s);
+        }
+    }
+    g_retired.push_back(std::move(r));
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+bool devbuf_grow(DevBuf& b, size_t bytes, size_t alloc) {
+    if (b.bytes >= bytes) return true;
+    devbuf_retire(b);
+    alloc = std::max(alloc, bytes);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        // a retired buffer whose readers have all finished: the smallest that fits, at most 4× the size
+        std::lock_guard<std::mutex> lk(g_mem_mu);
+        long best = -1;
+        for (size_t k = 0; k < g_retired.size(); ++k) {
+            Retired& r = g_retired[k];
+            if (r.device != dev || r.bytes < alloc || r.bytes > 4 * alloc) continue;
+            if (best >= 0 && r.bytes >= g_retired[(size_t)best].bytes) continue;
+            if (retired_ready(r)) best = (long)k;
+        }
+        if (best >= 0) {
+            b.p = g_retired[(size_t)best].p;
+            b.bytes = g_retired[(size_t)best].bytes;
+            g_retired.erase(g_retired.begin() + best);
+            return true;
+        }
+    }
+    if (hipMalloc(&b.p, alloc) != hipSuccess) {
+        b.p = nullptr;
+        return false;
+    }
+    b.bytes = alloc;
+    return true;
+}
+
+void release_retired(int device) {
+    std::lock_guard<std::mutex> lk(g_mem_mu);
+    std::vector<Retired> keep;
+    for (auto& r : g_retired) {
+        if (r.device != device) { keep.push_back(std::move(r)); continue; }
+        for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
+        (void)hipFree(r.p);                                // teardown: hipFree waits for the device
+    }
+    g_retired.swap(keep);
+}
+}  // namespace imlsgpu
+
 constexpr int kTimingKinds = 8;   // projection, index, solve chain, k_knn_wave, k_finish, k_ring_pca, k_major_avg, front end
 
 // Runtime options of a context (imls_set_option; include/imls_gpu.h documents each): the validated
@@ -207,37 +316,22 @@ int fail(imls_ctx* c, int code, const std::string& m) {
     return code;
 }
 
-// Grow-only device buffers with 25 % headroom: per-frame sizes vary by a few percent, and every
-// reallocation is a hipFree, which waits for the whole device (it would stall the other contexts'
-// work in flight and the host).
-bool grow(DevBuf& b, size_t bytes) {
-    if (b.bytes >= bytes) return true;
-    // work already enqueued on non-blocking streams may still read the old buffer: let it finish
-    // before the memory is released (a free under a pending kernel faults the card)
-    if (b.p) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(b.p);
-    }
-    b.p = nullptr;
-    b.bytes = 0;
-    const size_t want = bytes + bytes / 4 + 256;
-    if (hipMalloc(&b.p, want) != hipSuccess) return false;
-    b.bytes = want;
-    return true;
-}
+// Grow-only device buffers with 25 % headroom: per-frame sizes vary by a few percent.  A replaced
+// buffer is retired, not freed (devbuf_grow below): no reallocation waits for the device.
+bool grow(DevBuf& b, size_t bytes) { return devbuf_grow(b, bytes, bytes + bytes / 4 + 256); }
 
-// grow keeping the first `keep` bytes (copied on stream s; the old buffer is freed once s is past it)
+// grow keeping the first `keep` bytes (copied on stream s, a registered stream: the old buffer is
+// retired behind the copy)
 bool grow_keep(DevBuf& b, size_t bytes, size_t keep, hipStream_t s) {
     if (b.bytes >= bytes) return true;
     if (!b.p || keep == 0) return grow(b, bytes);
     DevBuf nb;
     if (!grow(nb, bytes)) return false;
     if (hipMemcpyAsync(nb.p, b.p, std::min(keep, b.bytes), hipMemcpyDeviceToDevice, s) != hipSuccess) {
-        (void)hipFree(nb.p);
+        devbuf_retire(nb);
         return false;
     }
-    (void)hipDeviceSynchronize();
-    (void)hipFree(b.p);
+    devbuf_retire(b);
     b = nb;
     return true;
 }
@@ -724,8 +818,11 @@ int upload_soa6(imls_ctx* c, DevBuf& dst, const float* xyz, const float* nrm, si
     hipStream_t us = c->stream;
 #if IMLS_UPLOAD_STREAM
     if (!c->stage_pending[which]) {
-        if (!c->ustream && hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess)
-            return fail(c, IMLS_ERR_DEVICE, "hipStreamCreate (upload)");
+        if (!c->ustream) {
+            if (hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess)
+                return fail(c, IMLS_ERR_DEVICE, "hipStreamCreate (upload)");
+            register_stream(c->ustream, c->device);
+        }
         us = c->ustream;
     }
 #endif
@@ -1154,6 +1251,7 @@ imls_ctx* imls_create(int device, const imls_params* p) {
         return nullptr;
     }
     c->stream = c->own;
+    register_stream(c->own, device);
     if (hipHostMalloc((void**)&c->h_misc, 32 * sizeof(double)) != hipSuccess ||
         // coherent: the NaN filter's compaction kernel writes the kept counts here directly
         hipHostMalloc((void**)&c->h_cnt, 4 * sizeof(int), hipHostMallocCoherent) != hipSuccess) {
@@ -1213,8 +1311,16 @@ void imls_destroy(imls_ctx* c) {
     if (c->ftable.p) (void)hipFree(c->ftable.p);
     if (c->h_ftable) (void)hipHostFree(c->h_ftable);
     if (c->ev_build) (void)hipEventDestroy(c->ev_build);
-    if (c->ustream) (void)hipStreamDestroy(c->ustream);
-    if (c->own) (void)hipStreamDestroy(c->own);
+    if (c->stream && c->stream != c->own) unregister_stream(c->stream);
+    if (c->ustream) {
+        unregister_stream(c->ustream);
+        (void)hipStreamDestroy(c->ustream);
+    }
+    if (c->own) {
+        unregister_stream(c->own);
+        (void)hipStreamDestroy(c->own);
+    }
+    release_retired(c->device);
     delete c;
 }
 
@@ -1222,6 +1328,14 @@ int imls_set_params(imls_ctx* c, const imls_params* p) {
     if (!c) return IMLS_ERR_ARG;
     int rc = check_params(c, p);
     if (rc) return rc;
+    // the map FIFO's entries are held in the form of the mode they were pushed under (incremental
+    // index: filtered points + sorted runs, device scans not copied; concatenation: raw SoA6 copies):
+    // the mode may change only while the FIFO is empty
+    auto inc_mode = [](int q) { return q >= 2 && q < kMaxFifoRuns; };
+    if (c->rng_init && !c->fifo.empty() && inc_mode(c->P.max_queue_size) != inc_mode(p->max_queue_size))
+        return fail(c, IMLS_ERR_STATE, "max_queue_size " + std::to_string(c->P.max_queue_size) + " -> " +
+                                           std::to_string(p->max_queue_size) +
+                                           " changes the map FIFO's index mode while it holds scans: imls_map_clear first");
     if (!c->rng_init || p->ransac_seed != c->P.ransac_seed) {   // creation, or a new seed: restart the stream
         c->rng_init = true;
         ransac_seed_host(p->ransac_seed, c->rng_seed_state);
@@ -1338,7 +1452,13 @@ int imls_set_rng_state(imls_ctx* c, const int32_t state[34]) {
 
 int imls_set_stream(imls_ctx* c, void* s) {
     if (!c) return IMLS_ERR_ARG;
-    c->stream = s ? (hipStream_t)s : c->own;
+    hipStream_t ns = s ? (hipStream_t)s : c->own;
+    if (ns != c->stream) {
+        // a caller's stream joins the registry (its pending work may read this context's buffers)
+        if (ns != c->own) register_stream(ns, c->device);
+        if (c->stream != c->own) unregister_stream(c->stream);
+    }
+    c->stream = ns;
     return IMLS_OK;
 }
 
@@ -1560,6 +1680,7 @@ static int map_push(imls_ctx* c, const float* xyz, const float* nrm, size_t n, s
     sl.nk = -1;
     sl.sorted = false;
     const bool inc = fifo_incremental(c);
+    sl.id = -1;                           // a pooled slot's run id / run belong to its last use
     if (inc) {
         for (const auto& e : c->fifo)     // a scan indexed in place (max_queue_size was 1) is not held
             if (e.ghost && e.n > 0) return fail(c, IMLS_ERR_STATE, "map FIFO holds a scan pushed with max_queue_size 1 (not kept): push again");

@@ -205,13 +205,7 @@ int front_end_run(hipStream_t s, const imls_front_params& p, const float* xyz_ho
                                        (unsigned*)nullptr, n, 0, 7, s);
     const size_t nn = (size_t)n;
     const size_t need = 3 * nn * 4 + nn + nn * 4 + nn * 4 + 2 * nn * 16 + 4 * nn * 4 + nn * 4 + cub_bytes + 128 * 4 + 16 * 256;
-    if (mem.bytes < need) {
-        if (mem.p) (void)hipFree(mem.p);
-        mem.p = nullptr;
-        mem.bytes = 0;
-        if (hipMalloc(&mem.p, need + need / 4) != hipSuccess) { err = "hipMalloc (front end)"; return IMLS_ERR_DEVICE; }
-        mem.bytes = need + need / 4;
-    }
+    if (!devbuf_grow(mem, need, need + need / 4)) { err = "hipMalloc (front end)"; return IMLS_ERR_DEVICE; }
     char* q = (char*)mem.p;
     float* xyz = carve<float>(q, 3 * nn);
     unsigned char* ok = carve<unsigned char>(q, nn);

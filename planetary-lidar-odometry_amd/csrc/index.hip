@@ -21,21 +21,10 @@ T* carve(char*& p, size_t n) {
 }
 
 bool ensure(DevBuf& b, size_t bytes, std::string& err) {
-    if (b.bytes >= bytes) return true;
-    // kernels already enqueued may still use the old buffer (a free under them faults the card)
-    if (b.p) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(b.p);
-    }
-    b.p = nullptr;
-    b.bytes = 0;
-    size_t want = bytes + bytes / 4 + 4096;
-    if (hipMalloc(&b.p, want) != hipSuccess) {
-        err = "hipMalloc failed (" + std::to_string(want) + " bytes)";
-        return false;
-    }
-    b.bytes = want;
-    return true;
+    // a replaced buffer is retired behind the work that may still read it (internal.h devbuf_grow)
+    if (devbuf_grow(b, bytes, bytes + bytes / 4 + 4096)) return true;
+    err = "hipMalloc failed (" + std::to_string(bytes + bytes / 4 + 4096) + " bytes)";
+    return false;
 }
 
 __global__ void k_flag_finite(const float* __restrict__ soa, size_t n, unsigned* __restrict__ flag) {

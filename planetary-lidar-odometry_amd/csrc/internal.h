@@ -35,6 +35,21 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+// Grow-only device buffers (api.hip).  A buffer being replaced may still be read by work already
+// enqueued on any of the library's streams, and hipFree would wait for the whole device (every
+// context's work in flight, and the host).  So the old buffer is RETIRED instead: an event is
+// recorded on every registered stream of its device that still has work, and the buffer is handed
+// out again (to any grow of a size it fits) only once all of those events have completed; retired
+// buffers are freed at teardown (imls_destroy).  devbuf_grow(b, bytes, alloc): no-op when b holds
+// `bytes`, else b becomes a buffer of ≥ alloc bytes (alloc ≥ bytes: the caller's headroom).
+bool devbuf_grow(DevBuf& b, size_t bytes, size_t alloc);
+void devbuf_retire(DevBuf& b);         // b → retired (empty afterwards)
+// the streams the library enqueues on (context, upload and caller-set streams), reference counted
+void register_stream(hipStream_t s, int device);
+void unregister_stream(hipStream_t s);
+// teardown: free every retired buffer of `device` (hipFree waits for the device)
+void release_retired(int device);
+
 // Parameters the kernels need, in a flat POD copied by value into launches.
 struct KParams {
     double h2, r2, cos_thr;   // cos_thr = cos(angle_thr_deg · π/180): the angle gates' fast path

@@ -238,15 +238,7 @@ struct HostRng {
     }
 };
 
-bool grow_buf(DevBuf& b, size_t bytes) {
-    if (b.bytes >= bytes) return true;
-    if (b.p) (void)hipFree(b.p);
-    b.p = nullptr;
-    b.bytes = 0;
-    if (hipMalloc(&b.p, bytes) != hipSuccess) return false;
-    b.bytes = bytes;
-    return true;
-}
+bool grow_buf(DevBuf& b, size_t bytes) { return devbuf_grow(b, bytes, bytes); }
 
 }  // namespace
 

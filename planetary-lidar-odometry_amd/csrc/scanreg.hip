@@ -305,13 +305,7 @@ int ring_pca_run(hipStream_t s, const imls_pca_params& p, const float* xyz, size
            o_nrm = align256(o_idx + nn * 4), o_ev = align256(o_nrm + nn * 12), o_evec = align256(o_ev + nn * 12),
            o_feat = align256(o_evec + nn * 36), o_flc = align256(o_feat + nn * 32), o_cnt = align256(o_flc + nn),
            o_cub = align256(o_cnt + 16), total = align256(o_cub + cub_bytes);
-    if (mem.bytes < total) {
-        if (mem.p) (void)hipFree(mem.p);
-        mem.p = nullptr;
-        mem.bytes = 0;
-        if (hipMalloc(&mem.p, total) != hipSuccess) { err = "hipMalloc (pca scratch)"; return IMLS_ERR_DEVICE; }
-        mem.bytes = total;
-    }
+    if (!devbuf_grow(mem, total, total)) { err = "hipMalloc (pca scratch)"; return IMLS_ERR_DEVICE; }
     char* m = (char*)mem.p;
     std::vector<float4> h(nn);
     for (int k = 0; k < n; ++k) h[k] = make_float4(xyz[k * stride], xyz[k * stride + 1], xyz[k * stride + 2], 0.f);

@@ -721,6 +721,17 @@ class LaserOdometry:
     def pipelined(self) -> bool:
         return len(self._ctxs) == 2
 
+    @property
+    def contexts(self) -> tuple:
+        """Every context this driver registers on (two in pipelined mode, which alternate frame by
+        frame).  `.ctx` is only the context of the current / last frame: a setting made through it
+        reaches every other frame only, so apply settings to all of them (`apply`)."""
+        return tuple(self._ctxs)
+
+    def apply(self, fn):
+        """fn(ctx) for every context (set_option, enable_stats, set_defer, kernel timing …)."""
+        return [fn(c) for c in self._ctxs]
+
     def __enter__(self):
         return self
 
@@ -747,6 +758,8 @@ class LaserOdometry:
             times.frame(timestamp)
             times.step("1. Preprocessing")
         if self.frame_count != 0:
+            if times:
+                times.tic()                            # laser_odometry.cpp:482: step 2 starts here
             if not registers:
                 # in_cloud / the map is empty: the first iteration's gate breaks with rPose = I (570-576)
                 result = dict(pose=np.eye(4), iters=0, status=_abi.IMLS_FRAME_TOO_FEW, trace=[])
@@ -792,10 +805,13 @@ class LaserOdometry:
 
 
 class TimesLog:
-    """TicToc::tocAndLog (tic_toc.h:28-38) as processData uses it (laser_odometry.cpp:418-420,
-    461-475, 660, 677): two clocks started together (t_whole, t_step); a step line is the time since
-    t_step started (tocAndLog does not restart it, so "2." includes "1."), `<step>: <ms> ms` with
-    std::fixed and 3 decimals, appended to <dir>/laser_odometry_times.txt."""
+    """TicToc::tocAndLog (tic_toc.h:28-38) as processData uses it (laser_odometry.cpp:418-420, 430,
+    461-475, 482, 660, 677): two clocks started together (t_whole, t_step); t_step restarts (tic) at
+    the start of step 1 and again at the start of step 2 (482), so "2." excludes "1."; a step line
+    is the time since t_step's last tic, `<step>: <ms> ms` with std::fixed and 3 decimals, appended
+    to <dir>/laser_odometry_times.txt.  One difference in what is inside step 2: in LaserOdometry's
+    pipelined mode the next map's push (accumulateTargetCloud, 663-664) runs beside the registration,
+    so its host work falls inside the step-2 interval (the reference times it after step 2)."""
 
     FILE = "laser_odometry_times.txt"
 
@@ -809,6 +825,9 @@ class TimesLog:
     def _append(self, line: str):
         with open(self.path, "a") as f:
             f.write(line + "\n")
+
+    def tic(self):
+        self.t_step = self._now()
 
     def frame(self, timestamp: str):
         self._append(f"Frame time: {timestamp}")

@@ -51,7 +51,13 @@ def _worker(rank, world, port, steps, q):
     elapsed, per, out = bench.timed_steps(step, steps, world, dev)
     # this rank's units form one sequence (seq 0 locally), in step order
     recs, trajs = bench.exchange_poses([(0, k, o[0]) for k, o in enumerate(out)], world, rank)
-    q.put((rank, elapsed, sum(per), recs, {s: (o.tolist(), t) for s, (o, t) in trajs.items()}))
+    # the per-rank roofline inputs (bench.main gathers them before ranks != 0 return): rank-specific
+    # synthetic busy pass / probe so the gathered rows are checkable
+    busy = {"projection_busy_ms": 2.0 * (rank + 1) * steps}
+    probe = {"kernel_avg_ms": {"k_knn_wave": 0.1 * (rank + 1), "k_finish": 0.05}}
+    vals = bench.rank_roofline(1e9 * (rank + 1), busy, steps, per, probe, 5e7)
+    roof = bench.gather_rank_roofline(vals, world, dev)
+    q.put((rank, elapsed, sum(per), recs, {s: (o.tolist(), t) for s, (o, t) in trajs.items()}, roof))
     dist.destroy_process_group()
 
 
@@ -75,7 +81,17 @@ def test_bench_dist_path_gloo_world2():
     elapsed = [t[1] for t in res]
     assert elapsed[0] == elapsed[1]                          # max over ranks, identical on every rank
     assert all(elapsed[0] >= t[2] for t in res)              # ≥ each rank's own time in its steps
-    for _, _, _, (seq, order, poses), trajs in res:
+    for r, (_, _, _, _, _, roof) in enumerate(res):
+        assert [d["rank"] for d in roof] == list(range(world))          # every rank's row, on every rank
+        for k, d in enumerate(roof):
+            assert d["algorithmic_bytes_per_step"] == 1e9 * (k + 1)
+            assert d["busy_projection_ms_per_step"] == 2.0 * (k + 1)
+            assert abs(d["achieved"] - 1e9 * (k + 1) / (2e-3 * (k + 1)) / 1e9) < 1e-6   # 500 GB/s
+            assert abs(d["frac"] - d["achieved"] / 8000.0) < 1e-12          # bench.HBM_PEAK_GBS
+            assert abs(d["serialised_launch_ms"] - (0.1 * (k + 1) + 0.05)) < 1e-12
+            assert d["serialised_frac"] > 0 and d["ms_per_step"] > 0
+        assert roof == res[0][5]                                         # identical on both ranks
+    for _, _, _, (seq, order, poses), trajs, _ in res:
         assert np.array_equal(poses, want)
         assert list(seq) == [r << 20 for r in range(world) for _ in range(steps)]
         assert list(order) == [k for _ in range(world) for k in range(steps)]

@@ -24,7 +24,7 @@ step bench_stream_host 300 python3 bench.py --workload stream --no-cpu --host-in
 step bench_B_q2000 400 python3 bench.py --queries 2000
 fi
 if [ $P2 = 1 ]; then
-step bench_stream_ransac 400 python3 bench.py --workload stream --no-cpu --solver RANSAC_DRPM
+step bench_stream_ransac 500 python3 bench.py --workload stream --solver RANSAC_DRPM
 step bench_A 400 python3 bench.py --workload A
 step bench_A_ransac 400 python3 bench.py --workload A --solver RANSAC_DRPM
 step bench_E 500 python3 bench.py --workload E
