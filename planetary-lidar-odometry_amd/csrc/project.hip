@@ -50,7 +50,9 @@ __device__ __forceinline__ int ld_const(const int* p) { return *(const __attribu
 __device__ __forceinline__ double ld_const(const double* p) { return *(const __attribute__((address_space(4))) double*)p; }
 constexpr int kFallbackBlocks = 64;
 constexpr int kFallbackBlocksBatched = 4;   // physical blocks per frame of a large batch (same slabs)
-static_assert(kWaveBlock == kPass1Block && kFallbackBlocks == kPass1Fallback, "pass-1 slab layout (solve.hip)");
+// queries per k_finish block = per pass-1 slab (the quad exact stage: 64; the one-lane form: 256)
+constexpr int kFinishPerBlock = IMLS_FINISH_QUAD ? kWaveBlock / 4 : kWaveBlock;
+static_assert(kFinishPerBlock == kPass1Block && kFallbackBlocks == kPass1Fallback, "pass-1 slab layout (solve.hip)");
 constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
 constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
 constexpr int kFStack = 256;        // frontier traversal's stack per wave (see knn_qwave_body)
@@ -1489,6 +1491,382 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
 }
 
 // =============================================================================================
+// Exact stage, one QUAD per query (round 6, the large frames' k_finish): 4 lanes per query, list
+// entry j in lane j & 3, slot j >> 2 (S = ⌈KL/4⌉ slots per lane).  The one-lane form ran ~12
+// dependent round trips per lane (list → 22 point gathers → sort → NN-1 normal → 3 normal chunks →
+// up to 6 IMLS point + normal chunks → store) with ≤ 1.9 waves per SIMD resident; here every
+// entry's point AND normal are gathered once, together (one round trip after the list), and stay in
+// the lanes: 44 gathers per query instead of ~83, 4× the waves.  Cross-lane work uses quad DPP
+// permutes (VALU, no LDS).  Same values as finish_body / finish_query, bit for bit:
+//   * order: the traversal writes the list by ascending fp32 key, which is nearly the exact (d²,
+//     index) order — one adjacency check (entry j vs j + 1) certifies it; a wave with a misordered
+//     pair (near-equal keys: slot-id keys drop 5 mantissa bits) sorts its quads by odd-even
+//     transposition across the lanes and re-gathers (rare);
+//   * count within r, NN-1 (first entry in order with d² > DBL_EPSILON), the K-th, the certificate,
+//     the gates, target = L[|S| − 1] (Q3), and the IMLS sums accumulated in list order (each
+//     term broadcast from its lane in turn) — the reference's evaluation order;
+//   * pass-1 slab per block of 64 queries: each quad's row split over its lanes (7 of the 28 terms
+//     each), reduced over the wave's quads (DPP row shifts + two xor exchanges) and the 4 waves.
+// Deferred (uncertified) queries: the block is one 64-slot region of fb_list (slot order), as the
+// one-lane kernel's waves were.
+// =============================================================================================
+constexpr int kQuadSwap1 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int kQuadSwap2 = 0x4E;   // [2,3,0,1]
+constexpr int kQuadRev = 0x1B;     // [3,2,1,0]
+constexpr int kQuadNext = 0x39;    // [1,2,3,0]
+template <int CTRL>
+__device__ __forceinline__ int qperm_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true); }
+template <int CTRL>
+__device__ __forceinline__ float qperm_f(float v) { return __int_as_float(qperm_i<CTRL>(__float_as_int(v))); }
+template <int CTRL>
+__device__ __forceinline__ double qperm_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = qperm_i<CTRL>((int)(unsigned)(unsigned long long)b);
+    const int hi = qperm_i<CTRL>((int)(unsigned)((unsigned long long)b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+// a value held by one lane of the quad (zero bits in the others) → every lane of the quad
+__device__ __forceinline__ int quad_or(int v) {
+    v |= qperm_i<kQuadSwap1>(v);
+    return v | qperm_i<kQuadSwap2>(v);
+}
+__device__ __forceinline__ double quad_or_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = quad_or((int)(unsigned)(unsigned long long)b);
+    const int hi = quad_or((int)(unsigned)((unsigned long long)b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ int quad_sum(int v) {
+    v += qperm_i<kQuadSwap1>(v);
+    return v + qperm_i<kQuadSwap2>(v);
+}
+__device__ __forceinline__ int quad_min(int v) {
+    v = min(v, qperm_i<kQuadSwap1>(v));
+    return min(v, qperm_i<kQuadSwap2>(v));
+}
+
+constexpr int kFinishQ = kWaveBlock / 4;   // queries per quad-kernel block (= one pass-1 slab, one fb region)
+#define IMLS_FINISH4_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 26 ? 4 : 2)))
+
+template <int KL>
+__device__ __forceinline__ void finish4_body(TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr,
+                                             const unsigned* __restrict__ qperm, int N, const double* __restrict__ pose,
+                                             const int* __restrict__ done, KParams kp, const int* __restrict__ lists,
+                                             const float* __restrict__ wlist, float4* __restrict__ cs,
+                                             float4* __restrict__ cd, float4* __restrict__ cn,
+                                             double* __restrict__ partial1, imls_iter_trace* __restrict__ tr,
+                                             unsigned long long* __restrict__ nbr_stats, unsigned* __restrict__ fb_list,
+                                             unsigned* __restrict__ fb_count, int bx) {
+    if (done && ld_const(done)) return;
+    constexpr int S = (KL + 3) / 4;
+    __shared__ double red[kWaveBlock / 64][kNormEq];
+    __shared__ unsigned rej_s[IMLS_NUM_REJ + 3];
+    __shared__ unsigned fbc[kWaveBlock / 64];
+    const int tid = threadIdx.x, lane = tid & 63, g = lane & 3, wv = tid >> 6;
+    if (tid < IMLS_NUM_REJ + 3) rej_s[tid] = 0;
+    __syncthreads();
+    const int slot = bx * kFinishQ + (tid >> 2);
+    const bool active = slot < N;              // quad-uniform
+    const int i = active ? (int)qperm[slot] : 0;
+    float xf[3] = {0.f, 0.f, 0.f}, yf[3] = {0.f, 0.f, 0.f}, nf[3] = {0.f, 0.f, 0.f};
+    double ns[3] = {0.0, 0.0, 0.0};
+    int cat = -2, kq = 0, i1 = -1;
+    if (active) {
+        const float4 sp4 = spt[i], sn4 = snr[i];
+        int pos[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int j = g + 4 * s;
+            const int v = lists[(size_t)min(j, KL - 1) * N + slot];
+            pos[s] = j < KL ? v : -1;
+        }
+        const float W = wlist[slot];
+        transform_query(pose, sp4, sn4, kp.transform_normal, xf, ns);
+        const double xd[3] = {xf[0], xf[1], xf[2]};
+        // every entry's point and normal in one round trip (pinned: not sunk into their uses)
+        float4 pt[S], nm[S];
+        auto gather = [&]() {
+#pragma unroll
+            for (int s = 0; s < S; ++s) pt[s] = t.mpt[max(pos[s], 0)];
+            if (!kp.matcher) {
+#pragma unroll
+                for (int s = 0; s < S; ++s) nm[s] = t.mnr[max(pos[s], 0)];
+            } else {
+#pragma unroll
+                for (int s = 0; s < S; ++s) nm[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                pin_loaded(pt[s]);
+                pin_loaded(nm[s]);
+            }
+        };
+        gather();
+        double ed[S];
+        int eid[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            ed[s] = pos[s] >= 0 ? exact_d2(xd, pt[s].x, pt[s].y, pt[s].z) : kInfD;
+            eid[s] = pos[s] >= 0 ? (int)__float_as_uint(pt[s].w) : 0x7fffffff;   // libnabo's tie order
+        }
+        // order check: entry j = (g, s) against j + 1 = (g + 1, s), or (0, s + 1) for g = 3
+        bool bad = false;
+        {
+            double rd[S];
+            int ri[S];
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                rd[s] = qperm_d<kQuadNext>(ed[s]);
+                ri[s] = qperm_i<kQuadNext>(eid[s]);
+            }
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                double nd = rd[s];
+                int ni = ri[s];
+                if (g == 3) {
+                    nd = s + 1 < S ? rd[s + 1 < S ? s + 1 : 0] : kInfD;
+                    ni = s + 1 < S ? ri[s + 1 < S ? s + 1 : 0] : 0x7fffffff;
+                }
+                bad |= lessp(nd, ni, ed[s], eid[s]);
+            }
+        }
+        if (__ballot(bad)) {
+            // odd-even transposition across the quad's entries until a pass swaps nothing, then the
+            // moved entries' points and normals are gathered again
+            bool swapped = true;
+            while (__ballot(swapped)) {
+                swapped = false;
+                // even phase: (4s, 4s+1), (4s+2, 4s+3) — partner lane g ^ 1, same slot
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const double od = qperm_d<kQuadSwap1>(ed[s]);
+                    const int oi = qperm_i<kQuadSwap1>(eid[s]), op = qperm_i<kQuadSwap1>(pos[s]);
+                    const bool lower = (g & 1) == 0;
+                    const bool take = lower ? lessp(od, oi, ed[s], eid[s]) : lessp(ed[s], eid[s], od, oi);
+                    if (take) { ed[s] = od; eid[s] = oi; pos[s] = op; }
+                    swapped |= take;
+                }
+                // odd phase: (4s+1, 4s+2) lanes 1 ↔ 2, and (4s+3, 4s+4) lane 3 slot s ↔ lane 0 slot s+1
+                double rd[S];
+                int ri[S], rp[S];
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    rd[s] = qperm_d<kQuadRev>(ed[s]);
+                    ri[s] = qperm_i<kQuadRev>(eid[s]);
+                    rp[s] = qperm_i<kQuadRev>(pos[s]);
+                }
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    double od = rd[s];
+                    int oi = ri[s], op = rp[s];
+                    bool has = g == 1 || g == 2;
+                    if (g == 3 && s + 1 < S) { od = rd[s + 1 < S ? s + 1 : 0]; oi = ri[s + 1 < S ? s + 1 : 0]; op = rp[s + 1 < S ? s + 1 : 0]; has = true; }
+                    if (g == 0 && s > 0) { od = rd[s > 0 ? s - 1 : 0]; oi = ri[s > 0 ? s - 1 : 0]; op = rp[s > 0 ? s - 1 : 0]; has = true; }
+                    const bool lower = g == 1 || g == 3;
+                    const bool take = has && (lower ? lessp(od, oi, ed[s], eid[s]) : lessp(ed[s], eid[s], od, oi));
+                    if (take) { ed[s] = od; eid[s] = oi; pos[s] = op; }
+                    swapped |= take;
+                }
+            }
+            gather();
+        }
+        const double r2 = kp.r2;
+        const int K = kp.K;
+        int cr = 0, j1 = 0x7fffffff;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const bool in = ed[s] <= r2;
+            cr += in ? 1 : 0;
+            if (in && ed[s] > DBL_EPSILON) j1 = min(j1, g + 4 * s);
+        }
+        const int cnt_r = quad_sum(cr);
+        j1 = quad_min(j1);
+        // entry j's values, from its lane (the others contribute zero bits)
+        auto pick_d = [&](const double (&v)[S], int j) -> double {
+            double m = 0.0;
+#pragma unroll
+            for (int s = 0; s < S; ++s) m = (j == g + 4 * s) ? v[s] : m;
+            return quad_or_d(m);
+        };
+        auto pick_i = [&](const int (&v)[S], int j) -> int {
+            int m = 0;
+#pragma unroll
+            for (int s = 0; s < S; ++s) m = (j == g + 4 * s) ? v[s] : m;
+            return quad_or(m);
+        };
+        const bool has1 = j1 != 0x7fffffff;
+        const double d1 = has1 ? pick_d(ed, j1) : kInfD;
+        const int p1 = has1 ? pick_i(pos, j1) : -1;
+        i1 = has1 ? j1 : -1;
+        const double dK = pick_d(ed, K - 1);
+        const bool full = W < kInfF;
+        double need = cnt_r >= K ? dK : r2;
+        bool cert = true;
+        if (full) {
+            if (i1 < 0) cert = false;
+            else need = fmax(need, d1);
+            cert = cert && (need < (double)W / kCertSlack);
+        }
+        if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_OPT_FORCE_FALLBACK)
+        if (!cert) {
+            cat = -3;
+            // the exact re-run's search ball: the list's own bound (finish_body)
+            const double lb = i1 < 0 ? r2 : fmax(cnt_r >= K ? dK : r2, d1);
+            if (g == 0) cs[i] = make_float4(0.f, 0.f, 0.f, (float)(fmin(lb, r2) * (1.0 + 1e-6)));
+        } else if (kp.matcher) {
+            cat = finish_plane(xf, ns, p1, t, kp, yf, nf);
+        } else {
+            // finish_query over L = entries 0 … cnt−1 (imls_icp.cpp:612-729)
+            const int cnt = min(K, cnt_r);
+            double nn[3] = {0.0, 0.0, 0.0};
+            cat = -1;
+            if (p1 < 0 || d1 > kp.h2) {
+                cat = IMLS_REJ_TOO_FAR;                             // imls_icp.cpp:612-625 (Q18)
+            } else if (kp.tv) {
+                const double4 v = t.tvn[i];
+                if (v.w == 0.0) cat = IMLS_REJ_NO_NORMAL;
+                nn[0] = v.x; nn[1] = v.y; nn[2] = v.z;
+            } else if (!kp.get_normals) {
+                cat = IMLS_REJ_INVALID_NORMAL;
+            } else {
+                float m0 = 0.f, m1 = 0.f, m2 = 0.f;
+#pragma unroll
+                for (int s = 0; s < S; ++s)
+                    if (j1 == g + 4 * s) { m0 = nm[s].x; m1 = nm[s].y; m2 = nm[s].z; }
+                nn[0] = __int_as_float(quad_or(__float_as_int(m0)));
+                nn[1] = __int_as_float(quad_or(__float_as_int(m1)));
+                nn[2] = __int_as_float(quad_or(__float_as_int(m2)));
+            }
+            if (cat == -1 && !(isfinite(nn[0]) && isfinite(nn[1]) && isfinite(nn[2]))) cat = IMLS_REJ_INVALID_NORMAL;
+            if (cat == -1 && kp.angle_on && angle_reject(ns, nn[0], nn[1], nn[2], kp.angle_thr_deg, kp.cos_thr))
+                cat = IMLS_REJ_NORMAL_CONSTRAINT;
+            if (cat == -1) {
+                kq = cnt;
+                bool ok[S];
+                int na = 0;
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const bool inl = g + 4 * s < cnt;
+                    bool o = inl && kp.get_normals && isfinite(nm[s].x) && isfinite(nm[s].y) && isfinite(nm[s].z);
+                    if (o && kp.angle_on) o = !angle_reject(ns, nm[s].x, nm[s].y, nm[s].z, kp.angle_thr_deg, kp.cos_thr);
+                    ok[s] = o;
+                    na += o ? 1 : 0;
+                }
+                const int nacc = quad_sum(na);
+                if (nacc < 3) {
+                    cat = IMLS_REJ_MLS_FAIL;                        // imls_icp.cpp:463-466
+                } else {
+                    const double hmax = sqrt(pick_d(ed, nacc - 1)) / 3;   // Q3: L[|S| − 1]
+                    const double ih2 = 1.0 / (hmax * hmax);             // as finish_query
+                    double w[S], pr[S];
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        const double dx = xd[0] - (double)pt[s].x, dy = xd[1] - (double)pt[s].y, dz = xd[2] - (double)pt[s].z;
+                        double dn = dx * dx;
+                        dn = dn + dy * dy;
+                        dn = dn + dz * dz;
+                        const double ww = exp(-dn * ih2);
+                        double p = (ww * dx) * (double)nm[s].x;
+                        p = p + (ww * dy) * (double)nm[s].y;
+                        p = p + (ww * dz) * (double)nm[s].z;
+                        w[s] = ok[s] ? ww : 0.0;
+                        pr[s] = ok[s] ? p : 0.0;
+                    }
+                    // Σ in list order (entry j = lane j & 3, slot j >> 2), as finish_query accumulates
+                    double wsum = 0.0, psum = 0.0;
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        wsum += qperm_d<0x00>(w[s]);
+                        psum += qperm_d<0x00>(pr[s]);
+                        wsum += qperm_d<0x55>(w[s]);
+                        psum += qperm_d<0x55>(pr[s]);
+                        wsum += qperm_d<0xAA>(w[s]);
+                        psum += qperm_d<0xAA>(pr[s]);
+                        wsum += qperm_d<0xFF>(w[s]);
+                        psum += qperm_d<0xFF>(pr[s]);
+                    }
+                    const double height = psum / (wsum + 1e-5);     // Q4
+                    if (isnan(height) || isinf(height)) {
+                        cat = IMLS_REJ_NAN_INF_HEIGHT;
+                    } else {
+                        yf[0] = (float)(xd[0] - height * nn[0]);    // imls_icp.cpp:719-729
+                        yf[1] = (float)(xd[1] - height * nn[1]);
+                        yf[2] = (float)(xd[2] - height * nn[2]);
+                        nf[0] = (float)nn[0]; nf[1] = (float)nn[1]; nf[2] = (float)nn[2];
+                    }
+                }
+            }
+        }
+        if (g == 0 && cat != -3) store_result(i, cat, xf, yf, nf, cs, cd, cn);
+    }
+    const bool lead = g == 0;
+    if (lead && cat >= 0) atomicAdd(&rej_s[cat], 1u);
+    if (lead && active && cat != -3) {
+        if (kq) atomicAdd(&rej_s[IMLS_NUM_REJ], (unsigned)kq);
+        if (i1 >= 0) atomicAdd(&rej_s[IMLS_NUM_REJ + 1], 1u);
+    }
+    if (lead && cat == -3) atomicAdd(&rej_s[IMLS_NUM_REJ + 2], 1u);
+    // deferred queries of the block (one 64-slot region), in slot order: no atomics, so the
+    // fallback's rows and slabs do not depend on timing
+    const unsigned long long dm = __ballot(lead && cat == -3);
+    if (lane == 0) fbc[wv] = (unsigned)__popcll(dm);
+    __syncthreads();                  // rej_s and fbc complete
+    if (lead && cat == -3) {
+        unsigned off = (unsigned)__popcll(dm & ((1ull << lane) - 1ull));
+#pragma unroll
+        for (int w = 0; w < kWaveBlock / 64; ++w) off += w < wv ? fbc[w] : 0u;
+        fb_list[(size_t)bx * kFinishQ + off] = (unsigned)i;
+    }
+    if (tid == 0) {
+        unsigned tot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaveBlock / 64; ++w) tot += fbc[w];
+        fb_count[bx] = tot;
+    }
+    // pass-1 slab of the block's 64 queries (grid solve chain only: N > kSmallRows, block-uniform)
+    if (N > kSmallRows) {
+        double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0, one = 0.0;
+        if (cat == -1) { plane_row(xf, yf, nf, a, bb); one = 1.0; }
+        double prod[kNormEq];
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = r; c < 6; ++c) prod[k++] = a[r] * a[c];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) prod[21 + r] = a[r] * bb;
+        prod[27] = one;
+        // lane g of a quad sums terms 7g … 7g+6 over the wave's 16 quads: row shifts by 4 and 8 leave
+        // each 16-lane row's sum in lane 12 + g, two xor exchanges add the rows (fixed association)
+        double v[7];
+#pragma unroll
+        for (int u = 0; u < 7; ++u) {
+            double x = g == 0 ? prod[u] : (g == 1 ? prod[7 + u] : (g == 2 ? prod[14 + u] : prod[21 + u]));
+            x = dpp_add_f64<0x114, 0xf>(x);    // row_shr:4
+            x = dpp_add_f64<0x118, 0xf>(x);    // row_shr:8 → lanes 12..15 of each row
+            x = x + xor_f64(x, 16);
+            x = x + xor_f64(x, 32);
+            v[u] = x;
+        }
+        if (lane >= 12 && lane < 16) {
+#pragma unroll
+            for (int u = 0; u < 7; ++u) red[wv][7 * g + u] = v[u];
+        }
+        __syncthreads();
+        if (tid < kNormEq) {
+            double sum = 0.0;
+#pragma unroll
+            for (int w = 0; w < kWaveBlock / 64; ++w) sum += red[w][tid];
+            partial1[(size_t)bx * kNormEq + tid] = sum;
+        }
+    }
+    if (tid < IMLS_NUM_REJ && rej_s[tid]) atomicAdd((unsigned long long*)&tr->reject[tid], (unsigned long long)rej_s[tid]);
+    if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
+        atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
+    if (nbr_stats && tid == IMLS_NUM_REJ + 2 && rej_s[tid]) atomicAdd(&nbr_stats[5], (unsigned long long)rej_s[tid]);
+}
+
+// =============================================================================================
 // Exact stage, one WAVE per query (a small frame registered alone — the config C/D deployment
 // shape, ≤ kSmallRows queries — where k_finish's one-lane-per-query latency chain (~30 µs per
 // launch for 2000 queries in 8 blocks) sets the frame latency): lane j holds list entry j, so the
@@ -2001,6 +2379,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave_f(
                              (int)blockIdx.x, fa);
 }
 
+#if IMLS_FINISH_QUAD
+#undef IMLS_FINISH_ATTR
+#define IMLS_FINISH_ATTR IMLS_FINISH4_ATTR
+#endif
 template <int KL>
 __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(
         TreeView t, const float4* __restrict__ spt, const float4* __restrict__ snr, const unsigned* __restrict__ qperm,
@@ -2008,8 +2390,13 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish(
         const float* __restrict__ wlist, float4* __restrict__ cs, float4* __restrict__ cd, float4* __restrict__ cn,
         double* __restrict__ partial1, imls_iter_trace* __restrict__ tr, unsigned long long* __restrict__ nbr_stats,
         unsigned* __restrict__ fb_list, unsigned* __restrict__ fb_count) {
+#if IMLS_FINISH_QUAD
+    finish4_body<KL>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr, nbr_stats, fb_list,
+                     fb_count, (int)blockIdx.x);
+#else
     finish_body<KL>(t, spt, snr, qperm, N, pose, done, kp, lists, wlist, cs, cd, cn, partial1, tr, nbr_stats, fb_list,
                     fb_count, (int)blockIdx.x);
+#endif
 }
 
 template <int KCAP>
@@ -2022,7 +2409,8 @@ __global__ __launch_bounds__(kProjBlock) void k_project_lane(
                             kFallbackBlocks);
 }
 
-__device__ __forceinline__ int wave_blocks_of(int N) { return (N + kWaveBlock - 1) / kWaveBlock; }
+// k_finish blocks of a frame (one pass-1 slab each, before the kFallbackBlocks fallback slabs)
+__host__ __device__ __forceinline__ int finish_blocks_of(int N) { return (N + kFinishPerBlock - 1) / kFinishPerBlock; }
 // traversal blocks for packets of qp queries per wave
 __host__ __device__ __forceinline__ int knn_blocks_of(int N, int qp) {
     const int per = qp * (kWaveBlock / 64);
@@ -2094,23 +2482,28 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_FINISH_ATTR void k_finish_b(const 
     batch_block(kp.xcd, f, bx);
     if (f >= npairs) return;
     const PairDev A = device_view(tab + f);
-    if (bx >= wave_blocks_of(A.N)) return;
+    if (bx >= finish_blocks_of(A.N)) return;
+#if IMLS_FINISH_QUAD
+    finish4_body<KL>(A.t, A.spt, A.snr, A.qperm, A.N, A.st.pose, A.st.done, kp, A.lists, wlist_of<KL>(A.lists, A.N), A.cs,
+                     A.cd, A.cn, A.st.partial1, A.trace + it, A.stats, A.fb_list, A.fb_count, bx);
+#else
     finish_body<KL>(A.t, A.spt, A.snr, A.qperm, A.N, A.st.pose, A.st.done, kp, A.lists, wlist_of<KL>(A.lists, A.N), A.cs,
                     A.cd, A.cn, A.st.partial1, A.trace + it, A.stats, A.fb_list, A.fb_count, bx);
+#endif
 }
 
 template <int KCAP>
 __global__ __launch_bounds__(kProjBlock) void k_project_lane_b(const PairDev* __restrict__ tab, KParams kp, int it) {
     const PairDev A = device_view(tab + blockIdx.y);
     project_lane_body<KCAP>(A.t, A.spt, A.snr, A.fb_list, A.fb_count, A.N, A.st.pose, A.st.done, kp, A.cs, A.cd, A.cn,
-                            A.st.partial1 + (size_t)wave_blocks_of(A.N) * kNormEq, A.trace + it, A.stats,
+                            A.st.partial1 + (size_t)finish_blocks_of(A.N) * kNormEq, A.trace + it, A.stats,
                             kFallbackBlocks);
 }
 
 template <int KL>
 void launch_wave_batch(hipStream_t s, const PairDev* tab, int npairs, int maxN, bool any_small, bool any_large,
                        const KParams& kp, int it, int use_prev) {
-    const int wb = (maxN + kWaveBlock - 1) / kWaveBlock;
+    const int wb = finish_blocks_of(maxN);
     const int gy = kp.xcd ? (npairs + 7) / 8 * 8 : npairs;
     if (any_small) {
         const int n = kp.qwave > 0 ? maxN : std::min(maxN, kQwaveAutoN);
@@ -2209,13 +2602,13 @@ void launch_project_batch(hipStream_t s, const PairDev* tab, const int* n_host, 
     else k_project_lane_b<32><<<g, kProjBlock, 0, s>>>(tab, kp, it);
 }
 
-int project_blocks(int N) { return (N + kWaveBlock - 1) / kWaveBlock + kFallbackBlocks; }
+int project_blocks(int N) { return finish_blocks_of(N) + kFallbackBlocks; }
 
 void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const float4* snr, const unsigned* qperm,
                     int N, const double* pose, const int* done, const KParams& kp, float4* cs, float4* cd, float4* cn,
                     double* partial1, imls_iter_trace* tr, unsigned long long* stats, unsigned* fb_list,
                     unsigned* fb_count, int lane_mode, const double* delta, int* lists, int use_prev, hipEvent_t* marks) {
-    const int wblocks = (N + kWaveBlock - 1) / kWaveBlock;
+    const int wblocks = finish_blocks_of(N);
     double* p_fb = partial1 + (size_t)wblocks * kNormEq;
     const int K = kp.K;
     // tensor voting: every source point's voted normal at this pose first (imls_icp.cpp:514-546)
