@@ -383,9 +383,10 @@ inline float4* xref_of(int* lists, int N) {
 inline size_t prevnn_bytes(int N) { return ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256 + (size_t)N * 20; }
 constexpr int kStatSkipped = 6;   // nbr_stats slot: lanes whose list was reused without traversal
 int project_blocks(int N);
-// k_finish: the exact stage one quad per query (1, round 6) or one lane per query (0, same-box A/B)
+// k_finish: the exact stage one lane per query (0) or one quad per query (1: round 6, measured slower —
+// DESIGN §5 round 6; kept for same-box A/B builds, tools/build_full_variant.sh quad -DIMLS_FINISH_QUAD=1)
 #ifndef IMLS_FINISH_QUAD
-#define IMLS_FINISH_QUAD 1
+#define IMLS_FINISH_QUAD 0
 #endif
 constexpr int kPass1Block = IMLS_FINISH_QUAD ? 64 : 256;   // queries per k_finish block (one pass-1 slab each)
 constexpr int kPass1Fallback = 64;     // k_project_lane fallback blocks (one slab each, after the k_finish slabs)

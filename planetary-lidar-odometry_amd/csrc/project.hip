@@ -1526,21 +1526,21 @@ __device__ __forceinline__ double qperm_d(double v) {
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 // a value held by one lane of the quad (zero bits in the others) → every lane of the quad
-__device__ __forceinline__ int quad_or(int v) {
+__device__ __forceinline__ __attribute__((unused)) int quad_or(int v) {
     v |= qperm_i<kQuadSwap1>(v);
     return v | qperm_i<kQuadSwap2>(v);
 }
-__device__ __forceinline__ double quad_or_d(double v) {
+__device__ __forceinline__ __attribute__((unused)) double quad_or_d(double v) {
     const long long b = __double_as_longlong(v);
     const int lo = quad_or((int)(unsigned)(unsigned long long)b);
     const int hi = quad_or((int)(unsigned)((unsigned long long)b >> 32));
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
-__device__ __forceinline__ int quad_sum(int v) {
+__device__ __forceinline__ __attribute__((unused)) int quad_sum(int v) {
     v += qperm_i<kQuadSwap1>(v);
     return v + qperm_i<kQuadSwap2>(v);
 }
-__device__ __forceinline__ int quad_min(int v) {
+__device__ __forceinline__ __attribute__((unused)) int quad_min(int v) {
     v = min(v, qperm_i<kQuadSwap1>(v));
     return min(v, qperm_i<kQuadSwap2>(v));
 }

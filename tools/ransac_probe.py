@@ -1,0 +1,32 @@
+"""Latency probe of the shipped solver's deployment call: LaserOdometry.process
+one frame at a time with RANSAC → DRPM (config.json's solver), on the config C/D-like stream frames
+(≤2000-query flat cloud vs the previous 118k-point filtered scan, 20 ICP iterations).  Prints the
+median / p90 wall time per call; run under rocprofv3 --kernel-trace --stats for the per-kernel split
+(tools/iter_profile_frame.py groups a trace per frame)."""
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402  (loads the library)
+import numpy as np  # noqa: E402
+from planetary_lidar_odometry_amd import imls_icp  # noqa: E402
+
+p = bench.solver_params("RANSAC_DRPM", 20)
+runner = bench.StreamRunner(1, p, 0, 0, frames_per_seq=6, fuse=False, unique=1, dev=None, resident=False, groups=1)
+fr = runner.seqs[0]
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+lat, iters = [], []
+with imls_icp.LaserOdometry(p, device=0) as lo:
+    for j in range(n + 3):
+        k = j % len(fr)
+        t0 = time.perf_counter()
+        r = lo.process(fr[k][0], fr[k][1])
+        if j >= 3:
+            lat.append((time.perf_counter() - t0) * 1e3)
+            if r is not None:
+                iters.append(r["iters"])
+    print(f"LaserOdometry.process RANSAC->DRPM: median {np.median(lat):.3f} ms  p90 {np.percentile(lat, 90):.3f} ms "
+          f"(pipelined {lo.pipelined}, {len(fr[0][1])} queries vs {len(fr[0][0])}-pt scan, iterations {np.mean(iters):.1f})")
+runner.close()
