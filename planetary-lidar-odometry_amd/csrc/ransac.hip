@@ -737,13 +737,9 @@ __device__ __forceinline__ void drpm_eig_body(const double* __restrict__ partial
     sym_eig6_wave(row, Dv.ev, Dv.U);
 }
 
-// per-point noise mean (36) and variance along the eigenvectors (6), degeneracy.h:14-72
-__device__ __forceinline__ void drpm_noise_body(const Rows& rows, int N, const SolveState& st, const DrpmDev& Dv, double sp,
-                                                double sn) {
-    if (*st.done) return;
-    __shared__ double red[(kBlock / 64) * kDrpmSlab];
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    double acc[kDrpmSlab];
+// the 42 noise terms of row i (zero when i ≥ N or the row is absent), degeneracy.h:14-72
+__device__ __forceinline__ void drpm_noise_terms(const Rows& rows, int i, int N, const DrpmDev& Dv, double sp, double sn,
+                                                 double (&acc)[kDrpmSlab]) {
 #pragma unroll
     for (int k = 0; k < kDrpmSlab; ++k) acc[k] = 0.0;
     double a[6], b, wt;
@@ -806,6 +802,16 @@ __device__ __forceinline__ void drpm_noise_body(const Rows& rows, int N, const S
             acc[36 + k] = 2 * aa * aa + 4 * aa * bb * bb;
         }
     }
+}
+
+// per-point noise mean (36) and variance along the eigenvectors (6), degeneracy.h:14-72
+__device__ __forceinline__ void drpm_noise_body(const Rows& rows, int N, const SolveState& st, const DrpmDev& Dv, double sp,
+                                                double sn) {
+    if (*st.done) return;
+    __shared__ double red[(kBlock / 64) * kDrpmSlab];
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    double acc[kDrpmSlab];
+    drpm_noise_terms(rows, i, N, Dv, sp, sn, acc);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < kDrpmSlab; ++k) {
@@ -822,6 +828,70 @@ __device__ __forceinline__ void drpm_noise_body(const Rows& rows, int N, const S
 
 __device__ __forceinline__ double normal_cdf(double mean, double sd, double x) {
     return 0.5 * erfc(-(x - mean) / (sd * sqrt(2.0)));   // Boost.Math cdf(normal(mean, sd), x)
+}
+
+// The DRPM decision and solve from the reduced noise terms tot[42] (solver.cpp:540-603), by wave 0
+// (every other thread returns): lane k < 6 evaluates prob[k] — the thread-0 loop's expressions for
+// that k, so the same bits — the minimum over k in order, then either the SNR-weighted
+// eigen-solution (thread 0) or the plain normal-equation solve by the whole wave (solve6_u: solve6's
+// operations with a wave-uniform pivot, bit for bit), Δ and the pose update by thread 0.  Round 6:
+// one thread ran all six probabilities and solve6's predicated pivot swaps (k_drpm_final 27 µs per
+// call on a lone 1600-row frame, profiles/r06_calib).
+__device__ __forceinline__ void drpm_solve_wave0(const SolveState& st, const DrpmDev& Dv, imls_iter_trace* tr,
+                                                 const KParams& kp, double threshold, const int* __restrict__ count_all,
+                                                 const int* __restrict__ count_in, int update_pose, const double* tot) {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    const double snr = 10.0;   // solver.cpp:547
+    double pk = 0.0;
+    if (lane < 6) {
+        const int k = lane;
+        double meas = 0, exp_noise = 0;
+        for (int r = 0; r < 6; ++r) {
+            double hu = 0, mu = 0;
+            for (int c = 0; c < 6; ++c) { hu += Dv.H[r * 6 + c] * Dv.U[k * 6 + c]; mu += tot[r * 6 + c] * Dv.U[k * 6 + c]; }
+            meas += Dv.U[k * 6 + r] * hu;
+            exp_noise += Dv.U[k * 6 + r] * mu;
+        }
+        const double sd = sqrt(tot[36 + k]);
+        const double tp = meas / (1.0 + snr);
+        const bool bad = isnan(exp_noise) || isnan(sd) || isnan(tp);
+        pk = bad ? 0.0 : normal_cdf(exp_noise, sd, tp);
+    }
+    double prob[6], pmin = INFINITY;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        prob[k] = readlane_f64(pk, k);
+        pmin = fmin(pmin, prob[k]);
+    }
+    double x[6];
+    if (pmin < threshold) {
+        if (lane) return;
+        double ut[6];
+        for (int k = 0; k < 6; ++k) {
+            const double dps = fabs(Dv.ev[k]) > 1e-10 ? prob[k] / Dv.ev[k] : 0.0;
+            double acc = 0;
+            for (int r = 0; r < 6; ++r) acc += Dv.U[k * 6 + r] * Dv.g[r];
+            ut[k] = dps * acc;
+        }
+        for (int r = 0; r < 6; ++r) {
+            double acc = 0;
+            for (int k = 0; k < 6; ++k) acc += Dv.U[k * 6 + r] * ut[k];
+            x[r] = acc;
+        }
+    } else {
+        double ne[kNormEq];
+        int k = 0;
+        for (int r = 0; r < 6; ++r)
+            for (int c = r; c < 6; ++c) ne[k++] = Dv.H[r * 6 + c];
+        for (int r = 0; r < 6; ++r) ne[21 + r] = Dv.g[r];
+        ne[27] = 0;
+        solve6_u(ne, x);
+        if (lane) return;
+    }
+    double D[16];
+    delta_from_x(x, D);
+    finish_iteration(st, tr, D, (double)*count_all, (double)*count_in, update_pose, kp);
 }
 
 __device__ __forceinline__ void drpm_final_body(int blocks, const SolveState& st, const DrpmDev& Dv, imls_iter_trace* tr,
@@ -849,49 +919,7 @@ __device__ __forceinline__ void drpm_final_body(int blocks, const SolveState& st
         tot[threadIdx.x] = s;
     }
     __syncthreads();
-    if (threadIdx.x) return;
-    double prob[6], pmin = INFINITY;
-    const double snr = 10.0;   // solver.cpp:547
-    for (int k = 0; k < 6; ++k) {
-        double meas = 0, exp_noise = 0;
-        for (int r = 0; r < 6; ++r) {
-            double hu = 0, mu = 0;
-            for (int c = 0; c < 6; ++c) { hu += Dv.H[r * 6 + c] * Dv.U[k * 6 + c]; mu += tot[r * 6 + c] * Dv.U[k * 6 + c]; }
-            meas += Dv.U[k * 6 + r] * hu;
-            exp_noise += Dv.U[k * 6 + r] * mu;
-        }
-        const double sd = sqrt(tot[36 + k]);
-        const double tp = meas / (1.0 + snr);
-        const bool bad = isnan(exp_noise) || isnan(sd) || isnan(tp);
-        prob[k] = bad ? 0.0 : normal_cdf(exp_noise, sd, tp);
-        pmin = fmin(pmin, prob[k]);
-    }
-    double x[6];
-    if (pmin < threshold) {
-        double ut[6];
-        for (int k = 0; k < 6; ++k) {
-            const double dps = fabs(Dv.ev[k]) > 1e-10 ? prob[k] / Dv.ev[k] : 0.0;
-            double acc = 0;
-            for (int r = 0; r < 6; ++r) acc += Dv.U[k * 6 + r] * Dv.g[r];
-            ut[k] = dps * acc;
-        }
-        for (int r = 0; r < 6; ++r) {
-            double acc = 0;
-            for (int k = 0; k < 6; ++k) acc += Dv.U[k * 6 + r] * ut[k];
-            x[r] = acc;
-        }
-    } else {
-        double ne[kNormEq];
-        int k = 0;
-        for (int r = 0; r < 6; ++r)
-            for (int c = r; c < 6; ++c) ne[k++] = Dv.H[r * 6 + c];
-        for (int r = 0; r < 6; ++r) ne[21 + r] = Dv.g[r];
-        ne[27] = 0;
-        solve6(ne, x);
-    }
-    double D[16];
-    delta_from_x(x, D);
-    finish_iteration(st, tr, D, (double)*count_all, (double)*count_in, update_pose, kp);
+    drpm_solve_wave0(st, Dv, tr, kp, threshold, count_all, count_in, update_pose, tot);
 }
 
 __global__ __launch_bounds__(256) void k_drpm_eig(const double* __restrict__ partial, int blocks, SolveState st, DrpmDev Dv) {
@@ -914,6 +942,155 @@ __global__ __launch_bounds__(256) void k_drpm_final(int blocks, SolveState st, D
                                                     imls_iter_trace* rtr) {
     drpm_final_body(blocks, st, Dv, tr, kp, threshold, count_all, count_in, update_pose);
     ransac_trace_t0(R, count_all, rtr);
+}
+
+// ---------------------------------------------------------------------------------------------
+// The lone frame's DRPM solve in ONE launch (round 6; frames of ≤ kSmallRows rows registered alone,
+// the config C/D deployment shape): pass 1 of the weighted normal equations over the inliers, the
+// eigendecomposition, the per-point noise terms and the DRPM solve + pose update — four launches of
+// one small grid each before (k_rows_pass1, k_drpm_eig, k_drpm_noise, k_drpm_final: with the inlier
+// compaction 78 µs per ICP iteration on a 1600-row frame, profiles/r06_calib/).  One 512-thread block
+// runs the phases between block barriers; the multi-block phases run as "virtual blocks" — block b of
+// the grid version is done by the 256-thread group (b mod 2) in round b / 2, with the same thread ↔
+// row mapping, the same per-wave reductions and the same slab order — so every value is the chain's
+// bit for bit (the batched frames keep the chain: alone and batched agree).  (The inlier compaction
+// stays its own 1024-thread launch: in this block its registers spilled the noise phase.)
+// ---------------------------------------------------------------------------------------------
+constexpr int kTailThreads = 512;
+__global__ __launch_bounds__(kTailThreads) void k_drpm_tail_small(Rows rows, int cap, int b1, SolveState st, DrpmDev Dv,
+                                                                  imls_iter_trace* tr, KParams kp, double threshold,
+                                                                  const int* __restrict__ count_all,
+                                                                  const int* __restrict__ count_in, int update_pose,
+                                                                  double sp, double sn, RansacDev R, imls_iter_trace* rtr) {
+    __shared__ double red_ne[kTailThreads / 64][kNormEq];
+    __shared__ double red_nz[kTailThreads / 64][kDrpmSlab];
+    __shared__ double acc[kDrpmSlab];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, grp = tid >> 8, t = tid & 255;
+    // a finished frame (before or by the inlier compaction) skips the solve, as the chain's kernels do,
+    // but RANSAC's own trace record is still written (k_drpm_final writes it whether or not it solved)
+    if (*st.done) {
+        ransac_trace_t0(R, count_all, rtr);
+        return;
+    }
+    // 2. pass 1 over the inlier rows (k_rows_pass1<kBlock>: slab b = rows [256b, 256b + 256))
+    for (int base = 0; base < b1; base += kTailThreads / kBlock) {
+        const int b = base + grp, i = b * kBlock + t;
+        double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0, wt = 1, cnt = 0;
+        if (b < b1 && i < cap && rows.get(i, a, bb, wt)) {
+            const double sw = sqrt(wt);
+            for (int k = 0; k < 6; ++k) a[k] = sw * a[k];
+            bb = sw * bb;
+            cnt = 1;
+        }
+        double v[32];
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = r; c < 6; ++c) v[k++] = a[r] * a[c];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) v[21 + r] = a[r] * bb;
+        v[27] = cnt;
+#pragma unroll
+        for (int q = kNormEq; q < 32; ++q) v[q] = 0.0;
+        const double sum = wave_sum28(v);
+        if (!(lane & 1) && (lane >> 1) < kNormEq) red_ne[wv][lane >> 1] = sum;
+        __syncthreads();
+        if (t < kNormEq && b < b1) {
+            double sacc = 0.0;
+            for (int w = 0; w < kBlock / 64; ++w) sacc += red_ne[grp * (kBlock / 64) + w][t];
+            st.partial1[(size_t)b * kNormEq + t] = sacc;
+        }
+        __syncthreads();
+    }
+    __threadfence_block();
+    __syncthreads();
+    // 3. H, g and the eigendecomposition (k_drpm_eig: 256 threads reduce the slabs, wave 0 solves)
+    {
+        double loc[kNormEq];
+#pragma unroll
+        for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
+        if (tid < 256)
+            for (int b = tid; b < b1; b += 256)
+#pragma unroll
+                for (int k = 0; k < kNormEq; ++k) loc[k] += st.partial1[(size_t)b * kNormEq + k];
+        double a32[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) a32[k] = k < kNormEq ? loc[k] : 0.0;
+        const double sum = wave_sum28(a32);
+        if (wv < 4 && !(lane & 1) && (lane >> 1) < kNormEq) red_ne[wv][lane >> 1] = sum;
+        __syncthreads();
+        if (tid < kNormEq) {
+            double sacc = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) sacc += red_ne[w][tid];
+            acc[tid] = sacc;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            const int k = lane < 6 ? lane : 0;
+            double row[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                const int r0 = k < c ? k : c, c0 = k < c ? c : k;
+                row[c] = acc[6 * r0 - r0 * (r0 - 1) / 2 + (c0 - r0)];
+            }
+            if (lane < 6) {
+#pragma unroll
+                for (int c = 0; c < 6; ++c) Dv.H[lane * 6 + c] = row[c];
+                Dv.g[lane] = acc[21 + lane];
+            }
+            sym_eig6_wave(row, Dv.ev, Dv.U);
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    // 4. per-point noise terms (k_drpm_noise: slab b = rows [256b, 256b + 256))
+    for (int base = 0; base < b1; base += kTailThreads / kBlock) {
+        const int b = base + grp;
+        double nz[kDrpmSlab];
+        drpm_noise_terms(rows, b < b1 ? b * kBlock + t : cap, cap, Dv, sp, sn, nz);
+#pragma unroll
+        for (int k = 0; k < kDrpmSlab; ++k) {
+            const double v = wave_sum(nz[k]);
+            if (lane == 0) red_nz[wv][k] = v;
+        }
+        __syncthreads();
+        if (t < kDrpmSlab && b < b1) {
+            double sacc = 0.0;
+            for (int w = 0; w < kBlock / 64; ++w) sacc += red_nz[grp * (kBlock / 64) + w][t];
+            Dv.slabs[(size_t)b * kDrpmSlab + t] = sacc;
+        }
+        __syncthreads();
+    }
+    __threadfence_block();
+    __syncthreads();
+    // 5. the slab totals (k_drpm_final: 256 threads), the DRPM decision and solve, RANSAC's record
+    {
+        double loc[kDrpmSlab];
+#pragma unroll
+        for (int k = 0; k < kDrpmSlab; ++k) loc[k] = 0.0;
+        if (tid < 256)
+            for (int b = tid; b < b1; b += 256)
+#pragma unroll
+                for (int k = 0; k < kDrpmSlab; ++k) loc[k] += Dv.slabs[(size_t)b * kDrpmSlab + k];
+        if (wv < 4) {
+#pragma unroll
+            for (int k = 0; k < kDrpmSlab; ++k) {
+                const double v = wave_sum(loc[k]);
+                if (lane == 0) red_nz[wv][k] = v;
+            }
+        }
+        __syncthreads();
+        if (tid < kDrpmSlab) {
+            double sacc = 0.0;
+            for (int w = 0; w < 256 / 64; ++w) sacc += red_nz[w][tid];
+            acc[tid] = sacc;
+        }
+        __syncthreads();
+        drpm_solve_wave0(st, Dv, tr, kp, threshold, count_all, count_in, update_pose, acc);
+        ransac_trace_t0(R, count_all, rtr);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -987,10 +1164,18 @@ __global__ __launch_bounds__(256) void k_drpm_final_b(const PairDev* __restrict_
 // met by the first hypotheses), 256, then the rest in chunks of kHypMax — three chunks for
 // max_iterations ≤ kHypMax + 272.  (Results do not depend on the chunking: exactly the draws
 // consumed are committed.)
-std::vector<int> ransac_chunks(int max_iterations) {
+// Hypothesis chunks.  Each hypothesis takes its own rand() word (the h-th ahead of the chunk's state)
+// and the select commits exactly the words used, so any chunking gives the same result; chunks only
+// trade wasted work after an early exit against launches.  Batched frames: 16, 256, then up to
+// kHypMax (throughput: a frame that exits early wastes little of the shared grid).  A frame alone
+// (lone = true, the deployment shape): 272, then up to kHypMax — the first two batched chunks in one
+// launch (both fit one wave of blocks, so the merged launch takes about as long as the 16; round 6:
+// a lone 1600-row frame without an early exit ran 3 hypothesis + 3 select launches per ICP iteration).
+std::vector<int> ransac_chunks(int max_iterations, bool lone = false) {
     std::vector<int> v;
     for (int started = 0; started < max_iterations;) {
-        const int cn = std::min(started == 0 ? 16 : started == 16 ? 256 : kHypMax, max_iterations - started);
+        const int want = lone ? (started == 0 ? 272 : kHypMax) : (started == 0 ? 16 : started == 16 ? 256 : kHypMax);
+        const int cn = std::min(want, max_iterations - started);
         v.push_back(cn);
         started += cn;
     }
@@ -1070,7 +1255,7 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
         k_ransac_begin<<<1, 64, 0, s>>>(F.cnt_all, kp.correspond_number, L.update_pose, L.st, L.tr, R);
     }
     // 2. hypotheses in chunks
-    for (const int cn : ransac_chunks(L.ransac.max_iterations)) {
+    for (const int cn : ransac_chunks(L.ransac.max_iterations, true)) {
         if (hyp_block_of(cap) == 64)
             k_ransac_hyp<64><<<cn, 64, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done);
         else
@@ -1086,13 +1271,20 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
     isrc.T = R.bestT;
     isrc.dist_thr = L.ransac.distance_threshold;
     isrc.h2 = L.ransac.huber_threshold * L.ransac.distance_threshold;
-    compact(isrc, cap, CompactOut{F.inl, F.cnt_in, F.wsum, cap}, 2);
-
-    // 4. final solve on the inliers (+ RANSAC's own trace record)
     KParams fk = kp;
     fk.correspond_number = 0;                       // the count gate ran before RANSAC
     double* inl = F.inl;
     Rows rows{nullptr, nullptr, nullptr, inl, inl + 3 * c, inl + 6 * c, inl + 9 * c, 1, F.cnt_in, F.wsum};
+    compact(isrc, cap, CompactOut{F.inl, F.cnt_in, F.wsum, cap}, 2);
+    if (L.ransac.final_method == IMLS_FINAL_DRPM && cap <= kSmallRows) {
+        // the DRPM solve of a small frame in one launch (k_drpm_tail_small: the four-kernel chain's values)
+        k_drpm_tail_small<<<1, kTailThreads, 0, s>>>(rows, cap, solve_blocks(cap), L.st, F.Dv, L.tr, fk,
+                                                     L.ransac.drpm_threshold, F.cnt_all, F.cnt_in, L.update_pose,
+                                                     L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals, R, L.tr);
+        return;
+    }
+
+    // 4. final solve on the inliers (+ RANSAC's own trace record)
     switch (L.ransac.final_method) {
         case IMLS_FINAL_LS:
             fk.solve_method = IMLS_SOLVE_LS;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 6: the lone frame's fused DRPM solve + merged first hypothesis chunk — RANSAC / stream /
+# batched-vs-single tests, then the lone-frame latency probe and its kernel trace.
+set -u
+O=gpurun_out/${OUT:-r06_ransac}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 700 python3 -u -m pytest tests/test_gpu_ransac.py tests/test_gpu_stream.py tests/test_gpu_frames.py \
+    tests/test_gpu_batch.py tests/test_gpu_grow.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 tools/ransac_probe.py 30 > $O/ransac_probe.out 2> $O/ransac_probe.err; echo "probe rc=$?"; cat $O/ransac_probe.out
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_ransac -o run -- python3 tools/ransac_probe.py 10 > $O/kt_ransac.out 2> $O/kt_ransac.err
+echo "kt rc=$?"
+echo done
