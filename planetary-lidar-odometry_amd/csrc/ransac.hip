@@ -945,35 +945,32 @@ __global__ __launch_bounds__(256) void k_drpm_final(int blocks, SolveState st, D
 }
 
 // ---------------------------------------------------------------------------------------------
-// The lone frame's DRPM solve in ONE launch (round 6; frames of ≤ kSmallRows rows registered alone,
-// the config C/D deployment shape): pass 1 of the weighted normal equations over the inliers, the
-// eigendecomposition, the per-point noise terms and the DRPM solve + pose update — four launches of
-// one small grid each before (k_rows_pass1, k_drpm_eig, k_drpm_noise, k_drpm_final: with the inlier
-// compaction 78 µs per ICP iteration on a 1600-row frame, profiles/r06_calib/).  One 512-thread block
-// runs the phases between block barriers; the multi-block phases run as "virtual blocks" — block b of
-// the grid version is done by the 256-thread group (b mod 2) in round b / 2, with the same thread ↔
-// row mapping, the same per-wave reductions and the same slab order — so every value is the chain's
-// bit for bit (the batched frames keep the chain: alone and batched agree).  (The inlier compaction
-// stays its own 1024-thread launch: in this block its registers spilled the noise phase.)
+// The lone frame's DRPM head in ONE launch (round 6; frames of ≤ kSmallRows rows registered alone,
+// the config C/D deployment shape): the inlier compaction, pass 1 of the weighted normal equations
+// over the inliers and the eigendecomposition — three launches before (k_compact_one, k_rows_pass1,
+// k_drpm_eig).  One 1024-thread block runs them between block barriers; pass 1 runs as "virtual
+// blocks" — block b of k_rows_pass1's grid is done by the 256-thread group (b mod 4) in round b / 4,
+// with the same thread ↔ row mapping, the same per-wave reductions and the same slab order, and the
+// slab sum by the first 256 threads as k_drpm_eig does it — so every value is the chain's bit for bit
+// (the batched frames keep the chain: alone and batched agree).  The noise terms and the solve stay
+// grid / one-block launches: fused into this block as well (virtual noise blocks, measured) the
+// frame's DRPM took 102.7 µs per ICP iteration against the chain's 70 (one CU for the noise phase,
+// its registers at 2 waves per SIMD; profiles/r06_ransac/).
 // ---------------------------------------------------------------------------------------------
-constexpr int kTailThreads = 512;
-__global__ __launch_bounds__(kTailThreads) void k_drpm_tail_small(Rows rows, int cap, int b1, SolveState st, DrpmDev Dv,
-                                                                  imls_iter_trace* tr, KParams kp, double threshold,
-                                                                  const int* __restrict__ count_all,
-                                                                  const int* __restrict__ count_in, int update_pose,
-                                                                  double sp, double sn, RansacDev R, imls_iter_trace* rtr) {
-    __shared__ double red_ne[kTailThreads / 64][kNormEq];
-    __shared__ double red_nz[kTailThreads / 64][kDrpmSlab];
-    __shared__ double acc[kDrpmSlab];
+constexpr int kHeadThreads = 1024;
+__global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(Source isrc, int cap, CompactOut out, CompactPost P,
+                                                                  Rows rows, int b1, SolveState st, DrpmDev Dv) {
+    __shared__ double red_ne[kHeadThreads / 64][kNormEq];
+    __shared__ double acc[kNormEq];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, grp = tid >> 8, t = tid & 255;
-    // a finished frame (before or by the inlier compaction) skips the solve, as the chain's kernels do,
-    // but RANSAC's own trace record is still written (k_drpm_final writes it whether or not it solved)
-    if (*st.done) {
-        ransac_trace_t0(R, count_all, rtr);
-        return;
-    }
-    // 2. pass 1 over the inlier rows (k_rows_pass1<kBlock>: slab b = rows [256b, 256b + 256))
-    for (int base = 0; base < b1; base += kTailThreads / kBlock) {
+    // 1. the inliers of the best Δ with their weights (k_compact_one, kind 2: an empty set fails the solve)
+    if (compact_skip(P)) return;
+    compact_one_body(isrc, cap, out, P);
+    __threadfence_block();
+    __syncthreads();
+    // 2. pass 1 over the inlier rows (k_rows_pass1<kBlock>, which runs whether or not the frame is done:
+    // slab b = rows [256b, 256b + 256))
+    for (int base = 0; base < b1; base += kHeadThreads / kBlock) {
         const int b = base + grp, i = b * kBlock + t;
         double a[6] = {0, 0, 0, 0, 0, 0}, bb = 0, wt = 1, cnt = 0;
         if (b < b1 && i < cap && rows.get(i, a, bb, wt)) {
@@ -1005,92 +1002,43 @@ __global__ __launch_bounds__(kTailThreads) void k_drpm_tail_small(Rows rows, int
     }
     __threadfence_block();
     __syncthreads();
-    // 3. H, g and the eigendecomposition (k_drpm_eig: 256 threads reduce the slabs, wave 0 solves)
-    {
-        double loc[kNormEq];
+    // 3. H, g and the eigendecomposition (k_drpm_eig: a finished frame stops here; 256 threads reduce
+    // the slabs, wave 0 solves)
+    if (*st.done) return;
+    double loc[kNormEq];
 #pragma unroll
-        for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
-        if (tid < 256)
-            for (int b = tid; b < b1; b += 256)
+    for (int k = 0; k < kNormEq; ++k) loc[k] = 0.0;
+    if (tid < 256)
+        for (int b = tid; b < b1; b += 256)
 #pragma unroll
-                for (int k = 0; k < kNormEq; ++k) loc[k] += st.partial1[(size_t)b * kNormEq + k];
-        double a32[32];
+            for (int k = 0; k < kNormEq; ++k) loc[k] += st.partial1[(size_t)b * kNormEq + k];
+    double a32[32];
 #pragma unroll
-        for (int k = 0; k < 32; ++k) a32[k] = k < kNormEq ? loc[k] : 0.0;
-        const double sum = wave_sum28(a32);
-        if (wv < 4 && !(lane & 1) && (lane >> 1) < kNormEq) red_ne[wv][lane >> 1] = sum;
-        __syncthreads();
-        if (tid < kNormEq) {
-            double sacc = 0.0;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) sacc += red_ne[w][tid];
-            acc[tid] = sacc;
-        }
-        __syncthreads();
-        if (tid < 64) {
-            const int k = lane < 6 ? lane : 0;
-            double row[6];
-#pragma unroll
-            for (int c = 0; c < 6; ++c) {
-                const int r0 = k < c ? k : c, c0 = k < c ? c : k;
-                row[c] = acc[6 * r0 - r0 * (r0 - 1) / 2 + (c0 - r0)];
-            }
-            if (lane < 6) {
-#pragma unroll
-                for (int c = 0; c < 6; ++c) Dv.H[lane * 6 + c] = row[c];
-                Dv.g[lane] = acc[21 + lane];
-            }
-            sym_eig6_wave(row, Dv.ev, Dv.U);
-        }
-        __threadfence_block();
-        __syncthreads();
-    }
-    // 4. per-point noise terms (k_drpm_noise: slab b = rows [256b, 256b + 256))
-    for (int base = 0; base < b1; base += kTailThreads / kBlock) {
-        const int b = base + grp;
-        double nz[kDrpmSlab];
-        drpm_noise_terms(rows, b < b1 ? b * kBlock + t : cap, cap, Dv, sp, sn, nz);
-#pragma unroll
-        for (int k = 0; k < kDrpmSlab; ++k) {
-            const double v = wave_sum(nz[k]);
-            if (lane == 0) red_nz[wv][k] = v;
-        }
-        __syncthreads();
-        if (t < kDrpmSlab && b < b1) {
-            double sacc = 0.0;
-            for (int w = 0; w < kBlock / 64; ++w) sacc += red_nz[grp * (kBlock / 64) + w][t];
-            Dv.slabs[(size_t)b * kDrpmSlab + t] = sacc;
-        }
-        __syncthreads();
-    }
-    __threadfence_block();
+    for (int k = 0; k < 32; ++k) a32[k] = k < kNormEq ? loc[k] : 0.0;
+    const double sum = wave_sum28(a32);
+    if (wv < 4 && !(lane & 1) && (lane >> 1) < kNormEq) red_ne[wv][lane >> 1] = sum;
     __syncthreads();
-    // 5. the slab totals (k_drpm_final: 256 threads), the DRPM decision and solve, RANSAC's record
-    {
-        double loc[kDrpmSlab];
+    if (tid < kNormEq) {
+        double sacc = 0.0;
 #pragma unroll
-        for (int k = 0; k < kDrpmSlab; ++k) loc[k] = 0.0;
-        if (tid < 256)
-            for (int b = tid; b < b1; b += 256)
-#pragma unroll
-                for (int k = 0; k < kDrpmSlab; ++k) loc[k] += Dv.slabs[(size_t)b * kDrpmSlab + k];
-        if (wv < 4) {
-#pragma unroll
-            for (int k = 0; k < kDrpmSlab; ++k) {
-                const double v = wave_sum(loc[k]);
-                if (lane == 0) red_nz[wv][k] = v;
-            }
-        }
-        __syncthreads();
-        if (tid < kDrpmSlab) {
-            double sacc = 0.0;
-            for (int w = 0; w < 256 / 64; ++w) sacc += red_nz[w][tid];
-            acc[tid] = sacc;
-        }
-        __syncthreads();
-        drpm_solve_wave0(st, Dv, tr, kp, threshold, count_all, count_in, update_pose, acc);
-        ransac_trace_t0(R, count_all, rtr);
+        for (int w = 0; w < 4; ++w) sacc += red_ne[w][tid];
+        acc[tid] = sacc;
     }
+    __syncthreads();
+    if (tid >= 64) return;
+    const int k = lane < 6 ? lane : 0;
+    double row[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        const int r0 = k < c ? k : c, c0 = k < c ? c : k;
+        row[c] = acc[6 * r0 - r0 * (r0 - 1) / 2 + (c0 - r0)];
+    }
+    if (lane < 6) {
+#pragma unroll
+        for (int c = 0; c < 6; ++c) Dv.H[lane * 6 + c] = row[c];
+        Dv.g[lane] = acc[21 + lane];
+    }
+    sym_eig6_wave(row, Dv.ev, Dv.U);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1275,14 +1223,19 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
     fk.correspond_number = 0;                       // the count gate ran before RANSAC
     double* inl = F.inl;
     Rows rows{nullptr, nullptr, nullptr, inl, inl + 3 * c, inl + 6 * c, inl + 9 * c, 1, F.cnt_in, F.wsum};
-    compact(isrc, cap, CompactOut{F.inl, F.cnt_in, F.wsum, cap}, 2);
     if (L.ransac.final_method == IMLS_FINAL_DRPM && cap <= kSmallRows) {
-        // the DRPM solve of a small frame in one launch (k_drpm_tail_small: the four-kernel chain's values)
-        k_drpm_tail_small<<<1, kTailThreads, 0, s>>>(rows, cap, solve_blocks(cap), L.st, F.Dv, L.tr, fk,
-                                                     L.ransac.drpm_threshold, F.cnt_all, F.cnt_in, L.update_pose,
-                                                     L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals, R, L.tr);
+        // a small frame: compaction + pass 1 + eigendecomposition in one launch (the chain's values),
+        // then the noise terms and the solve
+        const int b1 = solve_blocks(cap);
+        const CompactPost P{2, kp.correspond_number, L.update_pose, L.st, L.tr, R};
+        k_drpm_head_small<<<1, kHeadThreads, 0, s>>>(isrc, cap, CompactOut{F.inl, F.cnt_in, F.wsum, cap}, P, rows, b1, L.st,
+                                                     F.Dv);
+        k_drpm_noise<<<b1, kBlock, 0, s>>>(rows, cap, L.st, F.Dv, L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals);
+        k_drpm_final<<<1, 256, 0, s>>>(b1, L.st, F.Dv, L.tr, fk, L.ransac.drpm_threshold, F.cnt_all, F.cnt_in, L.update_pose,
+                                       R, L.tr);
         return;
     }
+    compact(isrc, cap, CompactOut{F.inl, F.cnt_in, F.wsum, cap}, 2);
 
     // 4. final solve on the inliers (+ RANSAC's own trace record)
     switch (L.ransac.final_method) {
