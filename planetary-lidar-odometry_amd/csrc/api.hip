@@ -195,8 +195,7 @@ struct imls_ctx {
     unsigned fifo_seq = 0;                // run ids: pushes mod kMaxFifoRuns
     int* h_fifo_cnt = nullptr;            // pinned [kMaxFifoRuns]: kept count of each run's filter
     unsigned* h_fifo_clamp = nullptr;     // pinned: points outside the frame at the last build
-    FifoRun* h_runtab = nullptr;          // pinned [kMaxFifoRuns]: the run table's upload source
-    DevBuf fifo_dev;                      // fq[4] | clamp counter | run table [kMaxFifoRuns]
+    DevBuf fifo_dev;                      // fq[4] | clamp counter
     bool fq_valid = false;
     std::vector<int> merged_ids;          // runs in the merged order, oldest first
     DevBuf mkey[2], mval[2];
@@ -1283,7 +1282,6 @@ void imls_destroy(imls_ctx* c) {
     for (DevBuf* b : {&c->fifo_dev, &c->mkey[0], &c->mkey[1], &c->mval[0], &c->mval[1], &c->fscr}) if (b->p) (void)hipFree(b->p);
     if (c->h_fifo_cnt) (void)hipHostFree(c->h_fifo_cnt);
     if (c->h_fifo_clamp) (void)hipHostFree(c->h_fifo_clamp);
-    if (c->h_runtab) (void)hipHostFree(c->h_runtab);
     if (c->ev_fifo) (void)hipEventDestroy(c->ev_fifo);
     if (c->macc.p) (void)hipFree(c->macc.p);
     if (c->skept.p) (void)hipFree(c->skept.p);
@@ -1494,8 +1492,8 @@ bool fifo_incremental(const imls_ctx* c) { return c->P.max_queue_size >= 2 && c-
 int ensure_fifo(imls_ctx* c) {
     if (c->h_fifo_cnt) return IMLS_OK;
     if (hipHostMalloc((void**)&c->h_fifo_cnt, kMaxFifoRuns * sizeof(int), hipHostMallocCoherent) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_fifo_clamp, 64) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_runtab, kMaxFifoRuns * sizeof(FifoRun)) != hipSuccess)
+        // coherent: the FIFO gather kernel writes the clamp count here directly
+        hipHostMalloc((void**)&c->h_fifo_clamp, 64, hipHostMallocCoherent) != hipSuccess)
         return fail(c, IMLS_ERR_DEVICE, "hipHostMalloc (FIFO)");
     *c->h_fifo_clamp = 0;
     if (!grow(c->fifo_dev, 256 + kMaxFifoRuns * sizeof(FifoRun))) return fail(c, IMLS_ERR_DEVICE, "hipMalloc (FIFO)");
@@ -1505,7 +1503,6 @@ int ensure_fifo(imls_ctx* c) {
 }
 float* fifo_fq(imls_ctx* c) { return (float*)c->fifo_dev.p; }
 unsigned* fifo_clamp(imls_ctx* c) { return (unsigned*)((char*)c->fifo_dev.p + 64); }
-FifoRun* fifo_runtab(imls_ctx* c) { return (FifoRun*)((char*)c->fifo_dev.p + 256); }
 
 // the target is the FIFO's incremental index: pending until its first use (or at once with n_map)
 int fifo_set_target(imls_ctx* c, size_t* n_map) {
@@ -1624,20 +1621,20 @@ int fifo_build(imls_ctx* c) {
         ids.push_back(e.id);
     }
     c->merged_ids = ids;
-    // run table: each run's records and its offset in the concatenation (the libnabo tie order)
+    // run table (by value in the gather launch): each run's records and its offset in the
+    // concatenation (the libnabo tie order)
+    FifoRunTable rt{};
     unsigned off = 0;
     for (auto& e : c->fifo) {
         if (e.nk <= 0) continue;
-        c->h_runtab[e.id] = FifoRun{fifo_run_pts(e.run.p, e.nk), fifo_run_nrm(e.run.p, e.nk), off, 0u};
+        rt.r[e.id] = FifoRun{fifo_run_pts(e.run.p, e.nk), fifo_run_nrm(e.run.p, e.nk), off, 0u};
         off += (unsigned)e.nk;
     }
-    if (hipMemcpyAsync(fifo_runtab(c), c->h_runtab, kMaxFifoRuns * sizeof(FifoRun), hipMemcpyHostToDevice, s) != hipSuccess)
-        return fail(c, IMLS_ERR_DEVICE, "run table upload");
-    int rc = fifo_index(s, K(c->mcur), V(c->mcur), c->M, fifo_runtab(c), fifo_fq(c), c->B, c->lkeys, c->mpt, c->nodes,
-                        c->treescratch, &c->Pl, &c->levels, c->err);
+    // the gather also copies this build's clamp count into the host's coherent word, read at the next
+    // build (after its wait for the map filter, which this stream runs after the gather)
+    int rc = fifo_index(s, K(c->mcur), V(c->mcur), c->M, rt, fifo_fq(c), fifo_clamp(c), c->h_fifo_clamp, c->B, c->lkeys,
+                        c->mpt, c->nodes, c->treescratch, &c->Pl, &c->levels, c->err);
     if (rc) return rc;
-    // this build's clamp count, read at the next build (its events order the copy before that read)
-    (void)hipMemcpyAsync(c->h_fifo_clamp, fifo_clamp(c), 4, hipMemcpyDeviceToHost, s);
     (void)hipEventRecord(c->ev_fifo, s);
     timed_end(c, 1, c->tgt_slot);
     c->tgt_slot = -1;

@@ -387,6 +387,7 @@ int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf
 
 void tree_rounds(hipStream_t s, const float4* mpt, int M, int B, int P, int levels, float4* nodes, float* leafbox,
                  float* rootsA, float* rootsB);
+void subtree_rounds(hipStream_t s, const float* leafbox, int P, int levels, float4* nodes, float* rootsA, float* rootsB);
 
 int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& tpt, DevBuf& tnr, DevBuf& mpt,
                       DevBuf& nodes, DevBuf& scratch, DevBuf& treescratch, DevBuf& permbuf, int* P_out, int* levels_out,
@@ -421,6 +422,11 @@ int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& t
 void tree_rounds(hipStream_t s, const float4* mpt, int M, int B, int P, int levels, float4* nodes, float* leafbox,
                  float* rootsA, float* rootsB) {
     k_leaf_boxes<<<grid_for(P), kBlock, 0, s>>>(mpt, M, B, P, leafbox);
+    subtree_rounds(s, leafbox, P, levels, nodes, rootsA, rootsB);
+}
+
+// the internal levels from P leaf boxes (k_subtree rounds, 256 boxes per block per round)
+void subtree_rounds(hipStream_t s, const float* leafbox, int P, int levels, float4* nodes, float* rootsA, float* rootsB) {
     const float* in = leafbox;
     float* outs[2] = {rootsA, rootsB};
     int count = P, D = levels, which = 0;
@@ -876,65 +882,101 @@ __global__ void k_fifo_frame(const float* __restrict__ part, int nparts, float* 
     }
 }
 
-// stable compaction of the merged order: entries whose run id (val >> 27) is live
+// stable compaction of the merged order: entries whose run id (val >> 27) is live.  Two launches
+// (round 6: count + scan + scatter and the scan's init were four): tiles of kKeepTile entries, 16 per
+// thread in order; the scatter block sums the earlier tiles' counts itself (≤ a few hundred words)
+// instead of a device-wide scan launch
 __device__ __forceinline__ bool live_entry(unsigned v, unsigned live) { return (live >> (v >> 27)) & 1u; }
+constexpr int kKeepPer = 16;
+constexpr int kKeepTile = kBlock * kKeepPer;
 __global__ __launch_bounds__(kBlock) void k_keep_count(const unsigned* __restrict__ val, int n, unsigned live, int* __restrict__ blk) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
     __shared__ int wc[kBlock / 64];
-    const unsigned long long m = __ballot(i < n && live_entry(val[i], live));
-    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
+    const int base = blockIdx.x * kKeepTile + threadIdx.x * kKeepPer;
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < kKeepPer; ++k) c += (base + k < n && live_entry(val[base + k], live)) ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
-        int c = 0;
-        for (int k = 0; k < kBlock / 64; ++k) c += wc[k];
-        blk[blockIdx.x] = c;
+        int t = 0;
+        for (int k = 0; k < kBlock / 64; ++k) t += wc[k];
+        blk[blockIdx.x] = t;
     }
 }
 __global__ __launch_bounds__(kBlock) void k_keep_scatter(const unsigned long long* __restrict__ key, const unsigned* __restrict__ val,
-                                                         int n, unsigned live, const int* __restrict__ off,
+                                                         int n, unsigned live, const int* __restrict__ blk,
                                                          unsigned long long* __restrict__ okey, unsigned* __restrict__ oval) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    __shared__ int wc[kBlock / 64];
-    const bool keep = i < n && live_entry(val[i], live);
-    const unsigned long long m = __ballot(keep);
-    if (lane == 0) wc[wv] = __popcll(m);
+    __shared__ int wsum[kBlock / 64];
+    __shared__ int s_off;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // this tile's output offset: Σ of the earlier tiles' counts
+    int pre = 0;
+    for (int b = tid; b < (int)blockIdx.x; b += kBlock) pre += blk[b];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+    if (lane == 0) wsum[wv] = pre;
     __syncthreads();
-    if (!keep) return;
-    int o = off[blockIdx.x];
-    for (int k = 0; k < wv; ++k) o += wc[k];
-    o += __popcll(m & ((1ull << lane) - 1ull));
-    okey[o] = key[i];
-    oval[o] = val[i];
+    if (tid == 0) {
+        int t = 0;
+        for (int k = 0; k < kBlock / 64; ++k) t += wsum[k];
+        s_off = t;
+    }
+    __syncthreads();
+    const int base = blockIdx.x * kKeepTile + tid * kKeepPer;
+    unsigned keepm = 0;
+#pragma unroll
+    for (int k = 0; k < kKeepPer; ++k) keepm |= (base + k < n && live_entry(val[base + k], live)) ? (1u << k) : 0u;
+    const int c = __popc(keepm);
+    // block-exclusive prefix of the per-thread counts (thread order = entry order)
+    int inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
+    }
+    __syncthreads();
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    int o = s_off + inc - c;
+    for (int k = 0; k < wv; ++k) o += wsum[k];
+    for (int k = 0; k < kKeepPer; ++k) {
+        if ((keepm >> k) & 1u) {
+            okey[o] = key[base + k];
+            oval[o] = val[base + k];
+            ++o;
+        }
+    }
 }
 
-// merge path: split[t] = entries of A among the first t·kMergeTile outputs of merge(A, B), A first on
-// equal keys (A: the older entries)
-__global__ void k_merge_split(const unsigned long long* __restrict__ a, int na, const unsigned long long* __restrict__ b, int nb,
-                              int tiles, int* __restrict__ split) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > tiles) return;
-    const long long d = std::min((long long)t * kMergeTile, (long long)na + nb);
+// merge path: the entries of A among the first d outputs of merge(A, B), A first on equal keys
+// (A: the older entries)
+__device__ __forceinline__ int merge_split_at(const unsigned long long* __restrict__ a, int na,
+                                              const unsigned long long* __restrict__ b, int nb, long long d) {
     int lo = (int)std::max(0ll, d - nb), hi = (int)std::min<long long>(d, na);
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (a[mid] <= b[d - 1 - mid]) lo = mid + 1;
         else hi = mid;
     }
-    split[t] = lo;
+    return lo;
 }
-// one output tile: both input segments in LDS, each entry's output rank = its index in its own
-// segment + the other segment's entries before it (B: strictly smaller keys after A's equal ones).
-// B's values are (bid << 27) | index (a run's entries in its sorted order)
+// one output tile of kMergeTile: its two splits by binary search on the diagonals (threads 0 / 1;
+// round 6: a separate split launch before), both input segments in LDS, each entry's output rank = its
+// index in its own segment + the other segment's entries before it (B: strictly smaller keys after
+// A's equal ones).  B's values are (bid << 27) | index (a run's entries in its sorted order)
 __global__ __launch_bounds__(kBlock) void k_merge_tile(const unsigned long long* __restrict__ a, const unsigned* __restrict__ av,
                                                        int na, const unsigned long long* __restrict__ b, unsigned bid, int nb,
-                                                       const int* __restrict__ split, unsigned long long* __restrict__ okey,
-                                                       unsigned* __restrict__ oval) {
+                                                       unsigned long long* __restrict__ okey, unsigned* __restrict__ oval) {
     __shared__ unsigned long long sk[kMergeTile];
     __shared__ unsigned sv[kMergeTile];
+    __shared__ int ssplit[2];
     const int t = blockIdx.x;
     const long long d0 = (long long)t * kMergeTile, d1 = std::min(d0 + kMergeTile, (long long)na + nb);
-    const int i0 = split[t], i1 = split[t + 1];
+    if (threadIdx.x < 2) ssplit[threadIdx.x] = merge_split_at(a, na, b, nb, threadIdx.x ? d1 : d0);
+    __syncthreads();
+    const int i0 = ssplit[0], i1 = ssplit[1];
     const int j0 = (int)(d0 - i0), j1 = (int)(d1 - i1);
     const int la = i1 - i0, lb = j1 - j0;
     for (int k = threadIdx.x; k < la; k += kBlock) { sk[k] = a[i0 + k]; sv[k] = av[i0 + k]; }
@@ -958,21 +1000,51 @@ __global__ __launch_bounds__(kBlock) void k_merge_tile(const unsigned long long*
 }
 
 // the index records from the merged order: mpt (xyz, bits(concatenated filtered index)), mnr, ipos,
-// and every B-th key (the leaves' first keys, for the seed search)
-__global__ void k_fifo_gather(const unsigned long long* __restrict__ mkey, const unsigned* __restrict__ mval, int M,
-                              const FifoRun* __restrict__ runs, int B, float4* __restrict__ mpt, float4* __restrict__ mnr,
-                              unsigned* __restrict__ ipos, unsigned long long* __restrict__ lkeys) {
+// every B-th key (the leaves' first keys, for the seed search) — and, fused in (round 6: four launches
+// fewer — k_leaf_boxes, and three small copies), each leaf's box (a segmented min / max over the B
+// lanes of its points: the same values as k_leaf_boxes' serial loop, min / max being exact), the
+// padded leaves' empty boxes, the quantisation after the leaf keys (TreeView::qparams) and this
+// build's clamp count into the host's coherent word.  The run table comes by value.
+__global__ __launch_bounds__(kBlock) void k_fifo_gather(const unsigned long long* __restrict__ mkey,
+                                                        const unsigned* __restrict__ mval, int M, FifoRunTable runs, int B,
+                                                        int L, int P, const float* __restrict__ fq,
+                                                        const unsigned* __restrict__ clamp, unsigned* __restrict__ h_clamp,
+                                                        float4* __restrict__ mpt, float4* __restrict__ mnr,
+                                                        unsigned* __restrict__ ipos, unsigned long long* __restrict__ lkeys,
+                                                        float* __restrict__ leafbox) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= M) return;
-    const unsigned v = mval[k];
-    const FifoRun r = runs[v >> 27];
-    const unsigned pos = v & ((1u << 27) - 1u);
-    const float4 p = r.rpt[pos];
-    const unsigned w = r.off + __float_as_uint(p.w);
-    mpt[k] = make_float4(p.x, p.y, p.z, __uint_as_float(w));
-    mnr[k] = r.rnr[pos];
-    ipos[w] = (unsigned)k;
-    if (k % B == 0) lkeys[k / B] = mkey[k];
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    if (k < M) {
+        const unsigned v = mval[k];
+        const FifoRun r = runs.r[v >> 27];
+        const unsigned pos = v & ((1u << 27) - 1u);
+        const float4 p = r.rpt[pos];
+        const unsigned w = r.off + __float_as_uint(p.w);
+        mpt[k] = make_float4(p.x, p.y, p.z, __uint_as_float(w));
+        mnr[k] = r.rnr[pos];
+        ipos[w] = (unsigned)k;
+        if (k % B == 0) lkeys[k / B] = mkey[k];
+        lo[0] = hi[0] = p.x; lo[1] = hi[1] = p.y; lo[2] = hi[2] = p.z;
+    }
+    // leaf k / B = lanes [k − k % B, … + B) of this wave (B divides 64)
+    for (int o = 1; o < B; o <<= 1) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = fminf(lo[d], __shfl_xor(lo[d], o, 64));
+            hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], o, 64));
+        }
+    }
+    if (k < M && k % B == 0) {
+        float* q = leafbox + (size_t)(k / B) * 6;
+        q[0] = lo[0]; q[1] = lo[1]; q[2] = lo[2]; q[3] = hi[0]; q[4] = hi[1]; q[5] = hi[2];
+    }
+    if (k < P - L) {                           // padded leaves L … P−1: empty boxes
+        float* q = leafbox + (size_t)(L + k) * 6;
+        q[0] = q[1] = q[2] = INFINITY;
+        q[3] = q[4] = q[5] = -INFINITY;
+    }
+    if (k < 4) reinterpret_cast<float*>(lkeys + L)[k] = fq[k];
+    if (k == 0) *h_clamp = *clamp;
 }
 
 }  // namespace
@@ -1034,36 +1106,29 @@ int fifo_run_build(hipStream_t s, const float4* fpt, const float4* fnr, int n, c
 int fifo_keep(hipStream_t s, const unsigned long long* key, const unsigned* val, int n, unsigned live,
               unsigned long long* okey, unsigned* oval, DevBuf& scratch, std::string& err) {
     if (n <= 0) return IMLS_OK;
-    const int nb = (int)grid_for(n);
-    size_t cub_bytes = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (int*)nullptr, (int*)nullptr, nb, s);
-    if (!ensure(scratch, 2 * (((size_t)nb * 4 + 255) / 256 * 256) + cub_bytes + 1024, err)) return IMLS_ERR_DEVICE;
-    char* p = (char*)scratch.p;
-    int* blk = carve<int>(p, nb);
-    int* off = carve<int>(p, nb);
-    void* cub_tmp = carve<char>(p, cub_bytes);
+    const int nb = (n + kKeepTile - 1) / kKeepTile;
+    if (!ensure(scratch, ((size_t)nb * 4 + 255) / 256 * 256 + 1024, err)) return IMLS_ERR_DEVICE;
+    int* blk = (int*)scratch.p;
     k_keep_count<<<nb, kBlock, 0, s>>>(val, n, live, blk);
-    hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, blk, off, nb, s);
-    k_keep_scatter<<<nb, kBlock, 0, s>>>(key, val, n, live, off, okey, oval);
+    k_keep_scatter<<<nb, kBlock, 0, s>>>(key, val, n, live, blk, okey, oval);
     if (hipGetLastError() != hipSuccess) { err = "FIFO compaction launch failed"; return IMLS_ERR_DEVICE; }
     return IMLS_OK;
 }
 
 int fifo_merge(hipStream_t s, const unsigned long long* a, const unsigned* av, int na, const unsigned long long* b,
                unsigned bid, int nb, unsigned long long* okey, unsigned* oval, DevBuf& scratch, std::string& err) {
+    (void)scratch;
+    (void)err;
     const int tiles = (int)(((long long)na + nb + kMergeTile - 1) / kMergeTile);
     if (tiles == 0) return IMLS_OK;
-    if (!ensure(scratch, (size_t)(tiles + 1) * 4 + 256, err)) return IMLS_ERR_DEVICE;
-    int* split = (int*)scratch.p;
-    k_merge_split<<<grid_for(tiles + 1), kBlock, 0, s>>>(a, na, b, nb, tiles, split);
-    k_merge_tile<<<tiles, kBlock, 0, s>>>(a, av, na, b, bid, nb, split, okey, oval);
+    k_merge_tile<<<tiles, kBlock, 0, s>>>(a, av, na, b, bid, nb, okey, oval);
     if (hipGetLastError() != hipSuccess) { err = "FIFO merge launch failed"; return IMLS_ERR_DEVICE; }
     return IMLS_OK;
 }
 
-int fifo_index(hipStream_t s, const unsigned long long* mkey, const unsigned* mval, int M, const FifoRun* runs_dev,
-               const float* fq, int B, DevBuf& lkeys, DevBuf& mpt, DevBuf& nodes, DevBuf& treescratch, int* P_out,
-               int* levels_out, std::string& err) {
+int fifo_index(hipStream_t s, const unsigned long long* mkey, const unsigned* mval, int M, const FifoRunTable& runs,
+               const float* fq, const unsigned* clamp, unsigned* h_clamp, int B, DevBuf& lkeys, DevBuf& mpt, DevBuf& nodes,
+               DevBuf& treescratch, int* P_out, int* levels_out, std::string& err) {
     if (M <= 0) { *P_out = 0; *levels_out = 0; return IMLS_OK; }
     const int L = (M + B - 1) / B;
     int P = 1, levels = 0;
@@ -1078,11 +1143,9 @@ int fifo_index(hipStream_t s, const unsigned long long* mkey, const unsigned* mv
     float* rootsA = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
     float* rootsB = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
     float4* mp = (float4*)mpt.p;
-    k_fifo_gather<<<grid_for(M), kBlock, 0, s>>>(mkey, mval, M, runs_dev, B, mp, mp + M, (unsigned*)(mp + 2 * (size_t)M),
-                                                 (unsigned long long*)lkeys.p);
-    // the quantisation after the leaf keys (TreeView::qparams), as morton_perm places it
-    (void)hipMemcpyAsync((unsigned long long*)lkeys.p + L, fq, 16, hipMemcpyDeviceToDevice, s);
-    tree_rounds(s, mp, M, B, P, levels, (float4*)nodes.p, leafbox, rootsA, rootsB);
+    k_fifo_gather<<<grid_for(M), kBlock, 0, s>>>(mkey, mval, M, runs, B, L, P, fq, clamp, h_clamp, mp, mp + M,
+                                                 (unsigned*)(mp + 2 * (size_t)M), (unsigned long long*)lkeys.p, leafbox);
+    subtree_rounds(s, leafbox, P, levels, (float4*)nodes.p, rootsA, rootsB);
     if (hipGetLastError() != hipSuccess) { err = "FIFO index launch failed"; return IMLS_ERR_DEVICE; }
     *P_out = P;
     *levels_out = levels;

@@ -338,6 +338,7 @@ struct FifoRun {
     unsigned pad;
 };
 constexpr int kMaxFifoRuns = 32;       // run ids (5 bits of a merged entry's value; 27 bits of position)
+struct FifoRunTable { FifoRun r[kMaxFifoRuns]; };   // by value in the gather launch (768 B of arguments)
 inline size_t fifo_part(size_t bytes) { return (bytes + 255) / 256 * 256; }
 inline size_t fifo_run_bytes(int n) { return fifo_part((size_t)n * 8) + 2 * fifo_part((size_t)n * 16); }
 inline unsigned long long* fifo_run_keys(void* run, int) { return (unsigned long long*)run; }
@@ -359,9 +360,10 @@ int fifo_keep(hipStream_t s, const unsigned long long* key, const unsigned* val,
 int fifo_merge(hipStream_t s, const unsigned long long* a, const unsigned* av, int na, const unsigned long long* b,
                unsigned bid, int nb, unsigned long long* okey, unsigned* oval, DevBuf& scratch, std::string& err);
 // the target index from the merged order (records, ipos, leaf keys + fq, leaf boxes, tree)
-int fifo_index(hipStream_t s, const unsigned long long* mkey, const unsigned* mval, int M, const FifoRun* runs_dev,
-               const float* fq, int B, DevBuf& lkeys, DevBuf& mpt, DevBuf& nodes, DevBuf& treescratch, int* P_out,
-               int* levels_out, std::string& err);
+// (clamp: the device clamp counter, copied to the host's coherent word h_clamp behind the build)
+int fifo_index(hipStream_t s, const unsigned long long* mkey, const unsigned* mval, int M, const FifoRunTable& runs,
+               const float* fq, const unsigned* clamp, unsigned* h_clamp, int B, DevBuf& lkeys, DevBuf& mpt, DevBuf& nodes,
+               DevBuf& treescratch, int* P_out, int* levels_out, std::string& err);
 
 // project.hip
 // k_knn_wave → k_finish (+ the exact k_project_lane fallback for uncertified queries); lane_mode
