@@ -350,12 +350,18 @@ namespace {
 constexpr int kMortonSortLo = 0;
 
 // Permutation (sorted → input index) of n float4 points by 48-bit Morton code over their bbox.
-// With lkeys: also the first key of each B-point leaf and the quantisation (seed search).
+// With lkeys: also the first key of each B-point leaf and the quantisation (seed search).  The sort
+// is double-buffered (round 6: the plain form ended in two copy-back launches of keys and values);
+// *perm_out = the buffer holding the permutation — perm's own storage when the caller needs it there
+// (need_in_perm: one device copy if the sort left it in scratch), else possibly scratch.
 int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf& perm, std::string& err,
-                DevBuf* lkeys = nullptr, int B = 0) {
+                DevBuf* lkeys = nullptr, int B = 0, const unsigned** perm_out = nullptr) {
     size_t cub_bytes = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                       (unsigned*)nullptr, (unsigned*)nullptr, n, kMortonSortLo, 48, s);
+    {
+        hipcub::DoubleBuffer<unsigned long long> kq(nullptr, nullptr);
+        hipcub::DoubleBuffer<unsigned> vq(nullptr, nullptr);
+        hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, kq, vq, n, kMortonSortLo, 48, s);
+    }
     const int bb_parts = 512;
     size_t need = 2 * (((size_t)n * 8 + 255) / 256 * 256) + (((size_t)n * 4 + 255) / 256 * 256) +
                   ((cub_bytes + 255) / 256) * 256 + bb_parts * 24 + 1024;
@@ -377,8 +383,15 @@ int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf
     k_bbox_partial<<<nb, kBlock, 0, s>>>(pts, n, bbpart);
     k_bbox_final<<<1, kBlock, 0, s>>>(bbpart, nb, bbox, qp);
     k_morton<<<grid_for(n), kBlock, 0, s>>>(pts, n, qp, k0, v0);
-    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, (unsigned*)perm.p, n, kMortonSortLo, 48, s);
-    if (lkeys) k_leaf_keys<<<grid_for(L), kBlock, 0, s>>>(k1, n, B, (unsigned long long*)lkeys->p);
+    hipcub::DoubleBuffer<unsigned long long> kb(k0, k1);
+    hipcub::DoubleBuffer<unsigned> vb(v0, (unsigned*)perm.p);
+    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, kb, vb, n, kMortonSortLo, 48, s);
+    if (lkeys) k_leaf_keys<<<grid_for(L), kBlock, 0, s>>>(kb.Current(), n, B, (unsigned long long*)lkeys->p);
+    if (perm_out) {
+        *perm_out = vb.Current();
+    } else if (vb.Current() != (unsigned*)perm.p) {
+        (void)hipMemcpyAsync(perm.p, vb.Current(), (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+    }
     if (hipGetLastError() != hipSuccess) { err = "morton sort launch failed"; return IMLS_ERR_DEVICE; }
     return IMLS_OK;
 }
@@ -398,7 +411,8 @@ int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& t
     int P = 1, levels = 0;
     while (P < L) { P <<= 1; ++levels; }
     if (levels > kStackDepth - 1) { err = "tree too deep for the traversal stack"; return IMLS_ERR_CAPACITY; }
-    int rc = morton_perm(s, (const float4*)tpt.p, M, scratch, permbuf, err, &lkeys, B);
+    const unsigned* perm = nullptr;
+    int rc = morton_perm(s, (const float4*)tpt.p, M, scratch, permbuf, err, &lkeys, B, &perm);
     if (rc) return rc;
     size_t need = ((size_t)P * 24 + 255) / 256 * 256 + 2 * (((size_t)P / kBlock + 1) * 24 + 256) + 1024;
     if (!ensure(treescratch, need, err) || !ensure(mpt, (size_t)M * 36 + 64, err) ||
@@ -408,7 +422,7 @@ int build_target_tree(hipStream_t s, int M, int bucket, DevBuf& lkeys, DevBuf& t
     float* leafbox = carve<float>(p, (size_t)P * 6);
     float* rootsA = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
     float* rootsB = carve<float>(p, ((size_t)P / kBlock + 1) * 6);
-    k_gather<<<grid_for(M), kBlock, 0, s>>>((const float4*)tpt.p, (const float4*)tnr.p, (const unsigned*)permbuf.p, M,
+    k_gather<<<grid_for(M), kBlock, 0, s>>>((const float4*)tpt.p, (const float4*)tnr.p, perm, M,
                                             (float4*)mpt.p, (float4*)mpt.p + M, (unsigned*)((float4*)mpt.p + 2 * (size_t)M));
     tree_rounds(s, (const float4*)mpt.p, M, B, P, levels, (float4*)nodes.p, leafbox, rootsA, rootsB);
     if (hipGetLastError() != hipSuccess) { err = "index build launch failed"; return IMLS_ERR_DEVICE; }
@@ -716,9 +730,13 @@ int build_batch(hipStream_t s, std::vector<BuildJob>& jobs, DevBuf& scratch, Dev
     }
     int end_bit = 48;
     while ((1ll << (end_bit - 48)) < nj) ++end_bit;
+    // double-buffered sort (round 6: the plain form copied keys and values back at its end)
     size_t cub_bytes = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                       (unsigned*)nullptr, (unsigned*)nullptr, (int)std::max<size_t>(total, 1), kMortonSortLo, end_bit, s);
+    {
+        hipcub::DoubleBuffer<unsigned long long> kq(nullptr, nullptr);
+        hipcub::DoubleBuffer<unsigned> vq(nullptr, nullptr);
+        hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, kq, vq, (int)std::max<size_t>(total, 1), kMortonSortLo, end_bit, s);
+    }
     const size_t need = 2 * ((total * 8 + 255) / 256 * 256) + 2 * ((total * 4 + 255) / 256 * 256) +
                         (cub_bytes + 255) / 256 * 256 + (size_t)nj * (kBBoxParts * 6 * 4 + 256) + (leaf_floats + root_floats) * 4 +
                         (size_t)nj * 4 * 256 + 4096;
@@ -786,8 +804,10 @@ int build_batch(hipStream_t s, std::vector<BuildJob>& jobs, DevBuf& scratch, Dev
     k_bbox_b<<<dim3(std::min<unsigned>(kBBoxParts, gx), nj), kBlock, 0, s>>>(jd);
     k_qparams_b<<<nj, 64, 0, s>>>(jd);
     k_morton_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd, k0, v0);
-    if (total > 0) hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, k1, v0, v1, (int)total, kMortonSortLo, end_bit, s);
-    k_place_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd, k1, v1);
+    hipcub::DoubleBuffer<unsigned long long> kb(k0, k1);
+    hipcub::DoubleBuffer<unsigned> vb(v0, v1);
+    if (total > 0) hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, kb, vb, (int)total, kMortonSortLo, end_bit, s);
+    k_place_b<<<dim3(gx, nj), kBlock, 0, s>>>(jd, kb.Current(), vb.Current());
     bool any_tree = false;
     for (auto& b : jobs) any_tree |= b.B > 0 && b.n > 0;
     if (any_tree) {
@@ -836,15 +856,18 @@ __global__ void k_morton_fq(const float4* __restrict__ pt, int n, const float* _
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(clamp, (unsigned)__popcll(m));
 }
 
-// a run's Morton-ordered records: rpt = (xyz, bits(local filtered index)), rnr
+// a run's Morton-ordered records: rpt = (xyz, bits(local filtered index)), rnr, and its sorted keys
+// (from wherever the double-buffered sort left them: no copy-back launches)
 __global__ void k_run_gather(const float4* __restrict__ pt, const float4* __restrict__ nr, const unsigned* __restrict__ perm,
-                             int n, float4* __restrict__ rpt, float4* __restrict__ rnr) {
+                             const unsigned long long* __restrict__ skey, int n, float4* __restrict__ rpt,
+                             float4* __restrict__ rnr, unsigned long long* __restrict__ rkey) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const unsigned j = perm[k];
     const float4 p = pt[j];
     rpt[k] = make_float4(p.x, p.y, p.z, __uint_as_float(j));
     rnr[k] = nr[j];
+    rkey[k] = skey[k];
 }
 
 // the FIFO quantisation frame: a cube of side 2 × the runs' largest bbox extent, its origin half an
@@ -1052,11 +1075,14 @@ __global__ __launch_bounds__(kBlock) void k_fifo_gather(const unsigned long long
 size_t fifo_scratch_bytes(int max_run, int nruns, int M) {
     size_t sort_b = 0, scan_b = 0;
     const int nb = (int)grid_for((size_t)std::max(M, 1));
-    hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                       (unsigned*)nullptr, (unsigned*)nullptr, std::max(max_run, 1), 0, 48);
+    {
+        hipcub::DoubleBuffer<unsigned long long> kq(nullptr, nullptr);
+        hipcub::DoubleBuffer<unsigned> vq(nullptr, nullptr);
+        hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, kq, vq, std::max(max_run, 1), 0, 48);
+    }
     hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, (int*)nullptr, (int*)nullptr, nb);
     const size_t n = (size_t)std::max(max_run, 1);
-    const size_t run = (n * 8 + 255) / 256 * 256 + 2 * ((n * 4 + 255) / 256 * 256) + (sort_b + 255) / 256 * 256 + 1024;
+    const size_t run = 2 * ((n * 8 + 255) / 256 * 256) + 2 * ((n * 4 + 255) / 256 * 256) + (sort_b + 255) / 256 * 256 + 1024;
     const size_t frame = (size_t)std::max(nruns, 1) * 64 * 24 + 1024;
     const size_t keep = 2 * (((size_t)nb * 4 + 255) / 256 * 256) + scan_b + 1024;
     const size_t merge = ((size_t)M / kMergeTile + 2) * 4 + 256;
@@ -1085,20 +1111,29 @@ int fifo_run_build(hipStream_t s, const float4* fpt, const float4* fnr, int n, c
                    DevBuf& run, DevBuf& scratch, std::string& err) {
     if (n <= 0) return IMLS_OK;
     if (n >= (1 << 27)) { err = "scan too large for the FIFO index"; return IMLS_ERR_CAPACITY; }
+    // double-buffered sort (round 6: the plain form ended in two copy-back launches, ~14 µs with their
+    // gaps on a 126k-point scan); k_run_gather takes the keys from the current buffer
     size_t cub_bytes = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                       (unsigned*)nullptr, (unsigned*)nullptr, n, 0, 48, s);
-    const size_t need = ((size_t)n * 8 + 255) / 256 * 256 + 2 * (((size_t)n * 4 + 255) / 256 * 256) + ((cub_bytes + 255) / 256) * 256 + 1024;
+    {
+        hipcub::DoubleBuffer<unsigned long long> kq(nullptr, nullptr);
+        hipcub::DoubleBuffer<unsigned> vq(nullptr, nullptr);
+        hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, kq, vq, n, 0, 48, s);
+    }
+    const size_t need = 2 * (((size_t)n * 8 + 255) / 256 * 256) + 2 * (((size_t)n * 4 + 255) / 256 * 256) +
+                        ((cub_bytes + 255) / 256) * 256 + 1024;
     if (!ensure(scratch, need, err) || !ensure(run, fifo_run_bytes(n), err)) return IMLS_ERR_DEVICE;
     char* p = (char*)scratch.p;
     unsigned long long* k0 = carve<unsigned long long>(p, n);
+    unsigned long long* k1 = carve<unsigned long long>(p, n);
     unsigned* v0 = carve<unsigned>(p, n);
     unsigned* v1 = carve<unsigned>(p, n);
     void* cub_tmp = carve<char>(p, cub_bytes);
-    unsigned long long* rkey = fifo_run_keys(run.p, n);
     k_morton_fq<<<grid_for(n), kBlock, 0, s>>>(fpt, n, fq, k0, v0, clamp);
-    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k0, rkey, v0, v1, n, 0, 48, s);
-    k_run_gather<<<grid_for(n), kBlock, 0, s>>>(fpt, fnr, v1, n, fifo_run_pts(run.p, n), fifo_run_nrm(run.p, n));
+    hipcub::DoubleBuffer<unsigned long long> kb(k0, k1);
+    hipcub::DoubleBuffer<unsigned> vb(v0, v1);
+    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, kb, vb, n, 0, 48, s);
+    k_run_gather<<<grid_for(n), kBlock, 0, s>>>(fpt, fnr, vb.Current(), kb.Current(), n, fifo_run_pts(run.p, n),
+                                                fifo_run_nrm(run.p, n), fifo_run_keys(run.p, n));
     if (hipGetLastError() != hipSuccess) { err = "FIFO run build launch failed"; return IMLS_ERR_DEVICE; }
     return IMLS_OK;
 }
