@@ -911,13 +911,16 @@ __global__ void k_fifo_frame(const float* __restrict__ part, int nparts, float* 
 // instead of a device-wide scan launch
 __device__ __forceinline__ bool live_entry(unsigned v, unsigned live) { return (live >> (v >> 27)) & 1u; }
 constexpr int kKeepPer = 16;
-constexpr int kKeepTile = kBlock * kKeepPer;
+constexpr int kKeepTile = kBlock * kKeepPer;   // entries per block: kKeepPer rounds of kBlock, coalesced
 __global__ __launch_bounds__(kBlock) void k_keep_count(const unsigned* __restrict__ val, int n, unsigned live, int* __restrict__ blk) {
     __shared__ int wc[kBlock / 64];
-    const int base = blockIdx.x * kKeepTile + threadIdx.x * kKeepPer;
+    const int base = blockIdx.x * kKeepTile + threadIdx.x;
     int c = 0;
 #pragma unroll
-    for (int k = 0; k < kKeepPer; ++k) c += (base + k < n && live_entry(val[base + k], live)) ? 1 : 0;
+    for (int k = 0; k < kKeepPer; ++k) {
+        const int i = base + k * kBlock;
+        c += (i < n && live_entry(val[i], live)) ? 1 : 0;
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
     if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
@@ -931,7 +934,7 @@ __global__ __launch_bounds__(kBlock) void k_keep_count(const unsigned* __restric
 __global__ __launch_bounds__(kBlock) void k_keep_scatter(const unsigned long long* __restrict__ key, const unsigned* __restrict__ val,
                                                          int n, unsigned live, const int* __restrict__ blk,
                                                          unsigned long long* __restrict__ okey, unsigned* __restrict__ oval) {
-    __shared__ int wsum[kBlock / 64];
+    __shared__ int wsum[kKeepPer][kBlock / 64];
     __shared__ int s_off;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     // this tile's output offset: Σ of the earlier tiles' counts
@@ -939,37 +942,40 @@ __global__ __launch_bounds__(kBlock) void k_keep_scatter(const unsigned long lon
     for (int b = tid; b < (int)blockIdx.x; b += kBlock) pre += blk[b];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
-    if (lane == 0) wsum[wv] = pre;
+    if (lane == 0) wsum[0][wv] = pre;
     __syncthreads();
     if (tid == 0) {
         int t = 0;
-        for (int k = 0; k < kBlock / 64; ++k) t += wsum[k];
+        for (int k = 0; k < kBlock / 64; ++k) t += wsum[0][k];
         s_off = t;
     }
     __syncthreads();
-    const int base = blockIdx.x * kKeepTile + tid * kKeepPer;
-    unsigned keepm = 0;
+    // every round's wave counts first (one barrier), then each entry's rank in tile order
+    const int base = blockIdx.x * kKeepTile + tid;
+    unsigned long long m[kKeepPer];
 #pragma unroll
-    for (int k = 0; k < kKeepPer; ++k) keepm |= (base + k < n && live_entry(val[base + k], live)) ? (1u << k) : 0u;
-    const int c = __popc(keepm);
-    // block-exclusive prefix of the per-thread counts (thread order = entry order)
-    int inc = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += u;
+    for (int k = 0; k < kKeepPer; ++k) {
+        const int i = base + k * kBlock;
+        m[k] = __ballot(i < n && live_entry(val[i], live));
+        if (lane == 0) wsum[k][wv] = __popcll(m[k]);
     }
     __syncthreads();
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    int o = s_off + inc - c;
-    for (int k = 0; k < wv; ++k) o += wsum[k];
+    int run = s_off;
+#pragma unroll
     for (int k = 0; k < kKeepPer; ++k) {
-        if ((keepm >> k) & 1u) {
-            okey[o] = key[base + k];
-            oval[o] = val[base + k];
-            ++o;
+        int before = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) {
+            before += w < wv ? wsum[k][w] : 0;
+            tot += wsum[k][w];
         }
+        if ((m[k] >> lane) & 1ull) {
+            const int i = base + k * kBlock;
+            const int o = run + before + __popcll(m[k] & ((1ull << lane) - 1ull));
+            okey[o] = key[i];
+            oval[o] = val[i];
+        }
+        run += tot;
     }
 }
 
@@ -986,9 +992,11 @@ __device__ __forceinline__ int merge_split_at(const unsigned long long* __restri
     return lo;
 }
 // one output tile of kMergeTile: its two splits by binary search on the diagonals (threads 0 / 1;
-// round 6: a separate split launch before), both input segments in LDS, each entry's output rank = its
-// index in its own segment + the other segment's entries before it (B: strictly smaller keys after
-// A's equal ones).  B's values are (bid << 27) | index (a run's entries in its sorted order)
+// round 6: a separate split launch before), both input segments in LDS; then each thread finds its own
+// diagonal split of the tile (one binary search in LDS) and merges its kMergePer consecutive outputs
+// sequentially (round 6: one binary search per output before), A first on equal keys.  B's values
+// are (bid << 27) | index (a run's entries in its sorted order)
+constexpr int kMergePer = kMergeTile / kBlock;
 __global__ __launch_bounds__(kBlock) void k_merge_tile(const unsigned long long* __restrict__ a, const unsigned* __restrict__ av,
                                                        int na, const unsigned long long* __restrict__ b, unsigned bid, int nb,
                                                        unsigned long long* __restrict__ okey, unsigned* __restrict__ oval) {
@@ -1005,20 +1013,24 @@ __global__ __launch_bounds__(kBlock) void k_merge_tile(const unsigned long long*
     for (int k = threadIdx.x; k < la; k += kBlock) { sk[k] = a[i0 + k]; sv[k] = av[i0 + k]; }
     for (int k = threadIdx.x; k < lb; k += kBlock) { sk[la + k] = b[j0 + k]; sv[la + k] = (bid << 27) | (unsigned)(j0 + k); }
     __syncthreads();
-    for (int k = threadIdx.x; k < la + lb; k += kBlock) {
-        const unsigned long long key = sk[k];
-        int r;
-        if (k < la) {                          // # B keys < key
-            int lo = la, hi = la + lb;
-            while (lo < hi) { const int mid = (lo + hi) >> 1; if (sk[mid] < key) lo = mid + 1; else hi = mid; }
-            r = k + (lo - la);
-        } else {                               // # A keys <= key
-            int lo = 0, hi = la;
-            while (lo < hi) { const int mid = (lo + hi) >> 1; if (sk[mid] <= key) lo = mid + 1; else hi = mid; }
-            r = (k - la) + lo;
-        }
-        okey[d0 + r] = key;
-        oval[d0 + r] = sv[k];
+    // this thread's outputs [q, q + kMergePer) of the tile: x of A's entries before output q
+    const int q = threadIdx.x * kMergePer, n = la + lb;
+    if (q >= n) return;
+    int lo = max(0, q - lb), hi = min(q, la);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sk[mid] <= sk[la + q - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    int x = lo, y = q - lo;
+    const int qe = min(q + kMergePer, n);
+    for (int r = q; r < qe; ++r) {
+        const bool takeA = y >= lb || (x < la && sk[x] <= sk[la + y]);
+        const int src = takeA ? x : la + y;
+        okey[d0 + r] = sk[src];
+        oval[d0 + r] = sv[src];
+        x += takeA ? 1 : 0;
+        y += takeA ? 0 : 1;
     }
 }
 
