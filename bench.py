@@ -1116,7 +1116,10 @@ def main():
             dist.destroy_process_group()
         return
 
-    traffic = None
+    # PMC traffic per launch (rocprofv3 counters cannot be read from inside this process): the
+    # pmc_traffic.json of a PMC pass of this same workload — tools/measure_round.sh runs its passes
+    # first and hands this run the fresh file; the driver's plain run reads the round's committed one
+    traffic = traffic_meta = None
     tj = pathlib.Path(args.traffic_json)
     stats0 = probe_ctx.index_stats()
     if tj.exists() and args.workload == "B":
@@ -1124,6 +1127,9 @@ def main():
             tdat = json.loads(tj.read_text())
             if tdat.get("queries") == stats0["queries"] and tdat.get("iters") == args.iters:
                 traffic = tdat.get("bytes_per_launch")
+                traffic_meta = {"source": str(tj), "fetch_factor": tdat.get("fetch_factor", 2.0),
+                                "ratio_vs_algorithmic": tdat.get("ratio_vs_algorithmic"),
+                                "calibrated": "calibration" in tdat, "scope": tdat.get("scope")}
         except (ValueError, OSError):
             traffic = None
 
@@ -1164,6 +1170,7 @@ def main():
                   "sequences on one device clock, busy pass)",
         "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "traffic": traffic,
+        "traffic_meta": traffic_meta,
         "algorithmic_bytes_per_step": bytes_per_step,
         "aggregate_GBps": agg,
         "aggregate_frac": agg / HBM_PEAK_GBS,

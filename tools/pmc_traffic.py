@@ -1,16 +1,23 @@
-"""HBM traffic per projection launch from the PMC passes of tools/measure_round.sh.
+"""HBM-side traffic per projection launch from the PMC passes of tools/measure_round.sh.
 
-traffic = 2·FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md § HBM: on gfx950 FETCH_SIZE reports ½ of
-the bytes of wide coalesced reads; WRITE_SIZE is exact for 16-B stores), per launch of
-k_knn_wave + k_finish, averaged over the dispatches of the PMC runs.  rocprofv3 reports both
-counters in KB.  Writes profiles/pmc_traffic.json (read by bench.py) and a copy next to the round's
-profiles.
-usage: python tools/pmc_traffic.py gpurun_out/measure profiles/<round_tag>
+traffic = 2·FETCH_SIZE + WRITE_SIZE per launch of k_knn_wave + k_finish, averaged over the dispatches of
+the PMC runs (rocprofv3 reports both counters in KB).  The factor 2 is calibrated for THIS access
+pattern by tools/calib/gather_cal (round 6): MI355X_MICROARCH.md §HBM gives ½ for wide coalesced
+streaming reads only; the calibration kernels read a known number of bytes as random 16-B float4 gathers
+(k_finish's list points and normals, the traversal's leaf rows) and show one 64-B FETCH_SIZE tally per
+gathered row — also when two gathers fall in the two different 64-B halves of one 128-B line
+(pair_h = pair_s), so a miss fetches a whole 128-B line and is tallied as 64 B: counted × 2 = bytes
+moved, the same factor as streaming.  FETCH_SIZE counts L2 misses served by the Infinity Cache too
+(40-MB table: 3.6 tallies per row vs 3.97 from HBM), so this is L2 ↔ fabric traffic; config B's 40-MB
+Morton map stays resident in the 256-MB Infinity Cache, so the HBM share of it is lower.
+usage: python tools/pmc_traffic.py <measure_dir> <profiles/round_dir> [gather_cal.json]
+Writes <profiles/round_dir>/pmc_traffic.json and <measure_dir>/pmc_traffic.json (bench.py --traffic-json).
 """
 import collections, csv, json, pathlib, sys
 
 src = pathlib.Path(sys.argv[1])
 dst = pathlib.Path(sys.argv[2])
+cal = json.loads(pathlib.Path(sys.argv[3]).read_text()) if len(sys.argv) > 3 and pathlib.Path(sys.argv[3]).exists() else None
 per = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     f = next((src / f"pmc_{c}").rglob("*counter_collection.csv"))
@@ -22,7 +29,14 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
 jf = src / "pmc_FETCH_SIZE.json"
 jf = jf if jf.exists() else src / "pmc_FETCH_SIZE.out"
 bench = json.loads(jf.read_text().strip().splitlines()[-1])
-kern = {k: 2 * per["FETCH_SIZE"].get(k, 0.0) + per["WRITE_SIZE"].get(k, 0.0) for k in ("k_knn_wave", "k_finish")}
+factor = 2.0
+kern = {k: factor * per["FETCH_SIZE"].get(k, 0.0) + per["WRITE_SIZE"].get(k, 0.0) for k in ("k_knn_wave", "k_finish")}
+alg = None
+try:
+    sp = bench["roofline"]["serialised_single_pair"]
+    alg = sp["algorithmic_bytes_per_launch"]
+except (KeyError, TypeError):
+    pass
 out = {
     "queries": bench["config"]["queries"],
     "iters": bench["config"]["icp_iterations"],
@@ -30,9 +44,25 @@ out = {
     "per_kernel_bytes": kern,
     "fetch_size_bytes_raw": per["FETCH_SIZE"],
     "write_size_bytes": per["WRITE_SIZE"],
-    "formula": "2*FETCH_SIZE + WRITE_SIZE (KB->bytes), per launch, k_knn_wave + k_finish",
+    "fetch_factor": factor,
+    "formula": "fetch_factor*FETCH_SIZE + WRITE_SIZE (KB->bytes), per launch, k_knn_wave + k_finish",
+    "algorithmic_bytes_per_launch": alg,
+    "ratio_vs_algorithmic": sum(kern.values()) / alg if alg else None,
+    "scope": "L2 <-> fabric bytes (Infinity-Cache hits included), not HBM-only",
 }
+if cal:
+    p = cal["patterns"]
+    out["calibration"] = {
+        "source": "tools/calib/gather_cal (known-byte kernels, separate FETCH_SIZE / WRITE_SIZE passes)",
+        "counted_per_read_byte": {k: v["counted_per_read_byte"] for k, v in p.items()},
+        "write_counted_per_byte": {k: v["write_counted_per_byte"] for k, v in p.items()},
+        "factor_stream": cal.get("factor_stream"),
+        "rand16_tally_per_row_bytes": {k: 16.0 * p[k]["counted_per_read_byte"] for k in p if k.startswith("rand16")},
+        "line_granularity": ("128 B: pair_h (two rows in different 64-B halves of one line) tallies as pair_s "
+                             "(one 32-B sector), pair_l (two lines) twice"),
+        "fetch_factor_gather16": factor,
+    }
 dst.mkdir(parents=True, exist_ok=True)
 (dst / "pmc_traffic.json").write_text(json.dumps(out, indent=1))
-pathlib.Path("profiles/pmc_traffic.json").write_text(json.dumps(out, indent=1))
+(src / "pmc_traffic.json").write_text(json.dumps(out, indent=1))
 print(json.dumps(out, indent=1))
