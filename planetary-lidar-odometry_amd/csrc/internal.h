@@ -379,10 +379,18 @@ void launch_project(hipStream_t s, const TreeView& t, const float4* spt, const f
 constexpr int kMaxKL = 46;       // list entries per query at most (the lone-frame path: K + 12 for K ≤ 32, capped)
 // per-query reference position + list guarantee (float4 xref[N]) and the key the list's answer
 // relied on (float nref[N]), after the [kMaxKL+1][N] list block
-inline float4* xref_of(int* lists, int N) {
+__host__ __device__ inline float4* xref_of(int* lists, int N) {
     return reinterpret_cast<float4*>(reinterpret_cast<char*>(lists) + ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256);
 }
-inline size_t prevnn_bytes(int N) { return ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256 + (size_t)N * 20; }
+// then the compacted traversal list of the packet kernel's later ICP iterations (round 6: the slots
+// whose list could not be reused, unsigned cmp[N]) and its count (one word, zeroed by k_finish)
+__host__ __device__ inline unsigned* cmp_of(int* lists, int N) {
+    return reinterpret_cast<unsigned*>(reinterpret_cast<char*>(xref_of(lists, N)) + ((size_t)N * 20 + 255) / 256 * 256);
+}
+__host__ __device__ inline unsigned* cmp_count_of(int* lists, int N) { return cmp_of(lists, N) + ((size_t)N + 63) / 64 * 64; }
+inline size_t prevnn_bytes(int N) {
+    return ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256 + ((size_t)N * 20 + 255) / 256 * 256 + ((size_t)N + 63) / 64 * 256 + 512;
+}
 constexpr int kStatSkipped = 6;   // nbr_stats slot: lanes whose list was reused without traversal
 int project_blocks(int N);
 // k_finish: the exact stage one lane per query (0) or one quad per query (1: round 6, measured slower —

@@ -53,6 +53,10 @@ constexpr int kFallbackBlocksBatched = 4;   // physical blocks per frame of a la
 // queries per k_finish block = per pass-1 slab (the quad exact stage: 64; the one-lane form: 256)
 constexpr int kFinishPerBlock = IMLS_FINISH_QUAD ? kWaveBlock / 4 : kWaveBlock;
 static_assert(kFinishPerBlock == kPass1Block && kFallbackBlocks == kPass1Fallback, "pass-1 slab layout (solve.hip)");
+// the later ICP iterations' packet traversal in two launches (reuse decision + compacted walk, round 6)
+#ifndef IMLS_COMPACT
+#define IMLS_COMPACT 1
+#endif
 constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
 constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
 constexpr int kFStack = 256;        // frontier traversal's stack per wave (see knn_qwave_body)
@@ -489,7 +493,16 @@ __device__ __forceinline__ float need_key_ids(const float (&lk)[KL], float r2, i
 // Slot-id keys in registers, positions in LDS: ~96 VGPRs and ~29 KB of LDS per 4-wave block — 5
 // waves/SIMD (round 4: the register list needed 160 VGPRs, 3 waves/SIMD; config B 331 → 406 pairs/s)
 #define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 26 ? 5 : 2)))
-template <int KL>
+// MODE (round 6, the later ICP iterations of the packet traversal, use_prev):
+//   0  one pass — every lane decides reuse and the packets walk for the lanes that cannot reuse;
+//   1  the reuse decision only (Verlet skip, prefill certificate): a reused list is settled here,
+//      every other slot is appended to the compacted list cmp (a wave's run by one atomic: the run
+//      order varies, the results cannot — the traversal only bounds lists that k_finish certifies);
+//   2  the walk over the compacted slots, 64 to a packet: packets of the queries that really
+//      re-traverse, instead of every packet walking for the few of its lanes that do (mid
+//      iterations: most lanes reuse their lists).  The lane redoes MODE 1's decision (same inputs,
+//      same outcome), its prefill included.
+template <int KL, int MODE = 0>
 __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
                                                          const double* __restrict__ pose,
@@ -498,7 +511,8 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                                                          int* __restrict__ lists, float* __restrict__ wlist,
                                                          float4* __restrict__ xref, float* __restrict__ nref,
                                                          int use_prev, unsigned long long* __restrict__ nbr_stats,
-                                                         int bx) {
+                                                         int bx, unsigned* __restrict__ cmp = nullptr,
+                                                         unsigned* __restrict__ cmp_count = nullptr) {
     if (done && ld_const(done)) return;
     __shared__ int snode[kWaveBlock / 64][kWaveStack];
     __shared__ float4 sboxa[kWaveBlock / 64][kWaveStack];   // stacked node boxes: lo.xyz, hi.x
@@ -513,8 +527,17 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     // most lanes seed: a smaller packet's union of neighbourhoods is smaller, and the launch lasts
     // as long as its slowest wave); lanes past the packet idle
     const int qp = kp.packet;
-    const int slot = (bx * (kWaveBlock / 64) + wv) * qp + lane;
-    const bool active = lane < qp && slot < N;
+    const int pslot = (bx * (kWaveBlock / 64) + wv) * qp + lane;
+    int slot = pslot;
+    bool active = lane < qp && slot < N;
+    if constexpr (MODE == 2) {
+        // packet = compacted entries [wave·qp, wave·qp + qp); the count is the prep launch's (no
+        // block barrier in this mode: use_prev — a wave past it leaves at once)
+        const int cnt = ld_const((const int*)cmp_count);
+        if ((bx * (kWaveBlock / 64) + wv) * qp >= cnt) return;
+        active = lane < qp && pslot < cnt;
+        slot = active ? (int)cmp[pslot] : 0;
+    }
     float xf[3] = {0.f, 0.f, 0.f};
     // the stored list's bound and reference (slot-indexed) load beside the query's point: one round
     // trip after the query index, not one more after the transform
@@ -638,6 +661,21 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             const float nk = need_();
             if (nk < kInfF && nk * (1.0f + 1e-5f) < wlow) { skip = true; wskip = wlow; }
         }
+    }
+    if constexpr (MODE == 1) {
+        // settle the reused lists; compact the rest for the MODE 2 walk
+        if (active && skip) wlist[slot] = wskip;
+        const unsigned long long sk = __ballot(skip);
+        if (nbr_stats && lane == 0 && sk) atomicAdd(&nbr_stats[kStatSkipped], (unsigned long long)__popcll(sk));
+        const bool need = active && !skip;
+        const unsigned long long nm = __ballot(need);
+        if (nm) {
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(cmp_count, (unsigned)__popcll(nm));
+            base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
+            if (need) cmp[base + (unsigned)__popcll(nm & ((1ull << lane) - 1ull))] = (unsigned)slot;
+        }
+        return;
     }
     // leaf scan shared by the seed pass and the traversal: the lanes in `want` test every point of
     // leaf `leaf` against their bound; `listed`: the leaf may hold points already in a lane's
@@ -1488,6 +1526,8 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid == IMLS_NUM_REJ + 2 && rej_s[tid]) atomicAdd(&nbr_stats[5], (unsigned long long)rej_s[tid]);
+    // the compacted walk of this iteration has read its count: zero it for the next iteration's prep
+    if (bx == 0 && tid == 0) *cmp_count_of(const_cast<int*>(lists), N) = 0u;
 }
 
 // =============================================================================================
@@ -1864,6 +1904,8 @@ __device__ __forceinline__ void finish4_body(TreeView t, const float4* __restric
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid == IMLS_NUM_REJ + 2 && rej_s[tid]) atomicAdd(&nbr_stats[5], (unsigned long long)rej_s[tid]);
+    // the compacted walk of this iteration has read its count: zero it for the next iteration's prep
+    if (bx == 0 && tid == 0) *cmp_count_of(const_cast<int*>(lists), N) = 0u;
 }
 
 // =============================================================================================
@@ -2359,6 +2401,16 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(
                       (int)blockIdx.x);
 }
 
+template <int KL, int MODE>
+__global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_m(
+        TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
+        const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
+        int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
+        unsigned long long* __restrict__ nbr_stats) {
+    knn_wave_body<KL, MODE>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, 1, nbr_stats,
+                            (int)blockIdx.x, cmp_of(lists, N), cmp_count_of(lists, N));
+}
+
 template <int KL>
 __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave(
         TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
@@ -2462,6 +2514,20 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const P
                                 bx);
 }
 
+template <int KL, int MODE>
+__global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_mb(const PairDev* __restrict__ tab, KParams kp,
+                                                                           int npairs) {
+    int f, bx;
+    batch_block(kp.xcd, f, bx);
+    if (f >= npairs) return;
+    const PairDev A = device_view(tab + f);
+    if (use_qwave(kp, A.N) || bx >= knn_blocks_of(A.N, kp.packet)) return;
+    float4* xref = xref_dev(A.lists, A.N);
+    knn_wave_body<KL, MODE>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
+                            wlist_of<KL>(A.lists, A.N), xref, reinterpret_cast<float*>(xref + A.N), 1, A.stats, bx,
+                            cmp_of(A.lists, A.N), cmp_count_of(A.lists, A.N));
+}
+
 template <int KL>
 __global__ __launch_bounds__(kWaveBlock) void k_knn_qwave_b(const PairDev* __restrict__ tab, KParams kp, int use_prev,
                                                             int npairs) {
@@ -2511,7 +2577,12 @@ void launch_wave_batch(hipStream_t s, const PairDev* tab, int npairs, int maxN, 
     }
     if (any_large) {
         const int kb = knn_blocks_of(maxN, kp.packet);
-        k_knn_wave_b<KL><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        if (use_prev && IMLS_COMPACT) {
+            k_knn_wave_mb<KL, 1><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, npairs);
+            k_knn_wave_mb<KL, 2><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, npairs);
+        } else {
+            k_knn_wave_b<KL><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        }
     }
     k_finish_b<KL><<<dim3(wb, gy), kWaveBlock, 0, s>>>(tab, kp, it, npairs);
 }
@@ -2555,7 +2626,13 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
     else if (use_qwave(kp, N))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
                                                                                           delta, lists, wlist, xref, nref, use_prev, stats);
-    else
+    else if (use_prev && IMLS_COMPACT) {
+        // later iterations: reuse decided per lane, then packets of the compacted re-traversing slots
+        k_knn_wave_m<KL, 1><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists,
+                                                                               wlist, xref, nref, stats);
+        k_knn_wave_m<KL, 2><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists,
+                                                                               wlist, xref, nref, stats);
+    } else
         k_knn_wave<KL><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist,
                                                                           xref, nref, use_prev, stats);
     if (marks) (void)hipEventRecord(marks[1], s);
