@@ -382,14 +382,16 @@ constexpr int kMaxKL = 46;       // list entries per query at most (the lone-fra
 __host__ __device__ inline float4* xref_of(int* lists, int N) {
     return reinterpret_cast<float4*>(reinterpret_cast<char*>(lists) + ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256);
 }
-// then the compacted traversal list of the packet kernel's later ICP iterations (round 6: the slots
-// whose list could not be reused, unsigned cmp[N]) and its count (one word, zeroed by k_finish)
+// then the compacted traversal lists of the packet kernel's later ICP iterations (round 6: per
+// traversal block, the slots whose list could not be reused, unsigned cmp[N]) and their counts (one
+// word per block, cmp_count[N / 64 + 1])
 __host__ __device__ inline unsigned* cmp_of(int* lists, int N) {
     return reinterpret_cast<unsigned*>(reinterpret_cast<char*>(xref_of(lists, N)) + ((size_t)N * 20 + 255) / 256 * 256);
 }
 __host__ __device__ inline unsigned* cmp_count_of(int* lists, int N) { return cmp_of(lists, N) + ((size_t)N + 63) / 64 * 64; }
 inline size_t prevnn_bytes(int N) {
-    return ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256 + ((size_t)N * 20 + 255) / 256 * 256 + ((size_t)N + 63) / 64 * 256 + 512;
+    return ((size_t)(kMaxKL + 1) * N * 4 + 255) / 256 * 256 + ((size_t)N * 20 + 255) / 256 * 256 + ((size_t)N + 63) / 64 * 256 +
+           ((size_t)N / 64 + 2) * 4 + 512;
 }
 constexpr int kStatSkipped = 6;   // nbr_stats slot: lanes whose list was reused without traversal
 int project_blocks(int N);

@@ -496,12 +496,14 @@ __device__ __forceinline__ float need_key_ids(const float (&lk)[KL], float r2, i
 // MODE (round 6, the later ICP iterations of the packet traversal, use_prev):
 //   0  one pass — every lane decides reuse and the packets walk for the lanes that cannot reuse;
 //   1  the reuse decision only (Verlet skip, prefill certificate): a reused list is settled here,
-//      every other slot is appended to the compacted list cmp (a wave's run by one atomic: the run
-//      order varies, the results cannot — the traversal only bounds lists that k_finish certifies);
-//   2  the walk over the compacted slots, 64 to a packet: packets of the queries that really
-//      re-traverse, instead of every packet walking for the few of its lanes that do (mid
-//      iterations: most lanes reuse their lists).  The lane redoes MODE 1's decision (same inputs,
-//      same outcome), its prefill included.
+//      the block's other slots are compacted, in slot (Morton) order, into the block's own region
+//      of cmp, with their count in cmp_count[block];
+//   2  the walk over a block's compacted slots, 64 to a packet: fewer packets walk, each full of
+//      queries that really re-traverse, from the block's 4·64 Morton-consecutive slots (instead of
+//      every packet walking for the few of its lanes that do).  The lane redoes MODE 1's decision
+//      (same inputs, same outcome), its prefill included.
+// (A first version compacted through one atomic counter per frame: packets of runs from anywhere in
+// the frame walked 2-6× longer — profiles/r06_compact_rejected/.)
 template <int KL, int MODE = 0>
 __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
@@ -531,12 +533,12 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     int slot = pslot;
     bool active = lane < qp && slot < N;
     if constexpr (MODE == 2) {
-        // packet = compacted entries [wave·qp, wave·qp + qp); the count is the prep launch's (no
-        // block barrier in this mode: use_prev — a wave past it leaves at once)
-        const int cnt = ld_const((const int*)cmp_count);
-        if ((bx * (kWaveBlock / 64) + wv) * qp >= cnt) return;
-        active = lane < qp && pslot < cnt;
-        slot = active ? (int)cmp[pslot] : 0;
+        // packet = the block's compacted entries [wv·qp, wv·qp + qp); the count is the prep launch's
+        // (no block barrier in this mode: use_prev — a wave past it leaves at once)
+        const int cnt = ld_const((const int*)cmp_count + bx);
+        if (wv * qp >= cnt) return;
+        active = lane < qp && wv * qp + lane < cnt;
+        slot = active ? (int)cmp[(size_t)bx * (kWaveBlock / 64) * qp + wv * qp + lane] : 0;
     }
     float xf[3] = {0.f, 0.f, 0.f};
     // the stored list's bound and reference (slot-indexed) load beside the query's point: one round
@@ -669,12 +671,17 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         if (nbr_stats && lane == 0 && sk) atomicAdd(&nbr_stats[kStatSkipped], (unsigned long long)__popcll(sk));
         const bool need = active && !skip;
         const unsigned long long nm = __ballot(need);
-        if (nm) {
-            unsigned base = 0;
-            if (lane == 0) base = atomicAdd(cmp_count, (unsigned)__popcll(nm));
-            base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
-            if (need) cmp[base + (unsigned)__popcll(nm & ((1ull << lane) - 1ull))] = (unsigned)slot;
+        __shared__ int wneed[kWaveBlock / 64];
+        if (lane == 0) wneed[wv] = __popcll(nm);
+        __syncthreads();              // every wave of the block reaches here (MODE 1 leaves below)
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaveBlock / 64; ++w) {
+            off += w < wv ? wneed[w] : 0;
+            tot += wneed[w];
         }
+        if (need) cmp[(size_t)bx * (kWaveBlock / 64) * qp + off + __popcll(nm & ((1ull << lane) - 1ull))] = (unsigned)slot;
+        if (tid == 0) cmp_count[bx] = (unsigned)tot;
         return;
     }
     // leaf scan shared by the seed pass and the traversal: the lanes in `want` test every point of
@@ -1526,8 +1533,6 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid == IMLS_NUM_REJ + 2 && rej_s[tid]) atomicAdd(&nbr_stats[5], (unsigned long long)rej_s[tid]);
-    // the compacted walk of this iteration has read its count: zero it for the next iteration's prep
-    if (bx == 0 && tid == 0) *cmp_count_of(const_cast<int*>(lists), N) = 0u;
 }
 
 // =============================================================================================
@@ -1904,8 +1909,6 @@ __device__ __forceinline__ void finish4_body(TreeView t, const float4* __restric
     if (nbr_stats && tid >= IMLS_NUM_REJ && tid < IMLS_NUM_REJ + 2 && rej_s[tid])
         atomicAdd(&nbr_stats[tid - IMLS_NUM_REJ], (unsigned long long)rej_s[tid]);
     if (nbr_stats && tid == IMLS_NUM_REJ + 2 && rej_s[tid]) atomicAdd(&nbr_stats[5], (unsigned long long)rej_s[tid]);
-    // the compacted walk of this iteration has read its count: zero it for the next iteration's prep
-    if (bx == 0 && tid == 0) *cmp_count_of(const_cast<int*>(lists), N) = 0u;
 }
 
 // =============================================================================================

@@ -49,10 +49,12 @@ def main():
     for r in rows:
         n = r["Kernel_Name"]
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        if not re.search(r"k_(knn_wave|knn_qwave|finish|project_lane)_b\b", n):   # full or reduced name
+        if not re.search(r"k_(knn_wave|knn_qwave|finish|project_lane)_(b|mb)\b", n):   # full or reduced name
             continue
         proj.append((s, e, n))
-        if re.search(r"k_knn_(wave|qwave)_b\b", n):
+        # one marker per traversal: the one-pass launch, or (round 6, later iterations) the reuse-
+        # decision launch k_knn_wave_mb<KL, 1> — its compacted walk <KL, 2> is projection time only
+        if re.search(r"k_knn_(wave|qwave)_b\b", n) or re.search(r"k_knn_wave_mb<\d+, ?1>", n):
             knn.append((s, e))
     knn.sort()
     proj.sort()
