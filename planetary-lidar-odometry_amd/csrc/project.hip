@@ -53,9 +53,11 @@ constexpr int kFallbackBlocksBatched = 4;   // physical blocks per frame of a la
 // queries per k_finish block = per pass-1 slab (the quad exact stage: 64; the one-lane form: 256)
 constexpr int kFinishPerBlock = IMLS_FINISH_QUAD ? kWaveBlock / 4 : kWaveBlock;
 static_assert(kFinishPerBlock == kPass1Block && kFallbackBlocks == kPass1Fallback, "pass-1 slab layout (solve.hip)");
-// the later ICP iterations' packet traversal in two launches (reuse decision + compacted walk, round 6)
+// the later ICP iterations' packet traversal in two launches (reuse decision + compacted walk, round 6):
+// measured slower (a walk's cost is its node visits, which compaction only concentrates into fewer,
+// longer walks — profiles/r06_compact_rejected/), off; kept for same-box A/B builds
 #ifndef IMLS_COMPACT
-#define IMLS_COMPACT 1
+#define IMLS_COMPACT 0
 #endif
 constexpr int kWideMax = 8;         // packet traversal: children tested per step (2^wide, wide ≤ 3)
 constexpr int kWaveStack = 64;       // its stack: ≤ 7 entries per step × ⌈23/3⌉ steps
@@ -76,6 +78,17 @@ constexpr float kReseed = 0.25f;    // temporal seed unless displacement² > kRe
 constexpr int kSparseLanes = 32;    // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
 constexpr int kWide = 3;            // binary levels descended per traversal step (8 boxes per step)
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
+// Round 6: the traversals search radius (1 + skin)·r, not r.  A query with fewer than K map points
+// within r ("underfull": the far, sparse part of a scan) relies on EVERY point within r; its list from
+// a search of radius r could never be reused (no skin: any move may bring a point inside r), so it
+// re-walked the whole r-ball every ICP iteration — the converged iterations' tail.  Searched to
+// (1 + skin)·r, its list certifies reuse while the query moves < skin·r / 2 (need = r², verlet_skip).
+// Dense queries are unaffected (their bound is the KL-th key ≪ r² after the seed / prefill); k_finish
+// still counts only the points within r.
+#ifndef IMLS_UNDER_SKIN
+#define IMLS_UNDER_SKIN 0.05
+#endif
+constexpr double kSearchR2 = (1.0 + IMLS_UNDER_SKIN) * (1.0 + IMLS_UNDER_SKIN);   // search r² / r²
 constexpr double kCertSlack = 1.0 + 4e-7;
 // list length for K ≤ 20 (the shipped K = 20)
 #ifndef IMLS_B_KL
@@ -440,7 +453,8 @@ __device__ __forceinline__ float need_key(const float (&lk)[KL], float r2, int K
         if (in && d1 == kInfF && lk[j] > 1e-15f) d1 = lk[j];
         if (j == K - 1) dK = lk[j];
     }
-    return cnt_r >= K ? fmaxf(dK, d1) : kInfF;
+    // fewer than K within r: the answer is every point within r (none when no NN-1 exists either)
+    return cnt_r >= K ? fmaxf(dK, d1) : (IMLS_UNDER_SKIN > 0 ? r2f : kInfF);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -487,7 +501,7 @@ __device__ __forceinline__ float need_key_ids(const float (&lk)[KL], float r2, i
         if (in && d1 == kInfF && I::lo(lk[j]) > 1e-15f) d1 = up;
         if (j == K - 1) dK = up;
     }
-    return cnt_r >= K ? fmaxf(dK, d1) : kInfF;
+    return cnt_r >= K ? fmaxf(dK, d1) : (IMLS_UNDER_SKIN > 0 ? r2f : kInfF);   // (need_key)
 }
 
 // Slot-id keys in registers, positions in LDS: ~96 VGPRs and ~29 KB of LDS per 4-wave block — 5
@@ -577,7 +591,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
         insert_key<KL>(lk, IK::make(d, s));
         mypos[s * kWaveBlock] = pos;
     };
-    const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
+    const float r2s = (float)(kp.r2 * kSearchR2) * kBoxSlack + 1e-30f;   // the search bound (radius (1 + skin)·r)
     float bnd = active ? r2s : -1.0f;
     const int P = t.P, B = t.B, M = t.M;
 #ifdef IMLS_DEBUG_WAVE_TRACE
@@ -1068,7 +1082,7 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
     }
     float lkey = kInfF;     // lane k < KL: entry k of the ascending list
     int lpos = -1;
-    const float r2s = (float)kp.r2 * kBoxSlack + 1e-30f;
+    const float r2s = (float)(kp.r2 * kSearchR2) * kBoxSlack + 1e-30f;   // the search bound (radius (1 + skin)·r)
     // h-gate search (IMLS matcher): a query with no map point within h is rejected as too far
     // whatever lies between h and r (imls_icp.cpp:612-625), so while the list holds nothing within
     // h the traversal bound is h², not r² (27× less volume for isolated queries, the launch's tail);
@@ -1345,10 +1359,12 @@ __device__ __forceinline__ void knn_qwave_body(TreeView t, const float4* __restr
         if (lane == 0) wlist[slot] = wskip;
     } else {
         if (lane < KL) lists[(size_t)lane * N + slot] = lpos;
+        const bool lpos_any = __ballot(lane < KL && lpos >= 0) != 0ull;
         float lkr[KL];   // the list gathered to every lane for the reuse key
 #pragma unroll
         for (int k = 0; k < KL; ++k) lkr[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lkey), k));
-        const float nk = need_key<KL>(lkr, (float)kp.r2, kp.K);
+        // an h-mode list left empty was searched only to h: never reused (need ∞)
+        const float nk = lpos_any ? need_key<KL>(lkr, (float)kp.r2, kp.K) : kInfF;
         if (lane == 0) {
             const float wk = worst();
             wlist[slot] = wk;
@@ -1486,8 +1502,9 @@ __device__ __forceinline__ void finish_body(TreeView t, const float4* __restrict
         double need = cnt_r >= K ? dK : r2;
         bool cert = true;
         if (full) {
-            if (i1 < 0) cert = false;
-            else need = fmax(need, d1);
+            // no NN-1 in the list: certified only if no map point within r lies outside it (round 6:
+            // before, never — a reused list of an isolated query went to the exact fallback)
+            need = i1 < 0 ? r2 : fmax(need, d1);
             cert = cert && (need < (double)W / kCertSlack);
         }
         if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_OPT_FORCE_FALLBACK)
@@ -1748,8 +1765,9 @@ __device__ __forceinline__ void finish4_body(TreeView t, const float4* __restric
         double need = cnt_r >= K ? dK : r2;
         bool cert = true;
         if (full) {
-            if (i1 < 0) cert = false;
-            else need = fmax(need, d1);
+            // no NN-1 in the list: certified only if no map point within r lies outside it (round 6:
+            // before, never — a reused list of an isolated query went to the exact fallback)
+            need = i1 < 0 ? r2 : fmax(need, d1);
             cert = cert && (need < (double)W / kCertSlack);
         }
         if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_OPT_FORCE_FALLBACK)
@@ -2098,8 +2116,9 @@ __device__ __forceinline__ void finish_q_core(TreeView t, const float4* __restri
     double need = cnt_r >= K ? dK : r2;
     bool cert = true;
     if (full) {
-        if (l1 < 0) cert = false;
-        else need = fmax(need, d1);
+        // no NN-1 in the list: certified only if no map point within r lies outside it (round 6:
+        // before, never — a reused list of an isolated query went to the exact fallback)
+        need = l1 < 0 ? r2 : fmax(need, d1);
         cert = cert && (need < (double)W / kCertSlack);
     }
     if (kp.force_fb && slot % kp.force_fb == 0) cert = false;   // test hook (IMLS_OPT_FORCE_FALLBACK)
