@@ -75,6 +75,13 @@ constexpr int kSeedTab = 1024;                // seed search: coarse leaf-key ta
 // traversal constants (measured in rounds 1-4; no runtime selectors)
 constexpr int kSeedHalf = 1;        // a seed scans the query's Morton leaf ± 1 neighbour leaf
 constexpr float kReseed = 0.25f;    // temporal seed unless displacement² > kReseed · previous worst key
+#ifndef IMLS_BCAST_SCALAR
+#define IMLS_BCAST_SCALAR 1
+#endif
+#ifndef IMLS_BC_GROUP
+#define IMLS_BC_GROUP 4
+#endif
+__attribute__((unused)) constexpr int kBcGroup = IMLS_BC_GROUP;          // broadcast leaf scan: points per scalar-load group (IMLS_BCAST_SCALAR)
 constexpr int kSparseLanes = 32;    // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
 constexpr int kWide = 3;            // binary levels descended per traversal step (8 boxes per step)
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
@@ -797,10 +804,55 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
 #endif
             }
         } else {
-            // broadcast: each point goes to every lane by v_readlane, every wanting lane tests it
-            // against its list
             if (listed) listed_mask();
             const bool wants = (want >> lane) & 1ull;
+#if IMLS_BCAST_SCALAR
+            // broadcast, round 6: the leaf's points come by scalar loads (wave-uniform addresses, a
+            // group of kBcGroup points per s_load burst, the next group in flight while this one is
+            // measured) and feed the distance VALUs as SGPR operands — no v_readlane per coordinate;
+            // a group none of whose points is under any wanting lane's bound (the common case once
+            // the bounds are tight) costs one compare and one branch instead of one per point.  The
+            // insertion order and the keys are the per-point scan's, bit for bit.
+            const kconst_f4* lp = (const kconst_f4*)t.mpt + base;
+            kf4v g[kBcGroup];
+#pragma unroll
+            for (int u = 0; u < kBcGroup; ++u) g[u] = lp[min(u, cnt - 1)];
+            for (int j0 = 0; j0 < cnt; j0 += kBcGroup) {
+                kf4v nx[kBcGroup];
+                const int jn = j0 + kBcGroup;
+                if (jn + kBcGroup <= cnt) {   // a whole group: one base address, immediate offsets
+                    const kconst_f4* q = lp + jn;
+#pragma unroll
+                    for (int u = 0; u < kBcGroup; ++u) nx[u] = q[u];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < kBcGroup; ++u) nx[u] = lp[min(jn + u, cnt - 1)];
+                }
+                float d[kBcGroup];
+                float dmin = kInfF;
+#pragma unroll
+                for (int u = 0; u < kBcGroup; ++u) {
+                    const float ex = g[u].x - xf[0], ey = g[u].y - xf[1], ez = g[u].z - xf[2];
+                    d[u] = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+                    dmin = fminf(dmin, d[u]);   // past cnt: a copy of the last point (never inserted)
+                }
+                if (__ballot(wants && dmin <= bnd)) {
+#pragma unroll
+                    for (int u = 0; u < kBcGroup; ++u) {
+                        const int j = j0 + u;
+                        const bool ins = j < cnt && wants && d[u] <= bnd && d[u] < thr_() && !((inl >> j) & 1ull);
+                        if (ins) {
+                            ins_(d[u], base + j);
+                            bnd = fmin_nn(r2s, thr_());
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kBcGroup; ++u) g[u] = nx[u];
+            }
+#else
+            // broadcast: each point goes to every lane by v_readlane, every wanting lane tests it
+            // against its list
             for (int j = 0; j < cnt; ++j) {
                 const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.x), j));
                 const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.y), j));
@@ -818,6 +870,7 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
                     bnd = fmin_nn(r2s, thr_());
                 }
             }
+#endif
         }
     };
     // seed (first ICP iteration, or a lane that moved far): the leaf holding the lane's own Morton
@@ -960,7 +1013,9 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             ++n_leaf;
             const int leaf = node - P;
             float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (lane < min(B, M - leaf * B)) mine = t.mpt[leaf * B + lane];
+            // (a broadcast scan reads the leaf by scalar loads: the per-lane copy only for a sparse one)
+            if ((!IMLS_BCAST_SCALAR || __popcll(em) <= kSparseLanes) && lane < min(B, M - leaf * B))
+                mine = t.mpt[leaf * B + lane];
             scan_leaf(leaf, em, use_prev || gmask, mine);
         }
         // pop: the stacked node's box is in LDS — re-check it against the shrunken lane bounds
