@@ -38,6 +38,7 @@ namespace {
 // large ones (the three passes over the rows dominate).  Exact either way (arg-max and counts).
 constexpr int kHypSmallRows = 4096;
 __host__ __device__ constexpr int hyp_block_of(int cap) { return cap <= kHypSmallRows ? 64 : 256; }
+constexpr int kHypUnroll = 8;        // FPS passes: rows per thread whose loads are in flight together
 constexpr int kHypGrid = 8192;        // batched hypothesis grid (blocks stride over the running frames' items)
 constexpr int kDrpmSlab = 42;         // 36 noise-mean terms + 6 variance terms per block
 
@@ -427,13 +428,6 @@ __device__ __forceinline__ void argmax_pair(double& v, int& i, double* sv, int* 
     __syncthreads();
 }
 
-// ‖s_a − s_b‖ as Eigen's (a − b).norm() evaluates it
-__device__ __forceinline__ double pdist(const double* s, int a, int b) {
-    const double dx = s[3 * (size_t)a] - s[3 * (size_t)b], dy = s[3 * (size_t)a + 1] - s[3 * (size_t)b + 1],
-                 dz = s[3 * (size_t)a + 2] - s[3 * (size_t)b + 2];
-    return sqrt((dx * dx + dy * dy) + dz * dz);
-}
-
 // Eigen ColPivHouseholderQR(R×6).solve(b): basic solution (free unknowns zero).  R is tiny (3);
 // every loop is unrolled with constant indices, the pivot swap is predicated.
 template <int RR>
@@ -580,23 +574,53 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
     __shared__ double T[16];
     __shared__ int cnt_s[NT / 64];
     const int f0 = (int)(rand_word_ahead(R.rng, h) >> 1) % n;   // rand() % n (solver.cpp / common.cpp:49)
+    // The two FPS passes: the taken points' coordinates in registers, each thread's rows in groups of
+    // kHypUnroll whose loads are all issued before the first compare (round 6: the loop reloaded
+    // s_f0 and waited on every row's load in turn — one L2 round trip per row, the lone frame's
+    // k_ransac_hyp 31 µs per chunk).  A thread still visits its rows in ascending order and keeps the
+    // first maximum (strict `>`), so the arg-max — larger value, then smaller index — is unchanged.
+    const double a0 = S[3 * (size_t)f0], a1 = S[3 * (size_t)f0 + 1], a2 = S[3 * (size_t)f0 + 2];
+    auto dist = [](double x0, double x1, double x2, const double (&b)[3]) {   // pdist(s, a, b): ‖s_a − s_b‖
+        const double dx = x0 - b[0], dy = x1 - b[1], dz = x2 - b[2];
+        return sqrt((dx * dx + dy * dy) + dz * dz);
+    };
+    auto load_rows = [&](int i0, double (&p)[kHypUnroll][3]) {
+#pragma unroll
+        for (int u = 0; u < kHypUnroll; ++u) {
+            const size_t i3 = 3 * (size_t)min(i0 + u * NT, n - 1);
+            p[u][0] = S[i3]; p[u][1] = S[i3 + 1]; p[u][2] = S[i3 + 2];
+        }
+    };
     // pass 1: farthest from f0 (common.cpp:48-66: strict `>` from −1, taken points skipped)
     double bv = -1.0;
     int bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < n; i += NT) {
-        if (i == f0) continue;
-        const double md = pdist(S, f0, i);
-        if (md > bv) { bv = md; bi = i; }
+    for (int i0 = threadIdx.x; i0 < n; i0 += kHypUnroll * NT) {
+        double p[kHypUnroll][3];
+        load_rows(i0, p);
+#pragma unroll
+        for (int u = 0; u < kHypUnroll; ++u) {
+            const int i = i0 + u * NT;
+            if (i >= n || i == f0) continue;
+            const double md = dist(a0, a1, a2, p[u]);
+            if (md > bv) { bv = md; bi = i; }
+        }
     }
     argmax_pair<NT>(bv, bi, sv, si);
     const int f1 = bi;
     // pass 2: farthest from {f0, f1} by the running minimum distance
+    const double c0 = S[3 * (size_t)f1], c1 = S[3 * (size_t)f1 + 1], c2 = S[3 * (size_t)f1 + 2];
     bv = -1.0;
     bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < n; i += NT) {
-        if (i == f0 || i == f1) continue;
-        const double md = fmin(pdist(S, f0, i), pdist(S, f1, i));
-        if (md > bv) { bv = md; bi = i; }
+    for (int i0 = threadIdx.x; i0 < n; i0 += kHypUnroll * NT) {
+        double p[kHypUnroll][3];
+        load_rows(i0, p);
+#pragma unroll
+        for (int u = 0; u < kHypUnroll; ++u) {
+            const int i = i0 + u * NT;
+            if (i >= n || i == f0 || i == f1) continue;
+            const double md = fmin(dist(a0, a1, a2, p[u]), dist(c0, c1, c2, p[u]));
+            if (md > bv) { bv = md; bi = i; }
+        }
     }
     argmax_pair<NT>(bv, bi, sv, si);
     const int f2 = bi;
@@ -706,6 +730,46 @@ __global__ void k_ransac_trace(const int* __restrict__ count_all, RansacDev R, i
 // ---------------------------------------------------------------------------------------------
 // DRPM (solver.cpp:499-603, degeneracy.h:14-131)
 // ---------------------------------------------------------------------------------------------
+// The wave's totals of the 42 DRPM terms by recursive halving (internal.h wave_sum28's scheme): terms
+// 0..31 in one pass (31 + 1 fp64 exchanges), 32..41 padded to 16 in another (15 + 2) — 49 exchanges
+// where 42 butterfly wave_sums issued 252 (round 6).  Lane 2k returns total k in r0 (k < 32) and
+// total 32 + k in r1 (k < 10).  A fixed association shared by every DRPM launch (alone and batched).
+template <int H, int N>
+__device__ __forceinline__ void halve_n(double (&a)[N], int lane) {
+    const bool up = (lane & (2 * H)) != 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        const double send = up ? a[i] : a[H + i];
+        const double keep = up ? a[H + i] : a[i];
+        a[i] = keep + xor_f64(send, 2 * H);
+    }
+    if constexpr (H > 1) halve_n<H / 2, N>(a, lane);
+}
+__device__ __forceinline__ void wave_sum42(const double (&v)[kDrpmSlab], double& r0, double& r1) {
+    const int lane = threadIdx.x & 63;
+    double a[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) a[k] = v[k];
+    halve_n<16, 32>(a, lane);
+    r0 = a[0] + xor_f64(a[0], 1);
+    double b[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) b[k] = k < kDrpmSlab - 32 ? v[32 + k] : 0.0;
+    halve_n<8, 16>(b, lane);
+    r1 = b[0] + xor_f64(b[0], 1);
+    r1 = r1 + xor_f64(r1, 32);
+}
+// lane 2k of wave wv writes its totals to red[wv][·] (the block's per-wave rows)
+__device__ __forceinline__ void wave_sum42_store(const double (&v)[kDrpmSlab], double* __restrict__ row) {
+    double r0, r1;
+    wave_sum42(v, r0, r1);
+    const int lane = threadIdx.x & 63;
+    if (!(lane & 1)) {
+        row[lane >> 1] = r0;
+        if ((lane >> 1) < kDrpmSlab - 32) row[32 + (lane >> 1)] = r1;
+    }
+}
+
 // reduce the weighted normal equations (pass-1 slabs), eigendecompose H
 __device__ __forceinline__ void drpm_eig_body(const double* __restrict__ partial, int blocks, const SolveState& st,
                                               const DrpmDev& Dv) {
@@ -812,12 +876,8 @@ __device__ __forceinline__ void drpm_noise_body(const Rows& rows, int N, const S
     const int i = blockIdx.x * kBlock + threadIdx.x;
     double acc[kDrpmSlab];
     drpm_noise_terms(rows, i, N, Dv, sp, sn, acc);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < kDrpmSlab; ++k) {
-        const double v = wave_sum(acc[k]);
-        if (lane == 0) red[wv * kDrpmSlab + k] = v;
-    }
+    const int wv = threadIdx.x >> 6;
+    wave_sum42_store(acc, red + wv * kDrpmSlab);
     __syncthreads();
     if (threadIdx.x < kDrpmSlab) {
         double s = 0.0;
@@ -906,12 +966,8 @@ __device__ __forceinline__ void drpm_final_body(int blocks, const SolveState& st
     for (int b = threadIdx.x; b < blocks; b += 256)
 #pragma unroll
         for (int k = 0; k < kDrpmSlab; ++k) loc[k] += Dv.slabs[(size_t)b * kDrpmSlab + k];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < kDrpmSlab; ++k) {
-        const double v = wave_sum(loc[k]);
-        if (lane == 0) red[wv * kDrpmSlab + k] = v;
-    }
+    const int wv = threadIdx.x >> 6;
+    wave_sum42_store(loc, red + wv * kDrpmSlab);
     __syncthreads();
     if (threadIdx.x < kDrpmSlab) {
         double s = 0.0;

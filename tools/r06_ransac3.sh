@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 6: pipelined FPS passes in k_ransac_hyp and halving reductions of the DRPM terms — RANSAC /
+# stream / batched tests, the lone-frame probe and its kernel trace, and the stream RANSAC leg.
+set -u
+O=gpurun_out/${OUT:-r06_ransac3}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 700 python3 -u -m pytest tests/test_gpu_ransac.py tests/test_gpu_stream.py tests/test_gpu_frames.py \
+    tests/test_gpu_batch.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 tools/ransac_probe.py 30 > $O/ransac_probe.out 2> $O/ransac_probe.err; echo "probe rc=$?"; cat $O/ransac_probe.out
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_ransac -o run -- python3 tools/ransac_probe.py 10 > $O/kt_ransac.out 2> $O/kt_ransac.err
+echo "kt rc=$?"
+timeout -k 10 400 python3 bench.py --workload stream --solver RANSAC_DRPM --no-cpu > $O/bench_stream_ransac.json 2> $O/bench_stream_ransac.err
+echo "bench rc=$?"; python3 -c "
+import json;d=json.loads(open('$O/bench_stream_ransac.json').read().strip().splitlines()[-1]);print(d['value'], d.get('single_frame'))"
+echo done
