@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(256) void k_drpm_final(int blocks, SolveState st, D
 // The lone frame's DRPM head in ONE launch (round 6; frames of ≤ kSmallRows rows registered alone,
 // the config C/D deployment shape): the inlier compaction, pass 1 of the weighted normal equations
 // over the inliers and the eigendecomposition — three launches before (k_compact_one, k_rows_pass1,
-// k_drpm_eig).  One 1024-thread block runs them between block barriers; pass 1 runs as "virtual
+// k_drpm_eig) — preceded by the last hypothesis chunk's selection (k_ransac_select, round 6).  One 1024-thread block runs them between block barriers; pass 1 runs as "virtual
 // blocks" — block b of k_rows_pass1's grid is done by the 256-thread group (b mod 4) in round b / 4,
 // with the same thread ↔ row mapping, the same per-wave reductions and the same slab order, and the
 // slab sum by the first 256 threads as k_drpm_eig does it — so every value is the chain's bit for bit
@@ -1014,13 +1014,26 @@ __global__ __launch_bounds__(256) void k_drpm_final(int blocks, SolveState st, D
 // its registers at 2 waves per SIMD; profiles/r06_ransac/).
 // ---------------------------------------------------------------------------------------------
 constexpr int kHeadThreads = 1024;
-__global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(Source isrc, int cap, CompactOut out, CompactPost P,
-                                                                  Rows rows, int b1, SolveState st, DrpmDev Dv) {
+struct SelectArgs {                   // the last hypothesis chunk's selection (k_ransac_select's arguments)
+    const int* count;
+    int chunk, max_iterations;
+    double min_pct;
+};
+__global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(SelectArgs sel, Source isrc, int cap, CompactOut out,
+                                                                  CompactPost P, Rows rows, int b1, SolveState st,
+                                                                  DrpmDev Dv) {
     __shared__ double red_ne[kHeadThreads / 64][kNormEq];
     __shared__ double acc[kNormEq];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, grp = tid >> 8, t = tid & 255;
-    // 1. the inliers of the best Δ with their weights (k_compact_one, kind 2: an empty set fails the solve)
     if (compact_skip(P)) return;
+    // 0. the last chunk's selection (k_ransac_select: skipped once RANSAC finished in an earlier chunk),
+    // by wave 0; its bestT feeds the compaction below
+    if (!*P.R.rdone) {
+        if (tid < 64) ransac_select_body(sel.count, P.R, sel.chunk, sel.max_iterations, sel.min_pct);
+        __threadfence_block();
+        __syncthreads();
+    }
+    // 1. the inliers of the best Δ with their weights (k_compact_one, kind 2: an empty set fails the solve)
     compact_one_body(isrc, cap, out, P);
     __threadfence_block();
     __syncthreads();
@@ -1258,13 +1271,17 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
         k_set_count<<<1, 64, 0, s>>>(F.cnt_all, L.N);
         k_ransac_begin<<<1, 64, 0, s>>>(F.cnt_all, kp.correspond_number, L.update_pose, L.st, L.tr, R);
     }
-    // 2. hypotheses in chunks
-    for (const int cn : ransac_chunks(L.ransac.max_iterations, true)) {
-        if (hyp_block_of(cap) == 64)
-            k_ransac_hyp<64><<<cn, 64, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done);
-        else
-            k_ransac_hyp<256><<<cn, 256, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done);
-        k_ransac_select<<<1, 64, 0, s>>>(F.cnt_all, R, cn, L.ransac.max_iterations, L.ransac.min_inliers_percentage, done);
+    // 2. hypotheses in chunks, 256 threads per hypothesis (a lone frame's chunk has ~1 block per CU, so
+    // the per-thread row chains, not the CU's occupancy, set the time: 64-thread blocks took 26.8 µs
+    // per 272-hypothesis chunk on a 1600-row frame).  A small DRPM frame's last selection runs at the
+    // head of k_drpm_head_small (one launch fewer per ICP iteration).
+    const std::vector<int> chunks = ransac_chunks(L.ransac.max_iterations, true);
+    const bool fold_select = L.ransac.final_method == IMLS_FINAL_DRPM && cap <= kSmallRows;
+    for (size_t ci = 0; ci < chunks.size(); ++ci) {
+        const int cn = chunks[ci];
+        k_ransac_hyp<256><<<cn, 256, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done);
+        if (!(fold_select && ci + 1 == chunks.size()))
+            k_ransac_select<<<1, 64, 0, s>>>(F.cnt_all, R, cn, L.ransac.max_iterations, L.ransac.min_inliers_percentage, done);
     }
 
     // 3. inliers of the best Δ with their Huber-like weights (order kept), Σw; an empty set stops
@@ -1284,8 +1301,9 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
         // then the noise terms and the solve
         const int b1 = solve_blocks(cap);
         const CompactPost P{2, kp.correspond_number, L.update_pose, L.st, L.tr, R};
-        k_drpm_head_small<<<1, kHeadThreads, 0, s>>>(isrc, cap, CompactOut{F.inl, F.cnt_in, F.wsum, cap}, P, rows, b1, L.st,
-                                                     F.Dv);
+        const SelectArgs sel{F.cnt_all, chunks.back(), L.ransac.max_iterations, L.ransac.min_inliers_percentage};
+        k_drpm_head_small<<<1, kHeadThreads, 0, s>>>(sel, isrc, cap, CompactOut{F.inl, F.cnt_in, F.wsum, cap}, P, rows, b1,
+                                                     L.st, F.Dv);
         k_drpm_noise<<<b1, kBlock, 0, s>>>(rows, cap, L.st, F.Dv, L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals);
         k_drpm_final<<<1, 256, 0, s>>>(b1, L.st, F.Dv, L.tr, fk, L.ransac.drpm_threshold, F.cnt_all, F.cnt_in, L.update_pose,
                                        R, L.tr);
