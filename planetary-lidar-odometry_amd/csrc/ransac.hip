@@ -41,6 +41,14 @@ __host__ __device__ constexpr int hyp_block_of(int cap) { return cap <= kHypSmal
 constexpr int kHypUnroll = 8;        // FPS passes: rows per thread whose loads are in flight together
 constexpr int kHypGrid = 8192;        // batched hypothesis grid (blocks stride over the running frames' items)
 constexpr int kDrpmSlab = 42;         // 36 noise-mean terms + 6 variance terms per block
+#ifdef IMLS_DEBUG_WAVE_TRACE
+// phase clocks (100 MHz ticks) of block 0's hypothesis [0..5] and of k_drpm_head_small [8..13];
+// [6], [14]: call counts (tools/ransac_probe.py with the debug build)
+__device__ unsigned long long g_dbg_ransac[16];
+#define RSTAMP(k) do { if (dbg_on) { g_dbg_ransac[k] += wall_clock64() - dbg_t; dbg_t = wall_clock64(); } } while (0)
+#else
+#define RSTAMP(k) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // glibc random() TYPE_3 (what rand() returns): state = a ring of 31 words + front / rear indices
@@ -573,6 +581,11 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
     __shared__ int si[NT / 64];
     __shared__ double T[16];
     __shared__ int cnt_s[NT / 64];
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    const bool dbg_on = blockIdx.x == 0 && threadIdx.x == 0 && h == 0;
+    long long dbg_t = wall_clock64();
+    if (dbg_on) g_dbg_ransac[6] += 1;
+#endif
     const int f0 = (int)(rand_word_ahead(R.rng, h) >> 1) % n;   // rand() % n (solver.cpp / common.cpp:49)
     // The two FPS passes: the taken points' coordinates in registers, each thread's rows in groups of
     // kHypUnroll whose loads are all issued before the first compare (round 6: the loop reloaded
@@ -606,6 +619,7 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
         }
     }
     argmax_pair<NT>(bv, bi, sv, si);
+    RSTAMP(0);
     const int f1 = bi;
     // pass 2: farthest from {f0, f1} by the running minimum distance
     const double c0 = S[3 * (size_t)f1], c1 = S[3 * (size_t)f1 + 1], c2 = S[3 * (size_t)f1 + 2];
@@ -623,6 +637,7 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
         }
     }
     argmax_pair<NT>(bv, bi, sv, si);
+    RSTAMP(1);
     const int f2 = bi;
     if (threadIdx.x == 0) {
         const int id[3] = {f0, f1, f2};
@@ -643,7 +658,9 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
             b[r] = bb;
         }
         colpiv_qr_small<3>(A, b, x);
+        RSTAMP(2);
         delta_from_x(x, D);
+        RSTAMP(3);
 #pragma unroll
         for (int k = 0; k < 16; ++k) T[k] = D[k];
     }
@@ -668,6 +685,7 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
         R.counts[h] = tot;
     }
     if (threadIdx.x < 16) R.T[(size_t)h * 16 + threadIdx.x] = T[threadIdx.x];
+    RSTAMP(4);
 }
 // one frame: hypotheses blockIdx.x, blockIdx.x + gridDim.x, … of the chunk
 template <int NT>
@@ -785,7 +803,7 @@ __device__ __forceinline__ void drpm_eig_body(const double* __restrict__ partial
     block_sum28<256>(loc, red, acc);
     if (threadIdx.x >= 64) return;
     // H (row-major, from the upper-triangle terms) and g; the eigendecomposition by wave 0, lane k
-    // holding row k (sym_eig6_wave: the oracle's Jacobi, operation for operation)
+    // holding row k (sym_eig6_wave_rr: the oracle's Jacobi in round-robin order)
     const int lane = threadIdx.x, k = lane < 6 ? lane : 0;
     double row[6];
 #pragma unroll
@@ -798,7 +816,7 @@ __device__ __forceinline__ void drpm_eig_body(const double* __restrict__ partial
         for (int c = 0; c < 6; ++c) Dv.H[lane * 6 + c] = row[c];
         Dv.g[lane] = acc[21 + lane];
     }
-    sym_eig6_wave(row, Dv.ev, Dv.U);
+    sym_eig6_wave_rr(row, Dv.ev, Dv.U);
 }
 
 // the 42 noise terms of row i (zero when i ≥ N or the row is absent), degeneracy.h:14-72
@@ -1026,6 +1044,11 @@ __global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(SelectArgs sel
     __shared__ double acc[kNormEq];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, grp = tid >> 8, t = tid & 255;
     if (compact_skip(P)) return;
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    const bool dbg_on = tid == 0;
+    long long dbg_t = wall_clock64();
+    if (dbg_on) g_dbg_ransac[14] += 1;
+#endif
     // 0. the last chunk's selection (k_ransac_select: skipped once RANSAC finished in an earlier chunk),
     // by wave 0; its bestT feeds the compaction below
     if (!*P.R.rdone) {
@@ -1033,10 +1056,12 @@ __global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(SelectArgs sel
         __threadfence_block();
         __syncthreads();
     }
+    RSTAMP(8);
     // 1. the inliers of the best Δ with their weights (k_compact_one, kind 2: an empty set fails the solve)
     compact_one_body(isrc, cap, out, P);
     __threadfence_block();
     __syncthreads();
+    RSTAMP(9);
     // 2. pass 1 over the inlier rows (k_rows_pass1<kBlock>, which runs whether or not the frame is done:
     // slab b = rows [256b, 256b + 256))
     for (int base = 0; base < b1; base += kHeadThreads / kBlock) {
@@ -1071,6 +1096,7 @@ __global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(SelectArgs sel
     }
     __threadfence_block();
     __syncthreads();
+    RSTAMP(10);
     // 3. H, g and the eigendecomposition (k_drpm_eig: a finished frame stops here; 256 threads reduce
     // the slabs, wave 0 solves)
     if (*st.done) return;
@@ -1107,8 +1133,19 @@ __global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(SelectArgs sel
         for (int c = 0; c < 6; ++c) Dv.H[lane * 6 + c] = row[c];
         Dv.g[lane] = acc[21 + lane];
     }
-    sym_eig6_wave(row, Dv.ev, Dv.U);
+    RSTAMP(11);
+    sym_eig6_wave_rr(row, Dv.ev, Dv.U);
+    RSTAMP(12);
 }
+#ifdef IMLS_DEBUG_WAVE_TRACE
+}  // namespace
+}  // namespace imlsgpu
+extern "C" int imls_debug_ransac(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(imlsgpu::g_dbg_ransac), 128) == hipSuccess ? 0 : -1;
+}
+namespace imlsgpu {
+namespace {
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Batched RANSAC / DRPM kernels (launch_ransac_batch): frame = tab[blockIdx.y], the same bodies as

@@ -3,6 +3,7 @@ one frame at a time with RANSAC → DRPM (config.json's solver), on the config C
 (≤2000-query flat cloud vs the previous 118k-point filtered scan, 20 ICP iterations).  Prints the
 median / p90 wall time per call; run under rocprofv3 --kernel-trace --stats for the per-kernel split
 (tools/iter_profile_frame.py groups a trace per frame)."""
+import ctypes as C
 import pathlib
 import sys
 import time
@@ -29,4 +30,13 @@ with imls_icp.LaserOdometry(p, device=0) as lo:
                 iters.append(r["iters"])
     print(f"LaserOdometry.process RANSAC->DRPM: median {np.median(lat):.3f} ms  p90 {np.percentile(lat, 90):.3f} ms "
           f"(pipelined {lo.pipelined}, {len(fr[0][1])} queries vs {len(fr[0][0])}-pt scan, iterations {np.mean(iters):.1f})")
+lib = runner.ctxs[0].lib if hasattr(runner, "ctxs") else None
 runner.close()
+if lib is not None and hasattr(lib, "imls_debug_ransac"):   # the DEBUG_WAVE_TRACE build (IMLS_LIB_PATH)
+    buf = np.zeros(16, np.uint64)
+    lib.imls_debug_ransac(C.c_void_p(buf.ctypes.data))
+    nh, nd = max(int(buf[6]), 1), max(int(buf[14]), 1)
+    print("  k_ransac_hyp block 0, ticks (100 MHz) per call:",
+          {k: round(float(buf[i]) / nh, 1) for i, k in enumerate(["rng+pass1", "pass2", "qr", "delta", "count"])})
+    print("  k_drpm_head_small, ticks per call:",
+          {k: round(float(buf[8 + i]) / nd, 1) for i, k in enumerate(["select", "compact", "pass1", "slab sum", "eig"])})
