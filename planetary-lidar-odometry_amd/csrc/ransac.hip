@@ -803,7 +803,7 @@ __device__ __forceinline__ void drpm_eig_body(const double* __restrict__ partial
     block_sum28<256>(loc, red, acc);
     if (threadIdx.x >= 64) return;
     // H (row-major, from the upper-triangle terms) and g; the eigendecomposition by wave 0, lane k
-    // holding row k (sym_eig6_wave_rr: the oracle's Jacobi in round-robin order)
+    // holding row k (sym_eig6_wave: the oracle's Jacobi, operation for operation)
     const int lane = threadIdx.x, k = lane < 6 ? lane : 0;
     double row[6];
 #pragma unroll
@@ -816,7 +816,7 @@ __device__ __forceinline__ void drpm_eig_body(const double* __restrict__ partial
         for (int c = 0; c < 6; ++c) Dv.H[lane * 6 + c] = row[c];
         Dv.g[lane] = acc[21 + lane];
     }
-    sym_eig6_wave_rr(row, Dv.ev, Dv.U);
+    sym_eig6_wave(row, Dv.ev, Dv.U);
 }
 
 // the 42 noise terms of row i (zero when i ≥ N or the row is absent), degeneracy.h:14-72
@@ -1134,8 +1134,13 @@ __global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(SelectArgs sel
         Dv.g[lane] = acc[21 + lane];
     }
     RSTAMP(11);
-    sym_eig6_wave_rr(row, Dv.ev, Dv.U);
+    const int sweeps = sym_eig6_wave(row, Dv.ev, Dv.U);
     RSTAMP(12);
+#ifdef IMLS_DEBUG_WAVE_TRACE
+    if (dbg_on) g_dbg_ransac[13] += (unsigned long long)sweeps;
+#else
+    (void)sweeps;
+#endif
 }
 #ifdef IMLS_DEBUG_WAVE_TRACE
 }  // namespace

@@ -521,24 +521,18 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 
 constexpr double kDrpmEigRelTol = 1e-30;   // the oracle's DRPM Jacobi stop (imls_oracle.cpp sym_eig)
 
-// The DRPM 6×6 eigendecomposition by one wave, lane k < 6 holding row k of the matrix and of the
-// eigenvector accumulator (a_row: row k of the symmetric input; every lane calls; ev / U as sym_eig,
-// written by lanes < 6).  Round 5 ran the oracle's cyclic sweep operation for operation (15 dependent
-// angle chains of divisions and square roots per sweep, 19.2 µs per call on a lone frame); round 6
-// runs each sweep's 15 rotations in 5 rounds of 3 disjoint pairs (round-robin order): a round's three
-// angles come from three disjoint 2×2 blocks of the same matrix and the rotations are applied together
-// — all columns (lane-local), then all rows (each pair's two lanes exchange their rows, one shuffle per
-// element).  Same stop rule as the oracle's sym_eig; the sweep order and the rounding of the entries
-// two rotations of a round share differ, so the eigenpairs agree with the oracle to rounding, not bit
-// for bit (DRPM parity is a tolerance, tests/test_gpu_ransac.py).
-__device__ inline void sym_eig6_wave_rr(const double (&a_row)[6], double* __restrict__ ev, double* __restrict__ U) {
+// sym_eig<6> by one wave, lane k < 6 holding row k of the matrix and of the eigenvector accumulator:
+// the same sweeps, rotations and per-element expressions in the same order (a rotation's column
+// update is lane-local, its row update reads rows p and q after it, as the sequential loops do), so
+// the result is the one-thread routine's (with the relative stop below); ~6× shorter dependency chains.  a_row: row k of the
+// symmetric input (lanes < 6).  Every lane of the wave calls; ev / U (as sym_eig) written by lanes < 6.
+__device__ inline int sym_eig6_wave(const double (&a_row)[6], double* __restrict__ ev, double* __restrict__ U) {
     constexpr int N = 6;
-    constexpr int RP[5][3] = {{0, 1, 2}, {0, 3, 1}, {0, 2, 1}, {0, 1, 4}, {0, 2, 3}};
-    constexpr int RQ[5][3] = {{5, 4, 3}, {4, 5, 2}, {3, 4, 5}, {2, 3, 5}, {1, 5, 4}};
     const int lane = threadIdx.x & 63;
     double a[N], v[N];
 #pragma unroll
     for (int c = 0; c < N; ++c) { a[c] = a_row[c]; v[c] = lane == c ? 1.0 : 0.0; }
+    // stop at off-diagonal mass < max(1e-300, 1e-30·‖H‖_F²) (the oracle's sym_eig with DRPM's rel_tol)
     double fro = 0;
 #pragma unroll
     for (int r = 0; r < N; ++r)
@@ -548,6 +542,7 @@ __device__ inline void sym_eig6_wave_rr(const double (&a_row)[6], double* __rest
             fro += x * x;
         }
     const double stop = fmax(1e-300, kDrpmEigRelTol * fro);
+    int sweeps = 0;
     for (int sweep = 0; sweep < 100; ++sweep) {
         double off = 0;
 #pragma unroll
@@ -558,56 +553,38 @@ __device__ inline void sym_eig6_wave_rr(const double (&a_row)[6], double* __rest
                 off += apq * apq;
             }
         if (off < stop) break;
+        ++sweeps;
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            int partner = lane;
-            bool low = false;
+        for (int p = 0; p < N; ++p)
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                if (lane == RP[r][i]) { partner = RQ[r][i]; low = true; }
-                if (lane == RQ[r][i]) partner = RP[r][i];
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = readlane_f64(a[q], p);
+                if (apq != 0) {
+                    const double app = readlane_f64(a[p], p), aqq = readlane_f64(a[q], q);
+                    const double theta = (aqq - app) / (2 * apq);
+                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
+                    const double c = 1 / sqrt(t * t + 1), s = t * c;
+                    {
+                        const double akp = a[p], akq = a[q];
+                        a[p] = c * akp - s * akq;
+                        a[q] = s * akp + c * akq;
+                    }
+                    double rp[N], rq[N];
+#pragma unroll
+                    for (int k = 0; k < N; ++k) { rp[k] = readlane_f64(a[k], p); rq[k] = readlane_f64(a[k], q); }
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        const double apk = rp[k], aqk = rq[k];
+                        if (lane == p) a[k] = c * apk - s * aqk;
+                        if (lane == q) a[k] = s * apk + c * aqk;
+                    }
+                    {
+                        const double vkp = v[p], vkq = v[q];
+                        v[p] = c * vkp - s * vkq;
+                        v[q] = s * vkp + c * vkq;
+                    }
+                }
             }
-            double dself = 0.0, apq = 0.0;
-#pragma unroll
-            for (int c = 0; c < N; ++c) {
-                dself = lane == c ? a[c] : dself;
-                apq = partner == c ? a[c] : apq;
-            }
-            const double dpart = __shfl(dself, partner, 64);
-            double c = 1.0, s = 0.0;
-            if (low && apq != 0) {        // the pair's lower lane: a_pp = own diagonal, a_qq = the partner's
-                const double theta = (dpart - dself) / (2 * apq);
-                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
-                c = 1 / sqrt(t * t + 1);
-                s = t * c;
-            }
-            double cc[3], ss[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) { cc[i] = readlane_f64(c, RP[r][i]); ss[i] = readlane_f64(s, RP[r][i]); }
-            // columns p, q of every row (lane-local), and of the eigenvector accumulator
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const int p = RP[r][i], q = RQ[r][i];
-                const double akp = a[p], akq = a[q];
-                a[p] = cc[i] * akp - ss[i] * akq;
-                a[q] = ss[i] * akp + cc[i] * akq;
-                const double vkp = v[p], vkq = v[q];
-                v[p] = cc[i] * vkp - ss[i] * vkq;
-                v[q] = ss[i] * vkp + cc[i] * vkq;
-            }
-            // rows p, q: the pair's lanes exchange their (column-updated) rows
-            double cp = 1.0, sp = 0.0;
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-                if (lane == RP[r][i] || lane == RQ[r][i]) { cp = cc[i]; sp = ss[i]; }
-            double other[N];
-#pragma unroll
-            for (int k = 0; k < N; ++k) other[k] = __shfl(a[k], partner, 64);
-            if (lane < N) {
-#pragma unroll
-                for (int k = 0; k < N; ++k) a[k] = low ? cp * a[k] - sp * other[k] : sp * other[k] + cp * a[k];
-            }
-        }
     }
     int ord[N];
     double dg[N];
@@ -635,6 +612,7 @@ __device__ inline void sym_eig6_wave_rr(const double (&a_row)[6], double* __rest
             U[c * N + lane] = val;
         }
     }
+    return sweeps;   // sweeps run (the debug build records them)
 }
 
 }  // namespace

@@ -39,4 +39,5 @@ if lib is not None and hasattr(lib, "imls_debug_ransac"):   # the DEBUG_WAVE_TRA
     print("  k_ransac_hyp block 0, ticks (100 MHz) per call:",
           {k: round(float(buf[i]) / nh, 1) for i, k in enumerate(["rng+pass1", "pass2", "qr", "delta", "count"])})
     print("  k_drpm_head_small, ticks per call:",
-          {k: round(float(buf[8 + i]) / nd, 1) for i, k in enumerate(["select", "compact", "pass1", "slab sum", "eig"])})
+          {k: round(float(buf[8 + i]) / nd, 1) for i, k in enumerate(["select", "compact", "pass1", "slab sum", "eig"])},
+          "Jacobi sweeps per call", round(float(buf[13]) / nd, 2))
