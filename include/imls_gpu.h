@@ -168,7 +168,11 @@ void imls_destroy(imls_ctx* ctx);
 /* Replaces IMLSICPMatcher::setParameters (imls_icp.h:62-66). */
 int imls_set_params(imls_ctx* ctx, const imls_params* p);
 const char* imls_last_error(const imls_ctx* ctx);
-/* Run every launch of the context on `stream` (a hipStream_t); NULL restores the context's own. */
+/* Run every launch of the context on `stream` (a hipStream_t); NULL restores the context's own.
+ * A device buffer the context outgrows is not freed at once: it is retired behind an event recorded
+ * on every stream the context has used, and freed (or reused) once those events have passed — no
+ * device-wide synchronisation, so other contexts and other GPU users of the process keep running.
+ * The stream must stay valid until the context is destroyed or set to another stream. */
 int imls_set_stream(imls_ctx* ctx, void* hip_stream);
 int imls_synchronize(imls_ctx* ctx);
 
