@@ -689,13 +689,31 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
 }
 // one frame: hypotheses blockIdx.x, blockIdx.x + gridDim.x, … of the chunk
 template <int NT>
+// base > 0 (a lone frame's second chunk, its hypotheses base … base + chunk − 1 of the same draw
+// sequence): nothing is selected or committed between the chunks — every block first looks for a
+// hypothesis of the first chunk above the inlier minimum (the first chunk's selection would have
+// stopped RANSAC there) and leaves if there is one; one selection over both chunks follows (at the head
+// of k_drpm_head_small), which is the two sequential selections' result: the first exceeding
+// hypothesis ends the scan, the first maximum before it wins, exactly `used` draws are committed.
+template <int NT>
 __global__ __launch_bounds__(NT) void k_ransac_hyp(const double* __restrict__ rows, const int* __restrict__ count,
                                                    int cap, RansacDev R, double dist_thr, int chunk,
-                                                   const int* __restrict__ done) {
+                                                   const int* __restrict__ done, int base, double min_pct) {
     if (*done || *R.rdone) return;
     const int n = *count;
+    if (base > 0) {
+        __shared__ int hit;
+        const int min_inliers = (int)(min_pct * (double)n);   // as ransac_select_body
+        if (threadIdx.x == 0) hit = 0;
+        __syncthreads();
+        for (int h = threadIdx.x; h < base; h += NT)
+            if (R.counts[h] > min_inliers) hit = 1;
+        __syncthreads();
+        if (hit) return;
+    }
     const size_t c3 = 3 * (size_t)cap;
-    for (int h = blockIdx.x; h < chunk; h += gridDim.x) ransac_hyp_one<NT>(rows, rows + c3, rows + 2 * c3, n, R, dist_thr, h);
+    for (int h = blockIdx.x; h < chunk; h += gridDim.x)
+        ransac_hyp_one<NT>(rows, rows + c3, rows + 2 * c3, n, R, dist_thr, base + h);
 }
 
 // Sequential semantics of the hypothesis loop (solver.cpp:244-326) over one chunk, by one wave: the
@@ -1042,6 +1060,8 @@ __global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(SelectArgs sel
                                                                   DrpmDev Dv) {
     __shared__ double red_ne[kHeadThreads / 64][kNormEq];
     __shared__ double acc[kNormEq];
+    // pass 1's slabs stay in LDS (round 6: through st.partial1 the slab sum waited on a global round trip)
+    __shared__ double slab[kSmallRows / kBlock][kNormEq];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, grp = tid >> 8, t = tid & 255;
     if (compact_skip(P)) return;
 #ifdef IMLS_DEBUG_WAVE_TRACE
@@ -1090,12 +1110,10 @@ __global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(SelectArgs sel
         if (t < kNormEq && b < b1) {
             double sacc = 0.0;
             for (int w = 0; w < kBlock / 64; ++w) sacc += red_ne[grp * (kBlock / 64) + w][t];
-            st.partial1[(size_t)b * kNormEq + t] = sacc;
+            slab[b][t] = sacc;
         }
         __syncthreads();
     }
-    __threadfence_block();
-    __syncthreads();
     RSTAMP(10);
     // 3. H, g and the eigendecomposition (k_drpm_eig: a finished frame stops here; 256 threads reduce
     // the slabs, wave 0 solves)
@@ -1106,7 +1124,7 @@ __global__ __launch_bounds__(kHeadThreads) void k_drpm_head_small(SelectArgs sel
     if (tid < 256)
         for (int b = tid; b < b1; b += 256)
 #pragma unroll
-            for (int k = 0; k < kNormEq; ++k) loc[k] += st.partial1[(size_t)b * kNormEq + k];
+            for (int k = 0; k < kNormEq; ++k) loc[k] += slab[b][k];
     double a32[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) a32[k] = k < kNormEq ? loc[k] : 0.0;
@@ -1317,13 +1335,26 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
     // the per-thread row chains, not the CU's occupancy, set the time: 64-thread blocks took 26.8 µs
     // per 272-hypothesis chunk on a 1600-row frame).  A small DRPM frame's last selection runs at the
     // head of k_drpm_head_small (one launch fewer per ICP iteration).
+    // Two chunks whose draws fit the jump table (the shipped 5000 hypotheses: 272 + 4728) run without a
+    // selection between them (k_ransac_hyp, base > 0): one selection over both, at the head.
     const std::vector<int> chunks = ransac_chunks(L.ransac.max_iterations, true);
     const bool fold_select = L.ransac.final_method == IMLS_FINAL_DRPM && cap <= kSmallRows;
-    for (size_t ci = 0; ci < chunks.size(); ++ci) {
-        const int cn = chunks[ci];
-        k_ransac_hyp<256><<<cn, 256, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done);
-        if (!(fold_select && ci + 1 == chunks.size()))
-            k_ransac_select<<<1, 64, 0, s>>>(F.cnt_all, R, cn, L.ransac.max_iterations, L.ransac.min_inliers_percentage, done);
+    const bool one_select = fold_select && chunks.size() == 2 && chunks[0] + chunks[1] <= kHypMax;
+    int sel_chunk = chunks.back();
+    if (one_select) {
+        k_ransac_hyp<256><<<chunks[0], 256, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, chunks[0],
+                                                    done, 0, 0.0);
+        k_ransac_hyp<256><<<chunks[1], 256, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, chunks[1],
+                                                    done, chunks[0], L.ransac.min_inliers_percentage);
+        sel_chunk = chunks[0] + chunks[1];
+    } else {
+        for (size_t ci = 0; ci < chunks.size(); ++ci) {
+            const int cn = chunks[ci];
+            k_ransac_hyp<256><<<cn, 256, 0, s>>>(F.all, F.cnt_all, cap, R, L.ransac.distance_threshold, cn, done, 0, 0.0);
+            if (!(fold_select && ci + 1 == chunks.size()))
+                k_ransac_select<<<1, 64, 0, s>>>(F.cnt_all, R, cn, L.ransac.max_iterations, L.ransac.min_inliers_percentage,
+                                                 done);
+        }
     }
 
     // 3. inliers of the best Δ with their Huber-like weights (order kept), Σw; an empty set stops
@@ -1343,7 +1374,7 @@ void launch_solve(hipStream_t s, const SolveLaunch& L) {
         // then the noise terms and the solve
         const int b1 = solve_blocks(cap);
         const CompactPost P{2, kp.correspond_number, L.update_pose, L.st, L.tr, R};
-        const SelectArgs sel{F.cnt_all, chunks.back(), L.ransac.max_iterations, L.ransac.min_inliers_percentage};
+        const SelectArgs sel{F.cnt_all, sel_chunk, L.ransac.max_iterations, L.ransac.min_inliers_percentage};
         k_drpm_head_small<<<1, kHeadThreads, 0, s>>>(sel, isrc, cap, CompactOut{F.inl, F.cnt_in, F.wsum, cap}, P, rows, b1,
                                                      L.st, F.Dv);
         k_drpm_noise<<<b1, kBlock, 0, s>>>(rows, cap, L.st, F.Dv, L.ransac.drpm_stdev_points, L.ransac.drpm_stdev_normals);
