@@ -687,8 +687,7 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
     if (threadIdx.x < 16) R.T[(size_t)h * 16 + threadIdx.x] = T[threadIdx.x];
     RSTAMP(4);
 }
-// one frame: hypotheses blockIdx.x, blockIdx.x + gridDim.x, … of the chunk
-template <int NT>
+// one frame: hypotheses blockIdx.x, blockIdx.x + gridDim.x, … of the chunk.
 // base > 0 (a lone frame's second chunk, its hypotheses base … base + chunk − 1 of the same draw
 // sequence): nothing is selected or committed between the chunks — every block first looks for a
 // hypothesis of the first chunk above the inlier minimum (the first chunk's selection would have
