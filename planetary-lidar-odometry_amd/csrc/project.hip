@@ -75,6 +75,10 @@ constexpr int kSeedTab = 1024;                // seed search: coarse leaf-key ta
 // traversal constants (measured in rounds 1-4; no runtime selectors)
 constexpr int kSeedHalf = 1;        // a seed scans the query's Morton leaf ± 1 neighbour leaf
 constexpr float kReseed = 0.25f;    // temporal seed unless displacement² > kReseed · previous worst key
+// the packet traversal prefetches the stack top's leaf points during a leaf scan (round 6 A/B)
+#ifndef IMLS_LEAF_PREFETCH
+#define IMLS_LEAF_PREFETCH 1
+#endif
 #ifndef IMLS_BCAST_SCALAR
 #define IMLS_BCAST_SCALAR 1
 #endif
@@ -948,6 +952,10 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
 #endif
     if (skip) bnd = -1.0f;           // a certified lane takes no part in the traversal
     int node = 1, sp = 0;
+#if IMLS_LEAF_PREFETCH
+    int pf_leaf = -1;                 // the leaf whose points `pf` holds (wave-uniform)
+    float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
     unsigned long long em = __ballot(active && !skip);   // lanes whose bound admits the current node's box
     const unsigned long long skipped = __ballot(skip);
     if (nbr_stats && lane == 0 && skipped) atomicAdd(&nbr_stats[kStatSkipped], (unsigned long long)__popcll(skipped));
@@ -1013,9 +1021,26 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
             ++n_leaf;
             const int leaf = node - P;
             float4 mine = make_float4(0.f, 0.f, 0.f, 0.f);
+#if IMLS_LEAF_PREFETCH
+            // the leaf's points were prefetched when it was the stack's top during the previous leaf
+            // scan; else loaded now.  Then the stack's top, when it is a leaf (most often the next node
+            // visited: a sibling at the bottom level), has its points in flight during this scan
+            if (leaf == pf_leaf) mine = pf;
+            else if (lane < min(B, M - leaf * B)) mine = t.mpt[leaf * B + lane];
+            pf_leaf = -1;
+            if (sp > 0) {
+                const int nn = __builtin_amdgcn_readfirstlane(snode[wv][sp - 1]);
+                if (nn >= P) {
+                    pf_leaf = nn - P;
+                    pf = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (lane < min(B, M - pf_leaf * B)) pf = t.mpt[pf_leaf * B + lane];
+                }
+            }
+#else
             // (a broadcast scan reads the leaf by scalar loads: the per-lane copy only for a sparse one)
             if ((!IMLS_BCAST_SCALAR || __popcll(em) <= kSparseLanes) && lane < min(B, M - leaf * B))
                 mine = t.mpt[leaf * B + lane];
+#endif
             scan_leaf(leaf, em, use_prev || gmask, mine);
         }
         // pop: the stacked node's box is in LDS — re-check it against the shrunken lane bounds
