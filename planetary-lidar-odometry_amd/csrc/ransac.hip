@@ -38,6 +38,9 @@ namespace {
 // large ones (the three passes over the rows dominate).  Exact either way (arg-max and counts).
 constexpr int kHypSmallRows = 4096;
 __host__ __device__ constexpr int hyp_block_of(int cap) { return cap <= kHypSmallRows ? 64 : 256; }
+#ifndef IMLS_QR_WAVE
+#define IMLS_QR_WAVE 1                // a hypothesis' 3×6 QR by one wave, a column per lane (round 6)
+#endif
 constexpr int kHypUnroll = 8;        // FPS passes: rows per thread whose loads are in flight together
 constexpr int kHypGrid = 8192;        // batched hypothesis grid (blocks stride over the running frames' items)
 constexpr int kDrpmSlab = 42;         // 36 noise-mean terms + 6 variance terms per block
@@ -571,6 +574,166 @@ __device__ void colpiv_qr_small(double A[RR][6], double b[RR], double x[6]) {
     }
 }
 
+// colpiv_qr_small<3> by one wave (round 6), lane c < 6 holding column c of A (a[r] = A[r][c]) with its
+// norms and original index: the pivot search reads the six norms, a swap exchanges two lanes' columns,
+// the Householder vector of column k is formed by every lane from lane k's column (the same scalar
+// expressions, so the same bits everywhere), and the update and the norm downdate of the columns
+// right of k run on their own lanes — the one-lane routine's operations, each on the lane that owns
+// the column, so x is its result bit for bit.  The back-substitution (3×3) runs on every lane from the
+// gathered factor.  A hypothesis block's QR 4.8 µs on one lane (tools/ransac_probe.py phase clocks).
+__device__ void colpiv_qr3_wave(double a[3], double b[3], double x[6]) {
+    constexpr int RR = 3, C = 6, S = 3;
+    const int lane = threadIdx.x & 63;
+    const double eps = DBL_EPSILON;
+    double nu, nd;
+    int perm = lane;
+    {
+        double sq = 0;
+#pragma unroll
+        for (int r = 0; r < RR; ++r) sq += a[r] * a[r];
+        nu = nd = sqrt(sq);
+    }
+    double maxnorm = 0;
+#pragma unroll
+    for (int k = 0; k < C; ++k) maxnorm = fmax(maxnorm, readlane_f64(nu, k));
+    const double thr_helper = (maxnorm * eps) * (maxnorm * eps) / (double)RR;
+    const double ndt = sqrt(eps);
+    int nonzero = S;
+    double maxpivot = 0;
+    double hc[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        int big = k;
+        double bv = readlane_f64(nu, k);
+#pragma unroll
+        for (int j = k + 1; j < C; ++j) {
+            const double nj = readlane_f64(nu, j);
+            if (nj > bv) { bv = nj; big = j; }
+        }
+        if (nonzero == S && bv * bv < thr_helper * (double)(RR - k)) nonzero = k;
+        if (big != k) {                       // wave-uniform: exchange the columns of lanes k and big
+            double ak[RR], ab[RR];
+#pragma unroll
+            for (int r = 0; r < RR; ++r) { ak[r] = readlane_f64(a[r], k); ab[r] = readlane_f64(a[r], big); }
+            const double nuk = readlane_f64(nu, k), nub = readlane_f64(nu, big);
+            const double ndk = readlane_f64(nd, k), ndb = readlane_f64(nd, big);
+            const int pk = __builtin_amdgcn_readlane(perm, k), pb = __builtin_amdgcn_readlane(perm, big);
+            if (lane == k) {
+#pragma unroll
+                for (int r = 0; r < RR; ++r) a[r] = ab[r];
+                nu = nub; nd = ndb; perm = pb;
+            } else if (lane == big) {
+#pragma unroll
+                for (int r = 0; r < RR; ++r) a[r] = ak[r];
+                nu = nuk; nd = ndk; perm = pk;
+            }
+        }
+        // makeHouseholderInPlace on column k, rows k..RR−1 (every lane, from lane k's column)
+        double col[RR];
+#pragma unroll
+        for (int r = 0; r < RR; ++r) col[r] = readlane_f64(a[r], k);
+        const double c0 = col[k];
+        double tail = 0;
+#pragma unroll
+        for (int r = k + 1; r < RR; ++r) tail += col[r] * col[r];
+        double tau, beta, v[RR];
+        if (tail <= DBL_MIN) {
+            tau = 0;
+            beta = c0;
+#pragma unroll
+            for (int r = k + 1; r < RR; ++r) v[r] = 0;
+        } else {
+            beta = sqrt(c0 * c0 + tail);
+            if (c0 >= 0) beta = -beta;
+#pragma unroll
+            for (int r = k + 1; r < RR; ++r) v[r] = col[r] / (c0 - beta);
+            tau = (beta - c0) / beta;
+        }
+        hc[k] = tau;
+        if (lane == k) {
+            a[k] = beta;
+#pragma unroll
+            for (int r = k + 1; r < RR; ++r) a[r] = v[r];
+        }
+        if (fabs(beta) > maxpivot) maxpivot = fabs(beta);
+        if (lane > k && lane < C) {
+            if (tau != 0) {
+                double tmp = a[k];
+#pragma unroll
+                for (int r = k + 1; r < RR; ++r) tmp += v[r] * a[r];
+                a[k] -= tau * tmp;
+#pragma unroll
+                for (int r = k + 1; r < RR; ++r) a[r] -= tau * v[r] * tmp;
+            }
+            if (nu != 0) {
+                double temp = fabs(a[k]) / nu;
+                temp = (1 + temp) * (1 - temp);
+                temp = temp < 0 ? 0 : temp;
+                const double r2 = nu / nd;
+                const double temp2 = temp * r2 * r2;
+                if (temp2 <= ndt) {
+                    double sq = 0;
+#pragma unroll
+                    for (int r = k + 1; r < RR; ++r) sq += a[r] * a[r];
+                    nd = nu = sqrt(sq);
+                } else {
+                    nu *= sqrt(temp);
+                }
+            }
+        }
+    }
+    // the factor's first S columns and the permutation, on every lane; the one-lane solve from here
+    double A[RR][S];
+    int pm[S];
+#pragma unroll
+    for (int c = 0; c < S; ++c) {
+#pragma unroll
+        for (int r = 0; r < RR; ++r) A[r][c] = readlane_f64(a[r], c);
+        pm[c] = __builtin_amdgcn_readlane(perm, c);
+    }
+    const double thr = eps * (double)S;
+    int nz = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) nz += (i < nonzero && fabs(A[i][i]) > thr * maxpivot) ? 1 : 0;
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = 0;
+    if (nz == 0) return;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        if (k < nz) {
+            const double tau = hc[k];
+            if (RR - k == 1) {
+                b[k] *= 1 - tau;
+            } else if (tau != 0) {
+                double tmp = b[k];
+#pragma unroll
+                for (int r = k + 1; r < RR; ++r) tmp += A[r][k] * b[r];
+                b[k] -= tau * tmp;
+#pragma unroll
+                for (int r = k + 1; r < RR; ++r) b[r] -= tau * A[r][k] * tmp;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = S - 1; i >= 0; --i) {
+        if (i < nz) {
+            double sacc = b[i];
+#pragma unroll
+            for (int j = i + 1; j < S; ++j)
+                if (j < nz) sacc -= A[i][j] * b[j];
+            b[i] = sacc / A[i][i];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        double val = 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+            if (i < nz && pm[i] == c) val = b[i];
+        x[c] = val;
+    }
+}
+
 // Hypothesis h of the current chunk, by one block: its draw (the FPS start) from the committed
 // rand() state, FPS(3), the 3×6 QR, Δ, its inlier count.
 template <int NT>
@@ -639,6 +802,38 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
     argmax_pair<NT>(bv, bi, sv, si);
     RSTAMP(1);
     const int f2 = bi;
+#if IMLS_QR_WAVE
+    if (threadIdx.x < 64) {                   // wave 0: lane c builds column c of the 3×6 system
+        const int id[3] = {f0, f1, f2};
+        const int lane = threadIdx.x, cc = lane < 6 ? lane : 0;
+        double a[3], b[3], x[6];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int k = id[r];
+            const double s0 = S[3 * k], s1 = S[3 * k + 1], s2 = S[3 * k + 2];
+            const double d0 = Dp[3 * k], d1 = Dp[3 * k + 1], d2 = Dp[3 * k + 2];
+            const double n0 = Np[3 * k], n1 = Np[3 * k + 1], n2 = Np[3 * k + 2];
+            const double col[6] = {n2 * s1 - n1 * s2, n0 * s2 - n2 * s0, n1 * s0 - n0 * s1, n0, n1, n2};
+            double v = col[0];
+#pragma unroll
+            for (int c = 1; c < 6; ++c) v = cc == c ? col[c] : v;
+            a[r] = v;
+            double bb = n0 * (d0 - s0);
+            bb = bb + n1 * (d1 - s1);
+            bb = bb + n2 * (d2 - s2);
+            b[r] = bb;
+        }
+        colpiv_qr3_wave(a, b, x);
+        RSTAMP(2);
+        if (lane == 0) {
+            double D[16];
+            delta_from_x(x, D);
+            RSTAMP(3);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) T[k] = D[k];
+        }
+    }
+#else
     if (threadIdx.x == 0) {
         const int id[3] = {f0, f1, f2};
         double A[3][6], b[3], x[6], D[16];
@@ -664,6 +859,7 @@ __device__ __forceinline__ void ransac_hyp_one(const double* __restrict__ S, con
 #pragma unroll
         for (int k = 0; k < 16; ++k) T[k] = D[k];
     }
+#endif
     __syncthreads();
     int c = 0;
     for (int i = threadIdx.x; i < n; i += NT) {
