@@ -78,11 +78,16 @@ struct KParams {
     int tv_k;                 // use_tensor_voting.k (≤ kTvMaxK)
     double tv_sigma, tv_thr;  // use_tensor_voting.sigma, .distance_threshold
     float tv_skin;            // TV ball lists reused while the query moved ≤ skin (m); 0 = every iteration walks the tree
+    int bfs;                  // this launch's packet walks start breadth-first (the first IMLS_BFS_ITERS iterations)
 };
 // the parameters of ICP iteration `it`'s projection launch (packet size of the traversal)
+#ifndef IMLS_BFS_ITERS
+#define IMLS_BFS_ITERS 3
+#endif
 inline KParams kp_at(const KParams& k, int it) {
     KParams r = k;
     r.packet = it >= 0 && it < k.pk_iters ? k.pk_small : 64;
+    r.bfs = it >= 0 && it < IMLS_BFS_ITERS;
     return r;
 }
 constexpr int kTvMaxK = 64;    // tensor-voting kNN size handled on device

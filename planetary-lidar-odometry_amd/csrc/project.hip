@@ -959,6 +959,104 @@ __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restri
     unsigned long long em = __ballot(active && !skip);   // lanes whose bound admits the current node's box
     const unsigned long long skipped = __ballot(skip);
     if (nbr_stats && lane == 0 && skipped) atomicAdd(&nbr_stats[kStatSkipped], (unsigned long long)__popcll(skipped));
+    if constexpr (MODE == 3) {
+        // Breadth-first top of the walk (round 6, the first ICP iterations, whose waves walk ~55 dependent
+        // node / leaf steps): the upper levels are expanded a whole level-step at a time — one lane per
+        // frontier node, its 2^sw children tested against the packet's box (the union of the lanes'
+        // search balls, a superset of every lane's own test) — while the frontier plus the depth-first
+        // pushes still to come below it fit the wave's stack; the frontier then becomes that stack
+        // (Morton order on top) and the depth-first walk continues from it, every entry re-checked
+        // against the lanes' shrinking bounds at its pop.  Exact either way: nothing a lane's ball
+        // reaches is dropped (the box is inflated past fp32 rounding), and k_finish certifies each list.
+        if (em) {
+            const bool walk = active && !skip;
+            const float rr = walk ? sqrtf(bnd * kBoxSlack) * (1.0f + 1e-5f) + 1e-5f : 0.f;
+            float plo[3], phi[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                plo[a] = walk ? xf[a] - rr : kInfF;
+                phi[a] = walk ? xf[a] + rr : -kInfF;
+            }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    plo[a] = fminf(plo[a], __shfl_xor(plo[a], o, 64));
+                    phi[a] = fmaxf(phi[a], __shfl_xor(phi[a], o, 64));
+                }
+            int fc = 1, lev = 0;
+            if (lane == 0) snode[wv][0] = 1;
+            while (lev < t.levels) {
+                const int sw = min(kWide, t.levels - lev), nk = 1 << sw;
+                const int below = t.levels - lev - sw;
+                const int reserve = (kWideMax - 1) * ((below + kWide - 1) / kWide);
+                const int n = lane < fc ? snode[wv][lane] : 0;
+                const float4* rec = t.nodes + 3 * ((size_t)(n > 0 ? n : 1) << (sw - 1));
+                auto child_box = [&](int k, float (&lo)[3], float (&hi)[3]) {
+                    const float4 ra = rec[3 * (k >> 1)], rb = rec[3 * (k >> 1) + 1], rc = rec[3 * (k >> 1) + 2];
+                    if (k & 1) { lo[0] = rb.z; lo[1] = rb.w; lo[2] = rc.x; hi[0] = rc.y; hi[1] = rc.z; hi[2] = rc.w; }
+                    else { lo[0] = ra.x; lo[1] = ra.y; lo[2] = ra.z; hi[0] = ra.w; hi[1] = rb.x; hi[2] = rb.y; }
+                };
+                unsigned cm = 0u;
+                if (lane < fc) {
+#pragma unroll
+                    for (int k = 0; k < kWideMax; ++k) {
+                        if (k >= nk) break;
+                        float lo[3], hi[3];
+                        child_box(k, lo, hi);
+                        const bool ov = lo[0] <= phi[0] && hi[0] >= plo[0] && lo[1] <= phi[1] && hi[1] >= plo[1] &&
+                                        lo[2] <= phi[2] && hi[2] >= plo[2];
+                        cm |= ov ? (1u << k) : 0u;
+                    }
+                }
+                // exclusive prefix of the lanes' child counts (the next frontier keeps Morton order)
+                const int cnt = __popc(cm);
+                int inc = cnt;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_up(inc, o, 64);
+                    if (lane >= o) inc += v;
+                }
+                const int total = __shfl(inc, 63, 64);
+                if (total == 0 || total + reserve > kWaveStack) break;
+                int off = inc - cnt;
+                if (cm) {
+#pragma unroll
+                    for (int k = 0; k < kWideMax; ++k) {
+                        if (!((cm >> k) & 1u)) continue;
+                        float lo[3], hi[3];
+                        child_box(k, lo, hi);
+                        snode[wv][off] = (n << sw) + k;
+                        sboxa[wv][off] = make_float4(lo[0], lo[1], lo[2], hi[0]);
+                        sboxb[wv][off] = make_float2(hi[1], hi[2]);
+                        ++off;
+                    }
+                }
+                fc = total;
+                lev += sw;
+                ++n_inner;
+            }
+            if (lev > 0) {
+                // the frontier becomes the depth-first stack, its Morton-first entry on top
+                int en = 0;
+                float4 ea = make_float4(0.f, 0.f, 0.f, 0.f);
+                float2 eb = make_float2(0.f, 0.f);
+                if (lane < fc) { en = snode[wv][lane]; ea = sboxa[wv][lane]; eb = sboxb[wv][lane]; }
+                if (lane < fc) { snode[wv][fc - 1 - lane] = en; sboxa[wv][fc - 1 - lane] = ea; sboxb[wv][fc - 1 - lane] = eb; }
+                sp = fc;
+                node = 0;
+                while (sp > 0) {
+                    --sp;
+                    const float4 b0 = sboxa[wv][sp];
+                    const float2 b1 = sboxb[wv][sp];
+                    const float d = box_d2(xf, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y);
+                    em = __ballot(d <= bnd * kBoxSlack);
+                    if (em) { node = snode[wv][sp]; break; }
+                }
+                if (!node) em = 0ull;
+            }
+        }
+    }
     while (em) {
         if (node < P) {
             // one step descends `sw` binary levels at once: the 2^sw descendants' boxes sit in
@@ -2503,6 +2601,16 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave(
                       (int)blockIdx.x);
 }
 
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_bfs(
+        TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
+        const double* __restrict__ pose, const int* __restrict__ done, KParams kp, const double* __restrict__ delta,
+        int* __restrict__ lists, float* __restrict__ wlist, float4* __restrict__ xref, float* __restrict__ nref,
+        int use_prev, unsigned long long* __restrict__ nbr_stats) {
+    knn_wave_body<KL, 3>(t, spt, qperm, N, pose, done, kp, delta, lists, wlist, xref, nref, use_prev, nbr_stats,
+                         (int)blockIdx.x);
+}
+
 template <int KL, int MODE>
 __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_m(
         TreeView t, const float4* __restrict__ spt, const unsigned* __restrict__ qperm, int N,
@@ -2616,6 +2724,19 @@ __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_b(const P
                                 bx);
 }
 
+template <int KL>
+__global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_bfsb(const PairDev* __restrict__ tab, KParams kp,
+                                                                             int use_prev, int npairs) {
+    int f, bx;
+    batch_block(kp.xcd, f, bx);
+    if (f >= npairs) return;
+    const PairDev A = device_view(tab + f);
+    if (use_qwave(kp, A.N) || bx >= knn_blocks_of(A.N, kp.packet)) return;
+    float4* xref = xref_dev(A.lists, A.N);
+    knn_wave_body<KL, 3>(A.t, A.spt, A.qperm, A.N, A.st.pose, A.st.done, kp, A.st.delta, A.lists,
+                         wlist_of<KL>(A.lists, A.N), xref, reinterpret_cast<float*>(xref + A.N), use_prev, A.stats, bx);
+}
+
 template <int KL, int MODE>
 __global__ __launch_bounds__(kWaveBlock) IMLS_KNN_ATTR void k_knn_wave_mb(const PairDev* __restrict__ tab, KParams kp,
                                                                            int npairs) {
@@ -2679,7 +2800,9 @@ void launch_wave_batch(hipStream_t s, const PairDev* tab, int npairs, int maxN, 
     }
     if (any_large) {
         const int kb = knn_blocks_of(maxN, kp.packet);
-        if (use_prev && IMLS_COMPACT) {
+        if (it < IMLS_BFS_ITERS) {
+            k_knn_wave_bfsb<KL><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, use_prev, npairs);
+        } else if (use_prev && IMLS_COMPACT) {
             k_knn_wave_mb<KL, 1><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, npairs);
             k_knn_wave_mb<KL, 2><<<dim3(kb, gy), kWaveBlock, 0, s>>>(tab, kp, npairs);
         } else {
@@ -2728,6 +2851,9 @@ void launch_wave(hipStream_t s, int blocks, const TreeView& t, const float4* spt
     else if (use_qwave(kp, N))
         k_knn_qwave<KL><<<(N + kWaveBlock / 64 - 1) / (kWaveBlock / 64), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp,
                                                                                           delta, lists, wlist, xref, nref, use_prev, stats);
+    else if (kp.bfs && IMLS_BFS_ITERS > 0)
+        k_knn_wave_bfs<KL><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists,
+                                                                              wlist, xref, nref, use_prev, stats);
     else if (use_prev && IMLS_COMPACT) {
         // later iterations: reuse decided per lane, then packets of the compacted re-traversing slots
         k_knn_wave_m<KL, 1><<<knn_blocks_of(N, kp.packet), kWaveBlock, 0, s>>>(t, spt, qperm, N, pose, done, kp, delta, lists,
