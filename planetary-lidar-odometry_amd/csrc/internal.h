@@ -82,7 +82,7 @@ struct KParams {
 };
 // the parameters of ICP iteration `it`'s projection launch (packet size of the traversal)
 #ifndef IMLS_BFS_ITERS
-#define IMLS_BFS_ITERS 3
+#define IMLS_BFS_ITERS 0   // breadth-first top levels: measured slower (profiles/r06_bfs_rejected/), off
 #endif
 inline KParams kp_at(const KParams& k, int it) {
     KParams r = k;
