@@ -344,6 +344,146 @@ int filter_batch(hipStream_t s, const std::vector<FilterJob>& jobs, DevBuf& scra
 
 namespace {
 
+// ---------------------------------------------------------------------------------------------
+// Stable (key, index) pair sort for the index builds' ≤ 256k-point sorts (round 6: the source's and a
+// FIFO run's Morton order — hipcub's radix sort runs a merge sort there, ~14 launches and ~100 µs per
+// 126k keys with their gaps).  The values are the input positions (k_morton / k_morton_fq), so
+// ordering the distinct (key, value) pairs is the stable radix sort's order, bit for bit.
+//   k_tile_sort: 4096-pair tiles bitonic-sorted in LDS by 512 threads;
+//   k_merge_pass: sorted runs of w merged pairwise, 2048 outputs per block — the block's two
+//   merge-path splits by a 128-ary search (128 threads per diagonal, 3 rounds for runs ≤ 2M), both
+//   input segments staged in LDS, each thread's 8 outputs merged sequentially.
+// ---------------------------------------------------------------------------------------------
+constexpr int kSortTile = 4096;
+constexpr int kSortTileThreads = 512;
+#ifndef IMLS_SMALL_SORT
+#define IMLS_SMALL_SORT 1
+#endif
+constexpr int kSortSmallMax = IMLS_SMALL_SORT ? 1 << 18 : 0;
+constexpr int kMergeOut = 2048;
+constexpr int kMergeOutPer = kMergeOut / kBlock;
+
+__device__ __forceinline__ bool pair_less(unsigned long long ka, unsigned va, unsigned long long kb, unsigned vb) {
+    return ka < kb || (ka == kb && va < vb);
+}
+
+__global__ __launch_bounds__(kSortTileThreads) void k_tile_sort(const unsigned long long* __restrict__ key,
+                                                               const unsigned* __restrict__ val, int n,
+                                                               unsigned long long* __restrict__ okey,
+                                                               unsigned* __restrict__ oval) {
+    __shared__ unsigned long long sk[kSortTile];
+    __shared__ unsigned sv[kSortTile];
+    const int base = blockIdx.x * kSortTile;
+    for (int e = threadIdx.x; e < kSortTile; e += kSortTileThreads) {
+        const int g = base + e;
+        sk[e] = g < n ? key[g] : ~0ull;     // padding sorts last (keys are < 2^48)
+        sv[e] = g < n ? val[g] : ~0u;
+    }
+    for (int size = 2; size <= kSortTile; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (int e = threadIdx.x; e < kSortTile / 2; e += kSortTileThreads) {
+                const int i = ((e & ~(stride - 1)) << 1) | (e & (stride - 1)), j = i + stride;
+                const bool up = (i & size) == 0;
+                const unsigned long long ki = sk[i], kj = sk[j];
+                const unsigned vi = sv[i], vj = sv[j];
+                if (pair_less(kj, vj, ki, vi) == up) { sk[i] = kj; sk[j] = ki; sv[i] = vj; sv[j] = vi; }
+            }
+        }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kSortTile; e += kSortTileThreads) {
+        const int g = base + e;
+        if (g < n) { okey[g] = sk[e]; oval[g] = sv[e]; }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_merge_pass(const unsigned long long* __restrict__ key,
+                                                       const unsigned* __restrict__ val, int n, int w,
+                                                       unsigned long long* __restrict__ okey,
+                                                       unsigned* __restrict__ oval) {
+    __shared__ unsigned long long sk[kMergeOut];
+    __shared__ unsigned sv[kMergeOut];
+    __shared__ int scnt[2][kBlock / 64];
+    __shared__ int ssplit[2];
+    const long long o0 = (long long)blockIdx.x * kMergeOut;
+    if (o0 >= n) return;                                   // block-uniform
+    const long long o1 = std::min(o0 + kMergeOut, (long long)n);
+    const long long ps = o0 / (2ll * w) * (2ll * w);       // the pair of runs holding this block's outputs
+    const int na = (int)std::min((long long)w, n - ps);
+    const int nb = (int)std::max(0ll, std::min((long long)w, n - ps - w));
+    const unsigned long long* ak = key + ps;
+    const unsigned* av = val + ps;
+    const unsigned long long* bk = key + ps + na;
+    const unsigned* bv = val + ps + na;
+    // the splits of the block's two diagonals: A's entries among the first d outputs, P(a) = A[a] < B[d−1−a]
+    // holds exactly below the split; 128 samples per round narrow [lo, hi] below ⌈span / 128⌉
+    const int g = threadIdx.x >> 7, lt = threadIdx.x & 127, wv = threadIdx.x >> 6;
+    const long long d = g ? o1 - ps : o0 - ps;
+    int lo = (int)std::max(0ll, d - nb), hi = (int)std::min(d, (long long)na);
+#pragma unroll
+    for (int round = 0; round < 3; ++round) {
+        const int span = hi - lo;
+        const int step = (span + 127) / 128;
+        const int pos = lo + lt * step;
+        const bool smp = span > 0 && pos < hi;
+        const bool pt = smp && pair_less(ak[pos], av[pos], bk[d - 1 - pos], bv[d - 1 - pos]);
+        const unsigned long long bt = __ballot(pt), bs = __ballot(smp);
+        if ((threadIdx.x & 63) == 0) { scnt[0][wv] = __popcll(bt); scnt[1][wv] = __popcll(bs); }
+        __syncthreads();
+        const int k = scnt[0][2 * g] + scnt[0][2 * g + 1], ns = scnt[1][2 * g] + scnt[1][2 * g + 1];
+        __syncthreads();
+        if (span > 0) {
+            if (k == 0) {
+                hi = lo;
+            } else {
+                const int last = lo + (k - 1) * step;
+                hi = k < ns ? lo + k * step : hi;
+                lo = last + 1;
+            }
+        }
+    }
+    if (lt == 0) ssplit[g] = lo;
+    __syncthreads();
+    const int i0 = ssplit[0], i1 = ssplit[1];
+    const int j0 = (int)(o0 - ps - i0), j1 = (int)(o1 - ps - i1);
+    const int la = i1 - i0, lb = j1 - j0;
+    for (int e = threadIdx.x; e < la; e += kBlock) { sk[e] = ak[i0 + e]; sv[e] = av[i0 + e]; }
+    for (int e = threadIdx.x; e < lb; e += kBlock) { sk[la + e] = bk[j0 + e]; sv[la + e] = bv[j0 + e]; }
+    __syncthreads();
+    const int q = threadIdx.x * kMergeOutPer, m = la + lb;
+    if (q >= m) return;
+    int x0 = std::max(0, q - lb), x1 = std::min(q, la);
+    while (x0 < x1) {
+        const int mid = (x0 + x1) >> 1;
+        if (pair_less(sk[mid], sv[mid], sk[la + q - 1 - mid], sv[la + q - 1 - mid])) x0 = mid + 1;
+        else x1 = mid;
+    }
+    int x = x0, y = q - x0;
+    const int qe = std::min(q + kMergeOutPer, m);
+    for (int r = q; r < qe; ++r) {
+        const bool takeA = y >= lb || (x < la && pair_less(sk[x], sv[x], sk[la + y], sv[la + y]));
+        const int src = takeA ? x : la + y;
+        okey[o0 + r] = sk[src];
+        oval[o0 + r] = sv[src];
+        x += takeA ? 1 : 0;
+        y += takeA ? 0 : 1;
+    }
+}
+
+// The pairs of (k0, v0) sorted; returns 1 when the result is in (k1, v1), 0 when in (k0, v0).
+int small_sort_pairs(hipStream_t s, unsigned long long* k0, unsigned* v0, unsigned long long* k1, unsigned* v1, int n) {
+    const int tiles = (n + kSortTile - 1) / kSortTile;
+    k_tile_sort<<<tiles, kSortTileThreads, 0, s>>>(k0, v0, n, k1, v1);
+    int cur = 1;
+    const int blocks = (n + kMergeOut - 1) / kMergeOut;
+    for (long long w = kSortTile; w < n; w *= 2) {
+        if (cur) k_merge_pass<<<blocks, kBlock, 0, s>>>(k1, v1, n, (int)w, k0, v0);
+        else k_merge_pass<<<blocks, kBlock, 0, s>>>(k0, v0, n, (int)w, k1, v1);
+        cur ^= 1;
+    }
+    return cur;
+}
+
 // The sort orders the full 48-bit Morton codes.  Sorting their top 32 bits only (two radix passes
 // fewer, the lone frame's index build ~15 µs shorter) coarsens the order inside 1/1625-extent cells:
 // config B's leaves and packets lose coherence, 423.7 → 397.5 pairs/s (round 4, profiles/r04_final3)
@@ -383,14 +523,24 @@ int morton_perm(hipStream_t s, const float4* pts, int n, DevBuf& scratch, DevBuf
     k_bbox_partial<<<nb, kBlock, 0, s>>>(pts, n, bbpart);
     k_bbox_final<<<1, kBlock, 0, s>>>(bbpart, nb, bbox, qp);
     k_morton<<<grid_for(n), kBlock, 0, s>>>(pts, n, qp, k0, v0);
-    hipcub::DoubleBuffer<unsigned long long> kb(k0, k1);
-    hipcub::DoubleBuffer<unsigned> vb(v0, (unsigned*)perm.p);
-    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, kb, vb, n, kMortonSortLo, 48, s);
-    if (lkeys) k_leaf_keys<<<grid_for(L), kBlock, 0, s>>>(kb.Current(), n, B, (unsigned long long*)lkeys->p);
+    unsigned long long* kcur;
+    unsigned* vcur;
+    if (n <= kSortSmallMax && kMortonSortLo == 0) {
+        const int r = small_sort_pairs(s, k0, v0, k1, (unsigned*)perm.p, n);
+        kcur = r ? k1 : k0;
+        vcur = r ? (unsigned*)perm.p : v0;
+    } else {
+        hipcub::DoubleBuffer<unsigned long long> kb(k0, k1);
+        hipcub::DoubleBuffer<unsigned> vb(v0, (unsigned*)perm.p);
+        hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, kb, vb, n, kMortonSortLo, 48, s);
+        kcur = kb.Current();
+        vcur = vb.Current();
+    }
+    if (lkeys) k_leaf_keys<<<grid_for(L), kBlock, 0, s>>>(kcur, n, B, (unsigned long long*)lkeys->p);
     if (perm_out) {
-        *perm_out = vb.Current();
-    } else if (vb.Current() != (unsigned*)perm.p) {
-        (void)hipMemcpyAsync(perm.p, vb.Current(), (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+        *perm_out = vcur;
+    } else if (vcur != (unsigned*)perm.p) {
+        (void)hipMemcpyAsync(perm.p, vcur, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
     }
     if (hipGetLastError() != hipSuccess) { err = "morton sort launch failed"; return IMLS_ERR_DEVICE; }
     return IMLS_OK;
@@ -1141,10 +1291,20 @@ int fifo_run_build(hipStream_t s, const float4* fpt, const float4* fnr, int n, c
     unsigned* v1 = carve<unsigned>(p, n);
     void* cub_tmp = carve<char>(p, cub_bytes);
     k_morton_fq<<<grid_for(n), kBlock, 0, s>>>(fpt, n, fq, k0, v0, clamp);
-    hipcub::DoubleBuffer<unsigned long long> kb(k0, k1);
-    hipcub::DoubleBuffer<unsigned> vb(v0, v1);
-    hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, kb, vb, n, 0, 48, s);
-    k_run_gather<<<grid_for(n), kBlock, 0, s>>>(fpt, fnr, vb.Current(), kb.Current(), n, fifo_run_pts(run.p, n),
+    unsigned long long* kcur;
+    unsigned* vcur;
+    if (n <= kSortSmallMax) {
+        const int r = small_sort_pairs(s, k0, v0, k1, v1, n);
+        kcur = r ? k1 : k0;
+        vcur = r ? v1 : v0;
+    } else {
+        hipcub::DoubleBuffer<unsigned long long> kb(k0, k1);
+        hipcub::DoubleBuffer<unsigned> vb(v0, v1);
+        hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, kb, vb, n, 0, 48, s);
+        kcur = kb.Current();
+        vcur = vb.Current();
+    }
+    k_run_gather<<<grid_for(n), kBlock, 0, s>>>(fpt, fnr, vcur, kcur, n, fifo_run_pts(run.p, n),
                                                 fifo_run_nrm(run.p, n), fifo_run_keys(run.p, n));
     if (hipGetLastError() != hipSuccess) { err = "FIFO run build launch failed"; return IMLS_ERR_DEVICE; }
     return IMLS_OK;
