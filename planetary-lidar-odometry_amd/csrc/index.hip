@@ -356,8 +356,10 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 constexpr int kSortTile = 4096;
 constexpr int kSortTileThreads = 512;
+// measured slower than hipcub's merge sort (k_tile_sort 61.7 µs + 5 merge passes of 9.8 µs per 126k keys;
+// FIFO index 0.218-0.221 vs 0.170-0.188 ms per registration, profiles/r06_sort_rejected/): off
 #ifndef IMLS_SMALL_SORT
-#define IMLS_SMALL_SORT 1
+#define IMLS_SMALL_SORT 0
 #endif
 constexpr int kSortSmallMax = IMLS_SMALL_SORT ? 1 << 18 : 0;
 constexpr int kMergeOut = 2048;
