@@ -527,8 +527,12 @@ __device__ __forceinline__ float need_key_ids(const float (&lk)[KL], float r2, i
 //      queries that really re-traverse, from the block's 4·64 Morton-consecutive slots (instead of
 //      every packet walking for the few of its lanes that do).  The lane redoes MODE 1's decision
 //      (same inputs, same outcome), its prefill included.
+//   3  the first ICP iterations' walk with a breadth-first top (k_knn_wave_bfs[b], IMLS_BFS_ITERS):
+//      the upper levels expanded against the packet's box, the frontier handed to the depth-first
+//      stack.  Measured slower (profiles/r06_bfs_rejected/): off by default, kept for A/B builds.
 // (A first version compacted through one atomic counter per frame: packets of runs from anywhere in
-// the frame walked 2-6× longer — profiles/r06_compact_rejected/.)
+// the frame walked 2-6× longer — profiles/r06_compact_rejected/.  Modes 1 and 2 are off as well:
+// IMLS_COMPACT.)
 template <int KL, int MODE = 0>
 __device__ __forceinline__ void knn_wave_body(TreeView t, const float4* __restrict__ spt,
                                                          const unsigned* __restrict__ qperm, int N,
