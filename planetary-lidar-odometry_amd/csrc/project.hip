@@ -86,7 +86,10 @@ constexpr float kReseed = 0.25f;    // temporal seed unless displacement² > kRe
 #define IMLS_BC_GROUP 4
 #endif
 __attribute__((unused)) constexpr int kBcGroup = IMLS_BC_GROUP;          // broadcast leaf scan: points per scalar-load group (IMLS_BCAST_SCALAR)
-constexpr int kSparseLanes = 32;    // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
+#ifndef IMLS_SPARSE_LANES
+#define IMLS_SPARSE_LANES 20
+#endif
+constexpr int kSparseLanes = IMLS_SPARSE_LANES;    // a leaf wanted by ≤ this many lanes is scanned per lane, not per point
 constexpr int kWide = 3;            // binary levels descended per traversal step (8 boxes per step)
 constexpr float kBoxSlack = 1.0f + 2e-6f;     // fp32 box / point distance vs exact: ≤ 3.1e-7 rel.
 // Round 6: the traversals search radius (1 + skin)·r, not r.  A query with fewer than K map points
