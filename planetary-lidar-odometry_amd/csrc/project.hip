@@ -520,7 +520,10 @@ __device__ __forceinline__ float need_key_ids(const float (&lk)[KL], float r2, i
 
 // Slot-id keys in registers, positions in LDS: ~96 VGPRs and ~29 KB of LDS per 4-wave block — 5
 // waves/SIMD (round 4: the register list needed 160 VGPRs, 3 waves/SIMD; config B 331 → 406 pairs/s)
-#define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 26 ? 5 : 2)))
+#ifndef IMLS_KNN_WAVES
+#define IMLS_KNN_WAVES 5
+#endif
+#define IMLS_KNN_ATTR __attribute__((amdgpu_waves_per_eu(KL <= 26 ? IMLS_KNN_WAVES : 2)))
 // MODE (round 6, the later ICP iterations of the packet traversal, use_prev):
 //   0  one pass — every lane decides reuse and the packets walk for the lanes that cannot reuse;
 //   1  the reuse decision only (Verlet skip, prefill certificate): a reused list is settled here,
